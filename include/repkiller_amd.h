@@ -1,0 +1,148 @@
+/* repkiller_amd.h -- C ABI of the MI355X-native repeat-fragment classifier.
+ *
+ * Drop-in boundary for the hot path of estebanpw/repkiller v0.9.b.  The
+ * reference has no FFI; its hot path is three in-process C++ calls made by
+ * execWithParams (/root/reference/src/repkiller.cpp:80-97):
+ *
+ *   generate_fragment_groups(db, FGList&, seq_mgr, len_ratio, pos_ratio)
+ *                                            commonFunctions.h:35 / .cpp:41-80
+ *   generate_diagonal_func(db, size_t *diag)  commonFunctions.h:59 / .cpp:161-177
+ *   sort_groups(FGList&, const size_t *diag)  commonFunctions.h:57 / .cpp:148-159
+ *
+ * plus the repeat flag chosen when a group is saved
+ * (save_frags_from_group, commonFunctions.cpp:106-115).  rk_classify() replaces
+ * all four: it takes the fragments as plain SoA arrays and returns, per input
+ * row, the group id (the `block` column the reference writes, creation order)
+ * and the repeat flag, plus the exact row order of the reference's output.
+ * Ingress (FragmentsDatabase, FragmentsDatabase.cpp:17-101) and egress
+ * (save_all_frag_pairs / SaverQueue, commonFunctions.cpp:101-146,
+ * SaverQueue.cpp:4-51) are provided host-side by rk_db_* / rk_saver_*.
+ *
+ * Conventions: every function returns 0 (RK_OK) or a negative rk_status; no
+ * exception crosses the ABI; all buffers are caller-owned; one rk_ctx per
+ * host thread (the reference runs up to 3 concurrent pairs, repkiller.cpp:60-72,
+ * each with private state -- contexts mirror that).  There is NO CPU fallback:
+ * rk_create fails with RK_E_NODEVICE when no gfx950 device is usable.
+ */
+#ifndef REPKILLER_AMD_H
+#define REPKILLER_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  RK_OK = 0,
+  RK_E_ARG = -1,
+  RK_E_IO = -2,          /* cannot open/read/write a file (reference: runtime_error) */
+  RK_E_COUNT = -3,       /* more Frag lines than the header total (FragmentsDatabase.cpp:99) */
+  RK_E_UB_BUCKET = -4,   /* xStart/10 >= vsize: the reference writes out of bounds (:96-97) */
+  RK_E_UB_CENTER = -5,   /* a probe would index past an occupancy array
+                            (SequenceOcupationList.cpp:17, :80 size_t wrap) */
+  RK_E_NOMEM = -6,
+  RK_E_HIP = -7,         /* a HIP runtime call failed; see rk_last_error */
+  RK_E_NODEVICE = -8,    /* no usable gfx950 device */
+  RK_E_TOO_MANY = -9,    /* n >= 2^32 - 1 (32-bit row ids) */
+  RK_E_INTERNAL = -10,   /* a device-side consistency check failed */
+} rk_status;
+
+/* ---- classification (the hot path) ----------------------------------- */
+
+typedef struct rk_ctx rk_ctx;
+
+/* Fragments in FILE order, exactly the fields the hot path reads
+ * (FragFile xStart/yStart/length/strand, structs.h:18-48). */
+typedef struct {
+  const uint64_t *x_start;
+  const uint64_t *y_start;
+  const uint64_t *length;
+  const uint8_t *strand; /* 'f' = forward lists, anything else = reverse lists */
+  uint64_t n;
+} rk_frags_soa;
+
+typedef struct {
+  uint64_t len_x_hdr; /* raw "SeqX length" header value; +1 applied inside (FragmentsDatabase.cpp:62) */
+  uint64_t len_y_hdr; /* raw "SeqY length" header value (FragmentsDatabase.cpp:65) */
+  double len_ratio;   /* > 0 (commonFunctions.cpp:26) */
+  double pos_ratio;   /* > 0 (commonFunctions.cpp:27) */
+} rk_params;
+
+typedef struct {
+  uint32_t *gid;       /* [n] group id per input row; UINT32_MAX = row in the dropped last bucket */
+  uint8_t *repval;     /* [n] 0 singleton / 1 representative / 2 repeated; 0xFF = dropped */
+  uint32_t *out_order; /* [n] input rows in the reference's output order; first n_out valid */
+  uint64_t n_out;      /* set by rk_classify*: rows written (= rows grouped) */
+  uint64_t n_groups;   /* set by rk_classify*: groups created */
+} rk_result;
+
+/* Per-call counters of the last rk_classify* on a context. */
+typedef struct {
+  uint64_t n_in, n_proc, n_groups;
+  uint32_t x_sweeps, y_sweeps, jump_rounds;
+  uint64_t x_hits, y_hits;
+  double device_ms; /* HIP-event time of the whole device pipeline */
+} rk_stats;
+
+int rk_create(rk_ctx **ctx, int device);
+void rk_destroy(rk_ctx *ctx);
+const char *rk_last_error(const rk_ctx *ctx);
+
+/* Host buffers in and out (H2D, device pipeline, D2H); blocking. */
+int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p, rk_result *out);
+
+/* Device buffers in and out (hipMalloc'd); runs on the context's stream and
+ * returns when the result is complete (n_out / n_groups are host values). */
+int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params *p,
+                       rk_result *out_dev);
+
+int rk_get_stats(const rk_ctx *ctx, rk_stats *st);
+
+/* ---- host ingress: FragmentsDatabase (FragmentsDatabase.cpp:17-101) ---- */
+
+typedef struct rk_db rk_db;
+
+/* Parse a GECKO-style CSV with the reference's acceptance rules.  Returns
+ * RK_E_IO if unreadable, RK_E_COUNT if more Frag lines than the header total. */
+int rk_db_load_csv(const char *path, rk_db **db);
+void rk_db_free(rk_db *db);
+/* Borrow the SoA view (valid until rk_db_free) and header values. */
+int rk_db_view(const rk_db *db, rk_frags_soa *soa, uint64_t *len_x_hdr, uint64_t *len_y_hdr,
+               uint64_t *total_hdr);
+
+/* ---- host egress: save_all_frag_pairs + SaverQueue ------------------- */
+
+/* Write the reference's output CSV (commonFunctions.cpp:101-146). */
+int rk_db_write_csv(const rk_db *db, const char *path, const rk_result *res);
+
+/* SaverQueue (SaverQueue.h:37-41): background writer thread.  add() takes
+ * ownership of copies of the result arrays; on open failure the request is
+ * written to represults-<k>.csv instead (SaverQueue.cpp:16-20). */
+typedef struct rk_saver rk_saver;
+int rk_saver_start(const rk_db *db, rk_saver **sq);
+int rk_saver_add(rk_saver *sq, const char *path, const rk_result *res, uint64_t n);
+int rk_saver_stop(rk_saver *sq); /* drains the queue, joins, frees */
+
+/* ---- synthetic inputs --------------------------------- */
+
+typedef struct {
+  uint64_t n;          /* fragments */
+  uint64_t genome_len; /* L: both sequences */
+  uint64_t seed;
+  double family_frac;  /* share of repeat-family fragments (0.8 default, 0.95 repeat-rich) */
+  uint32_t copies_lo;  /* copies per family ~ U[lo, hi): 2,30 default; 100,600 repeat-rich */
+  uint32_t copies_hi;
+} rk_synth_params;
+
+int rk_synth_generate(const rk_synth_params *p, uint64_t *x_start, uint64_t *y_start,
+                      uint64_t *length, uint8_t *strand, uint64_t *ident /* nullable */);
+int rk_synth_write_csv(const char *path, uint64_t n, const uint64_t *x_start,
+                       const uint64_t *y_start, const uint64_t *length, const uint8_t *strand,
+                       const uint64_t *ident /* nullable */, uint64_t len_x_hdr,
+                       uint64_t len_y_hdr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,346 @@
+"""repkiller_amd -- MI355X-native repeat-fragment classifier (estebanpw/repkiller hot path).
+
+Python binding over the C ABI in ``include/repkiller_amd.h`` (``librepkiller_amd.so``,
+built in-tree by ``make -C repkiller_amd/csrc``).  The classification runs only
+on a gfx950 GPU through hand-written HIP kernels; there is no CPU fallback --
+:class:`Context` raises if the library or the device is missing.
+
+Mapping to the reference (``/root/reference/src``):
+
+=====================================  ============================================
+reference                              here
+=====================================  ============================================
+``FragmentsDatabase(ifstream&, ...)``  :class:`FragmentsDatabase` (``rk_db_load_csv``)
+``generate_fragment_groups`` +         :meth:`Context.classify` /
+``generate_diagonal_func`` +           :meth:`Context.classify_device`
+``sort_groups`` + repeat flag          (``rk_classify`` / ``rk_classify_device``)
+``save_all_frag_pairs``                :meth:`FragmentsDatabase.save_all_frag_pairs`
+``SaverQueue``                         :class:`SaverQueue` (``rk_saver_*``)
+=====================================  ============================================
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librepkiller_amd.so")
+CLI_PATH = os.path.join(_HERE, "bin", "rk_repkiller")
+
+RK_OK = 0
+STATUS = {
+    0: "RK_OK", -1: "RK_E_ARG", -2: "RK_E_IO", -3: "RK_E_COUNT", -4: "RK_E_UB_BUCKET",
+    -5: "RK_E_UB_CENTER", -6: "RK_E_NOMEM", -7: "RK_E_HIP", -8: "RK_E_NODEVICE",
+    -9: "RK_E_TOO_MANY", -10: "RK_E_INTERNAL",
+}
+
+# every symbol include/repkiller_amd.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "rk_create", "rk_destroy", "rk_last_error", "rk_classify", "rk_classify_device",
+    "rk_get_stats", "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
+    "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
+    "rk_synth_write_csv",
+)
+
+
+class RkError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"{STATUS.get(code, code)}{': ' + msg if msg else ''}")
+
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class FragsSoA(ctypes.Structure):
+    _fields_ = [("x_start", ctypes.c_void_p), ("y_start", ctypes.c_void_p),
+                ("length", ctypes.c_void_p), ("strand", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("len_x_hdr", ctypes.c_uint64), ("len_y_hdr", ctypes.c_uint64),
+                ("len_ratio", ctypes.c_double), ("pos_ratio", ctypes.c_double)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("gid", ctypes.c_void_p), ("repval", ctypes.c_void_p),
+                ("out_order", ctypes.c_void_p), ("n_out", ctypes.c_uint64),
+                ("n_groups", ctypes.c_uint64)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("n_in", ctypes.c_uint64), ("n_proc", ctypes.c_uint64),
+                ("n_groups", ctypes.c_uint64), ("x_sweeps", ctypes.c_uint32),
+                ("y_sweeps", ctypes.c_uint32), ("jump_rounds", ctypes.c_uint32),
+                ("x_hits", ctypes.c_uint64), ("y_hits", ctypes.c_uint64),
+                ("device_ms", ctypes.c_double)]
+
+
+class SynthParams(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("genome_len", ctypes.c_uint64),
+                ("seed", ctypes.c_uint64), ("family_frac", ctypes.c_double),
+                ("copies_lo", ctypes.c_uint32), ("copies_hi", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load librepkiller_amd.so; raise loudly when it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # torch ships its own libamdhip64.so.7; when it is imported AFTER this library
+    # the process ends up with two HIP runtimes and torch.cuda cannot initialise.
+    # Importing it first makes both share one runtime (SONAME match).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: run `make -C repkiller_amd/csrc` "
+                           "(or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    sig = {
+        "rk_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
+        "rk_destroy": (None, [vp]),
+        "rk_last_error": (ctypes.c_char_p, [vp]),
+        "rk_classify": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA), ctypes.POINTER(Params),
+                                       ctypes.POINTER(Result)]),
+        "rk_classify_device": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA),
+                                              ctypes.POINTER(Params), ctypes.POINTER(Result)]),
+        "rk_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(Stats)]),
+        "rk_db_load_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(vp)]),
+        "rk_db_free": (None, [vp]),
+        "rk_db_view": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA), _u64p, _u64p, _u64p]),
+        "rk_db_write_csv": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(Result)]),
+        "rk_saver_start": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+        "rk_saver_add": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(Result),
+                                        ctypes.c_uint64]),
+        "rk_saver_stop": (ctypes.c_int, [vp]),
+        "rk_synth_generate": (ctypes.c_int, [ctypes.POINTER(SynthParams), vp, vp, vp, vp, vp]),
+        "rk_synth_write_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, vp, vp, vp, vp,
+                                              vp, ctypes.c_uint64, ctypes.c_uint64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def _check(rc: int, msg: str = ""):
+    if rc != RK_OK:
+        raise RkError(rc, msg)
+
+
+# --------------------------------------------------------------- synthetic --
+
+@dataclass
+class Frags:
+    """Fragments in FILE order (what FragmentsDatabase reads, SoA)."""
+    x_start: np.ndarray
+    y_start: np.ndarray
+    length: np.ndarray
+    strand: np.ndarray
+    ident: np.ndarray | None = None
+
+    @property
+    def n(self) -> int:
+        return int(self.x_start.shape[0])
+
+
+def synth(n: int, genome_len: int, seed: int, family_frac: float = 0.8,
+          copies: tuple[int, int] = (2, 30)) -> Frags:
+    """Deterministic synthetic fragment set (SURVEY.md §8d generator)."""
+    lib = load_library()
+    f = Frags(np.empty(n, np.uint64), np.empty(n, np.uint64), np.empty(n, np.uint64),
+              np.empty(n, np.uint8), np.empty(n, np.uint64))
+    p = SynthParams(n, genome_len, seed, family_frac, copies[0], copies[1])
+    _check(lib.rk_synth_generate(ctypes.byref(p), _ptr(f.x_start), _ptr(f.y_start),
+                                 _ptr(f.length), _ptr(f.strand), _ptr(f.ident)))
+    return f
+
+
+def write_input_csv(path: str, f: Frags, len_x_hdr: int, len_y_hdr: int) -> None:
+    lib = load_library()
+    ident = f.ident if f.ident is not None else f.length
+    _check(lib.rk_synth_write_csv(path.encode(), f.n, _ptr(f.x_start), _ptr(f.y_start),
+                                  _ptr(f.length), _ptr(f.strand), _ptr(ident),
+                                  len_x_hdr, len_y_hdr))
+
+
+# ------------------------------------------------------------------ ingress --
+
+@dataclass
+class ClassifyResult:
+    gid: np.ndarray        # uint32 per input row; 0xFFFFFFFF = dropped (last xStart/10 bucket)
+    repval: np.ndarray     # uint8 per input row: 0/1/2; 0xFF = dropped
+    out_order: np.ndarray  # uint32 input rows in output order (length n_out)
+    n_groups: int
+
+    def as_struct(self) -> Result:
+        return Result(_ptr(self.gid), _ptr(self.repval), _ptr(self.out_order),
+                      int(self.out_order.shape[0]), self.n_groups)
+
+
+class FragmentsDatabase:
+    """Parsed fragment CSV (FragmentsDatabase.cpp:17-101 acceptance rules)."""
+
+    def __init__(self, path: str):
+        lib = load_library()
+        h = ctypes.c_void_p()
+        rc = lib.rk_db_load_csv(path.encode(), ctypes.byref(h))
+        if rc == -2:
+            raise RkError(rc, f"Could not open input file {path}.")
+        if rc == -3:
+            raise RkError(rc, "Unexpected number of fragments")
+        _check(rc)
+        self._h = h
+        soa = FragsSoA()
+        lx, ly, tot = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib.rk_db_view(h, ctypes.byref(soa), ctypes.byref(lx), ctypes.byref(ly),
+                              ctypes.byref(tot)))
+        self.len_x_hdr, self.len_y_hdr, self.total_hdr = lx.value, ly.value, tot.value
+        n = soa.n
+
+        def view(ptr, dtype, count):
+            if count == 0:
+                return np.empty(0, dtype)
+            buf = (ctypes.c_uint8 * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+            return np.frombuffer(buf, dtype=dtype).copy()
+
+        self.frags = Frags(view(soa.x_start, np.uint64, n), view(soa.y_start, np.uint64, n),
+                           view(soa.length, np.uint64, n), view(soa.strand, np.uint8, n))
+
+    def getTotalFrags(self) -> int:  # FragmentsDatabase.h:32
+        return self.frags.n
+
+    def getA(self) -> int:  # FragmentsDatabase.h:23 (vsize)
+        return 1 + (self.len_x_hdr + 1) // 10
+
+    def save_all_frag_pairs(self, path: str, res: ClassifyResult) -> None:
+        """commonFunctions.cpp:131-146 (header echo + one line per member)."""
+        r = res.as_struct()
+        rc = load_library().rk_db_write_csv(self._h, path.encode(), ctypes.byref(r))
+        if rc == -2:
+            raise RkError(rc, "Could not open output directory " + path)
+        _check(rc)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().rk_db_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SaverQueue:
+    """SaverQueue.h:37-41 -- background CSV writer (start / addRequest / stop)."""
+
+    def __init__(self, db: FragmentsDatabase):
+        self._db = db
+        self._h = ctypes.c_void_p()
+        _check(load_library().rk_saver_start(db._h, ctypes.byref(self._h)))
+
+    def addRequest(self, path: str, res: ClassifyResult) -> None:
+        r = res.as_struct()
+        _check(load_library().rk_saver_add(self._h, path.encode(), ctypes.byref(r),
+                                           int(res.gid.shape[0])))
+
+    def stop(self) -> None:
+        if self._h:
+            rc = load_library().rk_saver_stop(self._h)
+            self._h = None
+            _check(rc)
+
+
+# ----------------------------------------------------------- classification --
+
+class Context:
+    """One device + stream + workspace (rk_ctx).  GPU only."""
+
+    def __init__(self, device: int = 0):
+        lib = load_library()
+        self._h = ctypes.c_void_p()
+        rc = lib.rk_create(ctypes.byref(self._h), device)
+        if rc != RK_OK:
+            raise RkError(rc, f"rk_create(device={device}) failed: a gfx950 GPU is required "
+                              "(no CPU fallback)")
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().rk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_error(self) -> str:
+        return load_library().rk_last_error(self._h).decode()
+
+    def stats(self) -> dict:
+        s = Stats()
+        _check(load_library().rk_get_stats(self._h, ctypes.byref(s)))
+        return {k: getattr(s, k) for k, _ in Stats._fields_}
+
+    def classify(self, f: Frags, len_x_hdr: int, len_y_hdr: int, len_ratio: float = 0.3,
+                 pos_ratio: float = 0.3) -> ClassifyResult:
+        """Host arrays in, host arrays out (rk_classify)."""
+        n = f.n
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+                ((f.x_start, np.uint64), (f.y_start, np.uint64), (f.length, np.uint64),
+                 (f.strand, np.uint8))]
+        soa = FragsSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), n)
+        gid = np.empty(n, np.uint32)
+        rep = np.empty(n, np.uint8)
+        order = np.empty(n, np.uint32)
+        res = Result(_ptr(gid), _ptr(rep), _ptr(order), 0, 0)
+        prm = Params(len_x_hdr, len_y_hdr, len_ratio, pos_ratio)
+        rc = load_library().rk_classify(self._h, ctypes.byref(soa), ctypes.byref(prm),
+                                        ctypes.byref(res))
+        if rc != RK_OK:
+            raise RkError(rc, self.last_error())
+        return ClassifyResult(gid, rep, order[:res.n_out].copy(), int(res.n_groups))
+
+    def classify_device(self, x, y, length, strand, gid, repval, out_order, len_x_hdr: int,
+                        len_y_hdr: int, len_ratio: float = 0.3, pos_ratio: float = 0.3):
+        """Device tensors (torch, on this context's GPU) in and out (rk_classify_device).
+
+        Returns (n_out, n_groups).  Inputs: uint64/int64 x, y, length and uint8 strand;
+        outputs: int32/uint32 gid and out_order, uint8 repval, all of length n.
+        """
+        n = int(x.shape[0])
+        soa = FragsSoA(x.data_ptr(), y.data_ptr(), length.data_ptr(), strand.data_ptr(), n)
+        res = Result(gid.data_ptr(), repval.data_ptr(), out_order.data_ptr(), 0, 0)
+        prm = Params(len_x_hdr, len_y_hdr, len_ratio, pos_ratio)
+        rc = load_library().rk_classify_device(self._h, ctypes.byref(soa), ctypes.byref(prm),
+                                               ctypes.byref(res))
+        if rc != RK_OK:
+            raise RkError(rc, self.last_error())
+        return int(res.n_out), int(res.n_groups)
+
+
+def build(jobs: int = 8) -> None:
+    """Compile librepkiller_amd.so + the CLI for gfx950 (hipcc cross-compiles without a GPU)."""
+    import subprocess
+    subprocess.run(["make", "-C", os.path.join(_HERE, "csrc"), f"-j{jobs}"], check=True)

@@ -1,0 +1,408 @@
+// rk_api.hip -- C ABI (include/repkiller_amd.h) and the device pipeline driver.
+//
+// One rk_ctx = one device + one HIP stream + one grow-only workspace in HBM,
+// mirroring the reference's one-private-state-per-worker model
+// (repkiller.cpp:60-72).  rk_classify_device runs, all on the context stream:
+//
+//   1 prep_keys        xStart/10 keys, last-bucket drop, probe validation
+//   2 counting_sort    -> processing order (stable bucket order of FragmentsDatabase)
+//   3 gather_proc      processing-order SoA + 100-bp bucket keys + sort key
+//   4 counting_sort x2 -> X and Y occupancy CSRs (SequenceOcupationList buckets)
+//   5 sweeps on X, then Y (rk_occupancy.hip) until every fragment is decided
+//   6 parents -> pointer jumping -> new-group rank (DPP scan) -> gid
+//   7 counting_sort    -> group member lists in processing order
+//   8 sort_groups      libstdc++ introsort per group; 9 emit flags / order
+//
+// Host synchronisation happens only where a data-dependent count decides the
+// next launch (kept rows, work-list sizes, jump convergence, group count).
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/repkiller_amd.h"
+#include "rk_internal.h"
+
+struct rk_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  void *ws = nullptr;  // device workspace
+  size_t ws_cap = 0;
+  uint32_t *host = nullptr;  // pinned readback words
+  // device copies for rk_classify (host-buffer entry point)
+  void *io = nullptr;
+  size_t io_cap = 0;
+  rk_stats stats{};
+  std::string err;
+};
+
+namespace {
+
+#define HIPCHK(ctx, call)                                                          \
+  do {                                                                             \
+    hipError_t e_ = (call);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);              \
+      return RK_E_HIP;                                                             \
+    }                                                                              \
+  } while (0)
+
+constexpr size_t ALIGN = 256;
+inline size_t align_up(size_t v) { return (v + ALIGN - 1) & ~(ALIGN - 1); }
+
+// bump allocator over the workspace (sizes first, then pointers)
+struct Carve {
+  char *base;
+  size_t off = 0;
+  template <class T>
+  T *take(size_t count) {
+    T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
+    off += align_up(count * sizeof(T) + 16);  // +16: uint4 tails of the scan
+    return p;
+  }
+};
+
+struct Plan {
+  uint64_t n, vsize, max_x, max_y;
+  uint32_t nbins_p, nbx, nby, maxbins;
+};
+
+struct Work {
+  uint32_t *ctrl;  // [0] err, [1..7] counters
+  uint32_t *pkey, *cnt, *tmp, *poff;
+  rk::Proc p;
+  uint32_t *xoff, *xent, *yoff, *yent;
+  uint32_t *isnew, *newrank, *goff, *gmem, *tag;
+  uint64_t *reckey;
+  uint32_t *workA, *workB, *big;
+  uint32_t *scan;
+  size_t scan_cap;
+};
+
+size_t carve(Carve &c, const Plan &pl, Work &w) {
+  const size_t n = pl.n + 1;
+  w.ctrl = c.take<uint32_t>(64);
+  w.pkey = c.take<uint32_t>(n);
+  w.cnt = c.take<uint32_t>((size_t)pl.maxbins + 1);
+  w.tmp = c.take<uint32_t>(n);
+  w.poff = c.take<uint32_t>((size_t)pl.nbins_p + 1);
+  w.p.row = c.take<uint32_t>(n);
+  w.p.xc = c.take<uint64_t>(n);
+  w.p.yc = c.take<uint64_t>(n);
+  w.p.len = c.take<uint64_t>(n);
+  w.p.ha = c.take<uint64_t>(n);
+  w.p.keyx = c.take<uint32_t>(n);
+  w.p.keyy = c.take<uint32_t>(n);
+  w.p.xstate = c.take<uint8_t>(n);
+  w.p.ystate = c.take<uint8_t>(n);
+  w.p.xwin = c.take<uint32_t>(n);
+  w.p.ywin = c.take<uint32_t>(n);
+  w.p.par = c.take<uint32_t>(n);
+  w.p.gid = c.take<uint32_t>(n);
+  w.xoff = c.take<uint32_t>(2 * (size_t)pl.nbx + 1);
+  w.xent = c.take<uint32_t>(n);
+  w.yoff = c.take<uint32_t>(2 * (size_t)pl.nby + 1);
+  w.yent = c.take<uint32_t>(n);
+  w.isnew = c.take<uint32_t>(n);
+  w.newrank = c.take<uint32_t>(n);
+  w.goff = c.take<uint32_t>(n);
+  w.gmem = c.take<uint32_t>(n);
+  w.tag = c.take<uint32_t>(n);
+  w.reckey = c.take<uint64_t>(n);
+  w.workA = c.take<uint32_t>(n);
+  w.workB = c.take<uint32_t>(n);
+  w.big = c.take<uint32_t>(n);
+  w.scan_cap = rk::scan_blocks((size_t)pl.maxbins + 2) + 64;
+  w.scan = c.take<uint32_t>(w.scan_cap);
+  return c.off;
+}
+
+int ensure_ws(rk_ctx *ctx, const Plan &pl, Work &w) {
+  Carve probe{nullptr};
+  size_t need = carve(probe, pl, w);
+  if (need > ctx->ws_cap) {
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    ctx->ws = nullptr;
+    ctx->ws_cap = 0;
+    hipError_t e = hipMalloc(&ctx->ws, need);
+    if (e != hipSuccess) {
+      ctx->err = std::string("workspace hipMalloc(") + std::to_string(need) + "): " +
+                 hipGetErrorString(e);
+      return e == hipErrorOutOfMemory ? RK_E_NOMEM : RK_E_HIP;
+    }
+    ctx->ws_cap = need;
+  }
+  Carve real{(char *)ctx->ws};
+  carve(real, pl, w);
+  return RK_OK;
+}
+
+int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count) {
+  HIPCHK(ctx, hipMemcpyAsync(ctx->host, dev, count * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return RK_OK;
+}
+
+int err_status(rk_ctx *ctx, uint32_t bits) {
+  if (bits & rk::ERRB_UB_BUCKET) {
+    ctx->err = "xStart/10 >= vsize: the reference indexes FragmentsDatabase out of bounds "
+               "(FragmentsDatabase.cpp:96-97)";
+    return RK_E_UB_BUCKET;
+  }
+  if (bits & rk::ERRB_UB_CENTER) {
+    ctx->err = "a fragment centre probes past an occupancy array "
+               "(SequenceOcupationList.cpp:17,80)";
+    return RK_E_UB_CENTER;
+  }
+  if (bits & rk::ERRB_INTERNAL) {
+    ctx->err = "device consistency check failed";
+    return RK_E_INTERNAL;
+  }
+  return RK_OK;
+}
+
+// run sweeps on one axis until no bucket has undecided entries
+int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, const uint32_t *key, Work &w, uint32_t m,
+                 uint32_t nbins, uint32_t *sweeps) {
+  uint32_t *cnt_dev = w.ctrl + 2, *next_dev = w.ctrl + 3, *big_dev = w.ctrl + 4;
+  rk::nonempty_bins(key, ax.ent, ax.off, nbins, m, w.workA, cnt_dev, ctx->stream);
+  int rc = readback(ctx, cnt_dev, 1);
+  if (rc) return rc;
+  uint32_t nwork = ctx->host[0];
+  uint32_t *cur = w.workA, *nxt = w.workB;
+  *sweeps = 0;
+  while (nwork) {
+    if (*sweeps > m + 2) {
+      ctx->err = "occupancy sweeps did not converge";
+      return RK_E_INTERNAL;
+    }
+    HIPCHK(ctx, hipMemsetAsync(next_dev, 0, sizeof(uint32_t), ctx->stream));
+    rk::occupancy_sweep(ax, cur, nwork, nxt, next_dev, w.big, big_dev, ctx->stream);
+    HIPCHK(ctx, hipGetLastError());
+    rc = readback(ctx, next_dev, 1);
+    if (rc) return rc;
+    nwork = ctx->host[0];
+    std::swap(cur, nxt);
+    ++*sweeps;
+  }
+  return RK_OK;
+}
+
+int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, rk_result *out) {
+  if (!ctx || !in || !prm || !out) return RK_E_ARG;
+  if (in->n >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
+  if (!(prm->len_ratio > 0) || !(prm->pos_ratio > 0)) {
+    ctx->err = "ratios must be greater than zero (commonFunctions.cpp:26-27)";
+    return RK_E_ARG;
+  }
+  if (in->n && (!in->x_start || !in->y_start || !in->length || !in->strand || !out->gid ||
+                !out->repval || !out->out_order))
+    return RK_E_ARG;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  std::memset(&ctx->stats, 0, sizeof ctx->stats);
+  hipStream_t st = ctx->stream;
+
+  Plan pl{};
+  pl.n = in->n;
+  const uint64_t len_x = prm->len_x_hdr + 1, len_y = prm->len_y_hdr + 1;  // FragmentsDatabase.cpp:62,65
+  pl.vsize = 1 + len_x / 10;                                                // :84
+  pl.max_x = len_x / 100;                                                   // SequenceOcupationList.cpp:4
+  pl.max_y = len_y / 100;
+  if (pl.vsize - 1 >= 0xFFFFFFF0ull || 2 * (pl.max_x + 1) >= 0xFFFFFFF0ull ||
+      2 * (pl.max_y + 1) >= 0xFFFFFFF0ull) {
+    ctx->err = "sequence length too large for 32-bit bucket ids";
+    return RK_E_ARG;
+  }
+  pl.nbins_p = (uint32_t)(pl.vsize - 1);
+  pl.nbx = (uint32_t)(pl.max_x + 1);
+  pl.nby = (uint32_t)(pl.max_y + 1);
+  pl.maxbins = std::max<uint64_t>(std::max<uint64_t>(pl.nbins_p, 2ull * pl.nbx),
+                                  std::max<uint64_t>(2ull * pl.nby, pl.n + 1));
+  Work w;
+  int rc = ensure_ws(ctx, pl, w);
+  if (rc) return rc;
+  const uint32_t n = (uint32_t)pl.n;
+  rk::ScanScratch ss{w.scan, w.scan_cap};
+  ctx->stats.n_in = n;
+
+  HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
+  HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, 64 * sizeof(uint32_t), st));
+  rk::fill_dropped(n, out->gid, out->repval, st);
+  rk::Frags f{in->x_start, in->y_start, in->length, in->strand, n};
+
+  // 1-2: processing order
+  rk::prep_keys(f, pl.vsize, pl.max_x, pl.max_y, w.pkey, w.ctrl, st);
+  rk::counting_sort(w.pkey, n, pl.nbins_p, w.poff, w.p.row, w.cnt, w.tmp, ss, st);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipMemcpyAsync(w.ctrl + 1, w.poff + pl.nbins_p, sizeof(uint32_t),
+                             hipMemcpyDeviceToDevice, st));
+  if ((rc = readback(ctx, w.ctrl, 2))) return rc;
+  if ((rc = err_status(ctx, ctx->host[0]))) return rc;
+  const uint32_t m = ctx->host[1];
+  ctx->stats.n_proc = m;
+  out->n_out = m;
+  out->n_groups = 0;
+  if (m == 0) {
+    HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    return RK_OK;
+  }
+
+  // 3-4: processing-order SoA and the two occupancy CSRs
+  rk::gather_proc(f, w.pkey, w.poff, w.p, m, pl.nbx, pl.nby, st);
+  rk::counting_sort(w.p.keyx, m, 2 * pl.nbx, w.xoff, w.xent, w.cnt, w.tmp, ss, st);
+  rk::counting_sort(w.p.keyy, m, 2 * pl.nby, w.yoff, w.yent, w.cnt, w.tmp, ss, st);
+  HIPCHK(ctx, hipGetLastError());
+
+  // 5: X, then Y
+  rk::Axis ax{w.xoff, w.xent, w.p.xc, w.p.len, w.p.xstate, w.p.xwin, pl.max_x, pl.nbx,
+              prm->len_ratio, prm->pos_ratio};
+  if ((rc = resolve_axis(ctx, ax, w.p.keyx, w, m, 2 * pl.nbx, &ctx->stats.x_sweeps))) return rc;
+  rk::init_ystate(w.p, m, st);
+  rk::Axis ay{w.yoff, w.yent, w.p.yc, w.p.len, w.p.ystate, w.p.ywin, pl.max_y, pl.nby,
+              prm->len_ratio, prm->pos_ratio};
+  if ((rc = resolve_axis(ctx, ay, w.p.keyy, w, m, 2 * pl.nby, &ctx->stats.y_sweeps))) return rc;
+
+  // 6: group roots and ids
+  rk::make_parents(w.p, m, w.isnew, w.ctrl, st);
+  HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
+  for (;;) {
+    HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
+    rk::jump_round(w.p, m, w.ctrl + 5, st);
+    if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
+    ctx->stats.jump_rounds++;
+    if (!ctx->host[0]) break;
+    if (ctx->stats.jump_rounds > 64) {
+      ctx->err = "pointer jumping did not converge";
+      return RK_E_INTERNAL;
+    }
+  }
+  rk::exclusive_scan_u32(w.isnew, w.newrank, (size_t)m + 1, ss, st);
+  if ((rc = readback(ctx, w.newrank + m, 1))) return rc;
+  const uint32_t G = ctx->host[0];
+  out->n_groups = G;
+  ctx->stats.n_groups = G;
+  rk::assign_gid(w.p, m, w.newrank, st);
+
+  // 7-9: members, in-group order, flags
+  rk::counting_sort(w.p.gid, m, G, w.goff, w.gmem, w.cnt, w.tmp, ss, st);
+  rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
+  rk::sort_groups(w.goff, G, w.reckey, w.tag, st);
+  rk::emit_result(w.tag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval, out->out_order, st);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
+  if ((rc = readback(ctx, w.ctrl, 1))) return rc;
+  if ((rc = err_status(ctx, ctx->host[0]))) return rc;
+  float ms = 0;
+  HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->stats.device_ms = ms;
+  return RK_OK;
+}
+
+}  // namespace
+
+extern "C" int rk_create(rk_ctx **out, int device) {
+  if (!out) return RK_E_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count)
+    return RK_E_NODEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RK_E_NODEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RK_E_NODEVICE;
+  auto ctx = new (std::nothrow) rk_ctx;
+  if (!ctx) return RK_E_NOMEM;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+      hipHostMalloc((void **)&ctx->host, 64 * sizeof(uint32_t), hipHostMallocDefault) !=
+          hipSuccess) {
+    rk_destroy(ctx);
+    return RK_E_HIP;
+  }
+  *out = ctx;
+  return RK_OK;
+}
+
+extern "C" void rk_destroy(rk_ctx *ctx) {
+  if (!ctx) return;
+  if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->io) (void)hipFree(ctx->io);
+  if (ctx->host) (void)hipHostFree(ctx->host);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+extern "C" const char *rk_last_error(const rk_ctx *ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+extern "C" int rk_get_stats(const rk_ctx *ctx, rk_stats *st) {
+  if (!ctx || !st) return RK_E_ARG;
+  *st = ctx->stats;
+  return RK_OK;
+}
+
+extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params *p,
+                                  rk_result *out_dev) {
+  if (!ctx) return RK_E_ARG;
+  ctx->err.clear();
+  try {
+    return classify_device(ctx, in_dev, p, out_dev);
+  } catch (...) {
+    ctx->err = "unexpected C++ exception";
+    return RK_E_INTERNAL;
+  }
+}
+
+extern "C" int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p,
+                           rk_result *out) {
+  if (!ctx || !in || !p || !out) return RK_E_ARG;
+  ctx->err.clear();
+  const size_t n = in->n;
+  if (n >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
+  if (n && (!in->x_start || !in->y_start || !in->length || !in->strand || !out->gid ||
+            !out->repval || !out->out_order))
+    return RK_E_ARG;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // device staging: x, y, len (u64), strand (u8) in; gid, order (u32), rep (u8) out
+  size_t need = align_up(n * 8 + 16) * 3 + align_up(n + 16) * 2 + align_up(n * 4 + 16) * 2;
+  if (need > ctx->io_cap) {
+    if (ctx->io) (void)hipFree(ctx->io);
+    ctx->io = nullptr;
+    ctx->io_cap = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->io, need));
+    ctx->io_cap = need;
+  }
+  Carve c{(char *)ctx->io};
+  uint64_t *dx = c.take<uint64_t>(n), *dy = c.take<uint64_t>(n), *dl = c.take<uint64_t>(n);
+  uint8_t *ds = c.take<uint8_t>(n), *drep = c.take<uint8_t>(n);
+  uint32_t *dgid = c.take<uint32_t>(n), *dord = c.take<uint32_t>(n);
+  hipStream_t st = ctx->stream;
+  if (n) {
+    HIPCHK(ctx, hipMemcpyAsync(dx, in->x_start, n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(dy, in->y_start, n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(dl, in->length, n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(ds, in->strand, n, hipMemcpyHostToDevice, st));
+  }
+  rk_frags_soa din{dx, dy, dl, ds, n};
+  rk_result dres{dgid, drep, dord, 0, 0};
+  int rc = rk_classify_device(ctx, &din, p, &dres);
+  if (rc) return rc;
+  out->n_out = dres.n_out;
+  out->n_groups = dres.n_groups;
+  if (n) {
+    HIPCHK(ctx, hipMemcpyAsync(out->gid, dgid, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(out->repval, drep, n, hipMemcpyDeviceToHost, st));
+    if (dres.n_out)
+      HIPCHK(ctx, hipMemcpyAsync(out->out_order, dord, dres.n_out * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+  }
+  return RK_OK;
+}

@@ -1,0 +1,205 @@
+// rk_sort.hip -- device exclusive scan and stable counting sort (gfx950).
+//
+// These are the "coverage histogram + scan" kernels of the design: every
+// bucketed structure of the reference -- the xStart/10 processing buckets of
+// FragmentsDatabase (FragmentsDatabase.cpp:84-97), the 100-bp occupancy
+// buckets of SequenceOcupationList (SequenceOcupationList.cpp:5-7,17) and the
+// FragsGroup member lists (commonFunctions.cpp:58,66,73) -- becomes a CSR
+// built by: histogram -> exclusive scan -> scatter -> in-bin rank fix.
+//
+// Scan: 256-thread blocks, 4096 u32 per tile (4 rows of 1024; each row one
+// coalesced uint4 per lane), wave inclusive scan in DPP (row_shr 1/2/4/8 then
+// row_bcast 15/31 -- GFX9 DPP, 6 VALU ops for 64 lanes), wave totals through
+// LDS, tiles chained by a recursive reduce-then-scan.
+#include "rk_internal.h"
+
+namespace rk {
+namespace {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ROW = SCAN_THREADS * 4;  // 1024
+constexpr int SCAN_TILE = SCAN_ROW * 4;     // 4096
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
+__device__ __forceinline__ uint4 load4(const uint32_t *in, size_t base, size_t n) {
+  if (base + 3 < n) return *reinterpret_cast<const uint4 *>(in + base);
+  uint4 v = {0, 0, 0, 0};
+  if (base + 0 < n) v.x = in[base + 0];
+  if (base + 1 < n) v.y = in[base + 1];
+  if (base + 2 < n) v.z = in[base + 2];
+  return v;
+}
+
+__device__ __forceinline__ void store4(uint32_t *out, size_t base, size_t n, uint4 v) {
+  if (base + 3 < n) {
+    *reinterpret_cast<uint4 *>(out + base) = v;
+    return;
+  }
+  if (base + 0 < n) out[base + 0] = v.x;
+  if (base + 1 < n) out[base + 1] = v.y;
+  if (base + 2 < n) out[base + 2] = v.z;
+}
+
+// exclusive block scan of one value per thread; returns the block total in *tot
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *tot) {
+  __shared__ uint32_t wsum[SCAN_THREADS / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = wave_incl_scan(v);
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_THREADS / 64; ++k) {
+    uint32_t s = wsum[k];
+    pre += k < w ? s : 0u;
+    all += s;
+  }
+  __syncthreads();
+  *tot = all;
+  return pre + inc - v;
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_reduce_tiles(const uint32_t *in, size_t n,
+                                                               uint32_t *sums) {
+  __shared__ uint32_t red[SCAN_THREADS / 64];
+  const size_t tile = (size_t)blockIdx.x * SCAN_TILE;
+  uint32_t s = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    uint4 v = load4(in, tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n);
+    s += v.x + v.y + v.z + v.w;
+  }
+  s = wave_incl_scan(s);
+  if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < SCAN_THREADS / 64; ++k) t += red[k];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of each tile, plus prefix[blockIdx] when given; in may == out
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const uint32_t *in, uint32_t *out,
+                                                             size_t n, const uint32_t *prefix) {
+  const size_t tile = (size_t)blockIdx.x * SCAN_TILE;
+  uint32_t carry = prefix ? prefix[blockIdx.x] : 0u;
+  uint4 v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = load4(in, tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    uint32_t t = v[r].x + v[r].y + v[r].z + v[r].w, tot;
+    uint32_t e = block_excl_scan(t, &tot) + carry;
+    uint4 o;
+    o.x = e;
+    o.y = o.x + v[r].x;
+    o.z = o.y + v[r].y;
+    o.w = o.z + v[r].z;
+    store4(out, tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n, o);
+    carry += tot;
+  }
+}
+
+__global__ void k_hist(const uint32_t *key, uint32_t m, uint32_t *cnt) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+    uint32_t k = key[i];
+    if (k != SKIP) atomicAdd(&cnt[k], 1u);
+  }
+}
+
+__global__ void k_scatter(const uint32_t *key, uint32_t m, uint32_t *cursor, uint32_t *tmp) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+    uint32_t k = key[i];
+    if (k != SKIP) tmp[atomicAdd(&cursor[k], 1u)] = i;
+  }
+}
+
+// Restore ascending index order inside every bin: the element at scattered
+// slot p moves to off[k] + (#bin members with a smaller index).
+__global__ void k_rankfix(const uint32_t *key, const uint32_t *off, uint32_t nbins,
+                          const uint32_t *tmp, uint32_t *perm) {
+  const uint32_t total = off[nbins];
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total;
+       p += gridDim.x * blockDim.x) {
+    uint32_t i = tmp[p];
+    uint32_t k = key[i];
+    uint32_t b = off[k], e = off[k + 1];
+    uint32_t r = 0;
+    for (uint32_t q = b; q < e; ++q) r += tmp[q] < i;
+    perm[b + r] = i;
+  }
+}
+
+__global__ void k_nonempty(const uint32_t *key, const uint32_t *perm, const uint32_t *off,
+                           uint32_t nbins, uint32_t *list, uint32_t *count) {
+  const uint32_t total = off[nbins];
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total;
+       p += gridDim.x * blockDim.x) {
+    uint32_t k = key[perm[p]];
+    if (off[k] == p) list[atomicAdd(count, 1u)] = k;
+  }
+}
+
+inline unsigned grid_for(size_t n, int threads) {
+  size_t g = (n + threads - 1) / threads;
+  if (g > 65536) g = 65536;
+  return (unsigned)(g ? g : 1);
+}
+
+}  // namespace
+
+size_t scan_blocks(size_t n) {
+  size_t total = 0;
+  while (n > (size_t)SCAN_TILE) {
+    n = (n + SCAN_TILE - 1) / SCAN_TILE;
+    total += (n + 4) & ~(size_t)3;  // keeps every level 16-B aligned
+  }
+  return total + 1;
+}
+
+void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
+                        hipStream_t st) {
+  if (n == 0) return;
+  if (n <= (size_t)SCAN_TILE) {
+    k_scan_tiles<<<1, SCAN_THREADS, 0, st>>>(in, out, n, nullptr);
+    return;
+  }
+  size_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  uint32_t *sums = ss.block_sums;
+  const size_t stride = (nb + 4) & ~(size_t)3;  // uint4 loads need 16-B alignment
+  ScanScratch rest{ss.block_sums + stride, ss.cap - stride};
+  k_reduce_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, n, sums);
+  exclusive_scan_u32(sums, sums, nb, rest, st);
+  k_scan_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, out, n, sums);
+}
+
+void counting_sort(const uint32_t *key, uint32_t m, uint32_t nbins, uint32_t *off, uint32_t *perm,
+                   uint32_t *cnt, uint32_t *tmp, ScanScratch ss, hipStream_t st) {
+  (void)hipMemsetAsync(cnt, 0, ((size_t)nbins + 1) * sizeof(uint32_t), st);
+  if (m) k_hist<<<grid_for(m, 256), 256, 0, st>>>(key, m, cnt);
+  exclusive_scan_u32(cnt, off, (size_t)nbins + 1, ss, st);
+  (void)hipMemcpyAsync(cnt, off, ((size_t)nbins + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+  if (m) {
+    k_scatter<<<grid_for(m, 256), 256, 0, st>>>(key, m, cnt, tmp);
+    // kept count is off[nbins] (device value): the kernel bounds itself by it
+    k_rankfix<<<grid_for(m, 256), 256, 0, st>>>(key, off, nbins, tmp, perm);
+  }
+}
+
+void nonempty_bins(const uint32_t *key, const uint32_t *perm, const uint32_t *off, uint32_t nbins,
+                   uint32_t m, uint32_t *list, uint32_t *d_count, hipStream_t st) {
+  (void)hipMemsetAsync(d_count, 0, sizeof(uint32_t), st);
+  if (m) k_nonempty<<<grid_for(m, 256), 256, 0, st>>>(key, perm, off, nbins, list, d_count);
+}
+
+}  // namespace rk

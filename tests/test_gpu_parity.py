@@ -1,0 +1,173 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference's golden outputs.  Bit-exact on every integer output: group id per
+row, repeat flag per row and the output row order (hence the CSV bytes).
+
+Sizes: edge fixtures, the 10k corpus (byte-exact CSV), synthetic cfg1/cfg2
+sets against the oracle arrays, the 1M sets against the reference's SHA-256
+(tests/golden/hashes.json), and property checks at larger sizes where the
+oracle would be slow.
+"""
+import gzip
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import EDGE, GOLDEN, ROOT, edge_cases
+from oracle import rk_oracle as ro
+
+import repkiller_amd as rk
+
+pytestmark = pytest.mark.gpu
+
+ERR = {"error:RK_E_UB_BUCKET": -4, "error:RK_E_UB_CENTER": -5, "error:RK_E_COUNT": -3}
+
+
+def gpu_vs_oracle(ctx, f, lx, ly, lr=0.3, pr=0.3):
+    got = ctx.classify(f, lx, ly, lr, pr)
+    rc, gid, rep, order, ng = ro.classify(f.x_start, f.y_start, f.length, f.strand, lx, ly, lr, pr)
+    assert rc == 0
+    assert got.n_groups == ng
+    assert np.array_equal(got.out_order, order)
+    assert np.array_equal(got.gid, gid)
+    assert np.array_equal(got.repval, rep)
+    return got
+
+
+@pytest.mark.parametrize("name,case", edge_cases(), ids=[n for n, _ in edge_cases()])
+def test_edge_fixture(gpu_ctx, tmp_path, name, case):
+    inp = os.path.join(EDGE, name + ".in.csv")
+    if case["expect"] == "error:RK_E_COUNT":
+        with pytest.raises(rk.RkError):
+            rk.FragmentsDatabase(inp)
+        return
+    db = rk.FragmentsDatabase(inp)
+    if case["expect"] != "ref":
+        with pytest.raises(rk.RkError) as e:
+            gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, case["len_ratio"],
+                             case["pos_ratio"])
+        assert e.value.code == ERR[case["expect"]]
+        return
+    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, case["len_ratio"],
+                           case["pos_ratio"])
+    out = tmp_path / "out.csv"
+    db.save_all_frag_pairs(str(out), res)
+    with open(os.path.join(EDGE, name + ".out.csv"), "rb") as f:
+        assert out.read_bytes() == f.read()
+
+
+def test_corpus10k_csv(gpu_ctx, tmp_path):
+    inp, out = tmp_path / "in.csv", tmp_path / "out.csv"
+    with gzip.open(os.path.join(GOLDEN, "corpus10k.in.csv.gz"), "rb") as fi, open(inp, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    db = rk.FragmentsDatabase(str(inp))
+    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr)
+    db.save_all_frag_pairs(str(out), res)
+    with gzip.open(os.path.join(GOLDEN, "corpus10k.out.csv.gz"), "rb") as f:
+        assert out.read_bytes() == f.read()
+
+
+@pytest.mark.parametrize("seed", [1, 11, 12])
+@pytest.mark.parametrize("lr,pr", [(0.3, 0.3), (0.05, 0.05), (1.5, 0.7), (0.3, 2.0)])
+def test_cfg1_vs_oracle(gpu_ctx, seed, lr, pr):
+    f = rk.synth(10000, 1_000_000, seed=seed)
+    gpu_vs_oracle(gpu_ctx, f, 1_000_000, 1_000_000, lr, pr)
+
+
+@pytest.mark.parametrize("n,L,kw", [
+    (200_000, 10_000_000, {}),
+    (200_000, 10_000_000, dict(family_frac=0.95, copies=(100, 600))),
+    (50_000, 200_000, dict(family_frac=0.95, copies=(100, 600))),  # very dense buckets
+    (30_000, 100_000, {}),  # upward probes active over the first 1% (c < max_index)
+])
+def test_synthetic_vs_oracle(gpu_ctx, n, L, kw):
+    f = rk.synth(n, L, seed=21, **kw)
+    gpu_vs_oracle(gpu_ctx, f, L, L)
+
+
+def test_empty_and_tiny(gpu_ctx):
+    f = rk.Frags(np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint64),
+                 np.zeros(0, np.uint8))
+    r = gpu_ctx.classify(f, 1000, 1000)
+    assert r.n_groups == 0 and r.out_order.size == 0
+    f = rk.Frags(np.array([10], np.uint64), np.array([20], np.uint64), np.array([30], np.uint64),
+                 np.array([ord('f')], np.uint8))
+    gpu_vs_oracle(gpu_ctx, f, 1000, 1000)
+
+
+def sha256_csv(db, res, path):
+    db.save_all_frag_pairs(path, res)
+    h = hashlib.sha256()
+    with open(path, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+with open(os.path.join(GOLDEN, "hashes.json")) as _f:
+    HASHES = json.load(_f)
+
+
+@pytest.mark.parametrize("key", sorted(HASHES))
+def test_1M_reference_hash(gpu_ctx, tmp_path, key):
+    h = HASHES[key]
+    kw = dict(h["synth"])
+    if "copies" in kw:
+        kw["copies"] = tuple(kw["copies"])
+    f = rk.synth(**kw)
+    L = kw["genome_len"]
+    inp = str(tmp_path / "in.csv")
+    rk.write_input_csv(inp, f, L, L)
+    with open(inp, "rb") as fh:
+        assert hashlib.sha256(fh.read()).hexdigest() == h["input_sha256"]
+    db = rk.FragmentsDatabase(inp)
+    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, h["len_ratio"], h["pos_ratio"])
+    assert sha256_csv(db, res, str(tmp_path / "out.csv")) == h["output_sha256"]
+
+
+def test_classify_device_torch(gpu_ctx):
+    import torch
+    f = rk.synth(100_000, 5_000_000, seed=7)
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(f.x_start.view(np.int64)).to(dev)
+    y = torch.from_numpy(f.y_start.view(np.int64)).to(dev)
+    ln = torch.from_numpy(f.length.view(np.int64)).to(dev)
+    s = torch.from_numpy(f.strand).to(dev)
+    gid = torch.empty(f.n, dtype=torch.int32, device=dev)
+    rep = torch.empty(f.n, dtype=torch.uint8, device=dev)
+    order = torch.empty(f.n, dtype=torch.int32, device=dev)
+    n_out, ng = gpu_ctx.classify_device(x, y, ln, s, gid, rep, order, 5_000_000, 5_000_000)
+    rc, g2, r2, o2, ng2 = ro.classify(f.x_start, f.y_start, f.length, f.strand, 5_000_000,
+                                      5_000_000)
+    assert ng == ng2 and n_out == o2.size
+    assert np.array_equal(gid.cpu().numpy().view(np.uint32), g2)
+    assert np.array_equal(rep.cpu().numpy(), r2)
+    assert np.array_equal(order[:n_out].cpu().numpy().view(np.uint32), o2)
+
+
+def test_repeat_calls_same_context(gpu_ctx):
+    """Workspace reuse across sizes must not leak state between calls."""
+    a = rk.synth(20_000, 2_000_000, seed=31)
+    b = rk.synth(3_000, 300_000, seed=32)
+    r1 = gpu_vs_oracle(gpu_ctx, a, 2_000_000, 2_000_000)
+    gpu_vs_oracle(gpu_ctx, b, 300_000, 300_000)
+    r3 = gpu_ctx.classify(a, 2_000_000, 2_000_000)
+    assert np.array_equal(r1.out_order, r3.out_order)
+
+
+def test_cli_matches_reference(tmp_path):
+    """rk_repkiller (C++ host driver) end to end: CSV in, CSV out, byte-exact."""
+    inp, out = tmp_path / "in.csv", tmp_path / "out.csv"
+    with gzip.open(os.path.join(GOLDEN, "corpus10k.in.csv.gz"), "rb") as fi, open(inp, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    p = subprocess.run([rk.CLI_PATH, str(inp), str(out), "0.05", "0.05", "0.3", "0.3"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    with gzip.open(os.path.join(GOLDEN, "corpus10k.out.csv.gz"), "rb") as f:
+        assert out.read_bytes() == f.read()  # last pair wins (E10)
+    p = subprocess.run([rk.CLI_PATH, str(inp), str(out), "0.3"], capture_output=True, text=True)
+    assert p.returncode == 1  # odd ratio count: usage error (E9)
