@@ -99,6 +99,28 @@ int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params 
 
 int rk_get_stats(const rk_ctx *ctx, rk_stats *st);
 
+/* Phase profiling: when enabled, HIP events are recorded on the context
+ * stream at every phase boundary of rk_classify*; rk_get_phase_ms returns the
+ * accumulated device milliseconds (and call counts) per phase. */
+enum {
+  RK_PH_PREP = 0,       /* xStart/10 keys, last-bucket drop, probe validation */
+  RK_PH_ORDER = 1,      /* processing-order counting sort (FragmentsDatabase buckets) */
+  RK_PH_GATHER = 2,     /* processing-order SoA, centres, sort keys */
+  RK_PH_OCC_CSR = 3,    /* X and Y 100-bp occupancy CSRs */
+  RK_PH_SWEEP_X = 4,    /* X-axis occupancy resolution */
+  RK_PH_SWEEP_Y = 5,    /* Y-axis occupancy resolution */
+  RK_PH_ROOTS = 6,      /* winner chains -> roots -> group ids */
+  RK_PH_MEMBERS = 7,    /* group member CSR */
+  RK_PH_GROUP_SORT = 8, /* libstdc++ introsort per group */
+  RK_PH_EMIT = 9,       /* repeat flags + output order */
+  RK_N_PHASES = 10
+};
+int rk_set_profiling(rk_ctx *ctx, int enable);
+int rk_get_phase_ms(const rk_ctx *ctx, double *ms /* [RK_N_PHASES] */,
+                    uint32_t *calls /* nullable */);
+int rk_reset_phases(rk_ctx *ctx);
+const char *rk_phase_name(int phase);
+
 /* ---- host ingress: FragmentsDatabase (FragmentsDatabase.cpp:17-101) ---- */
 
 typedef struct rk_db rk_db;

@@ -31,6 +31,7 @@ LIB_PATH = os.path.join(_HERE, "librepkiller_amd.so")
 CLI_PATH = os.path.join(_HERE, "bin", "rk_repkiller")
 
 RK_OK = 0
+N_PHASES = 10  # RK_N_PHASES
 STATUS = {
     0: "RK_OK", -1: "RK_E_ARG", -2: "RK_E_IO", -3: "RK_E_COUNT", -4: "RK_E_UB_BUCKET",
     -5: "RK_E_UB_CENTER", -6: "RK_E_NOMEM", -7: "RK_E_HIP", -8: "RK_E_NODEVICE",
@@ -40,7 +41,8 @@ STATUS = {
 # every symbol include/repkiller_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "rk_create", "rk_destroy", "rk_last_error", "rk_classify", "rk_classify_device",
-    "rk_get_stats", "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
+    "rk_get_stats", "rk_set_profiling", "rk_get_phase_ms", "rk_reset_phases", "rk_phase_name",
+    "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
     "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
     "rk_synth_write_csv",
 )
@@ -116,6 +118,10 @@ def load_library() -> ctypes.CDLL:
         "rk_classify_device": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA),
                                               ctypes.POINTER(Params), ctypes.POINTER(Result)]),
         "rk_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(Stats)]),
+        "rk_set_profiling": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rk_get_phase_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), _u32p]),
+        "rk_reset_phases": (ctypes.c_int, [vp]),
+        "rk_phase_name": (ctypes.c_char_p, [ctypes.c_int]),
         "rk_db_load_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(vp)]),
         "rk_db_free": (None, [vp]),
         "rk_db_view": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA), _u64p, _u64p, _u64p]),
@@ -302,6 +308,20 @@ class Context:
         s = Stats()
         _check(load_library().rk_get_stats(self._h, ctypes.byref(s)))
         return {k: getattr(s, k) for k, _ in Stats._fields_}
+
+    def set_profiling(self, on: bool = True) -> None:
+        _check(load_library().rk_set_profiling(self._h, int(on)))
+
+    def reset_phases(self) -> None:
+        _check(load_library().rk_reset_phases(self._h))
+
+    def phases(self) -> dict:
+        """{phase name: (accumulated device ms, calls)} since the last reset."""
+        lib = load_library()
+        ms = (ctypes.c_double * N_PHASES)()
+        calls = (ctypes.c_uint32 * N_PHASES)()
+        _check(lib.rk_get_phase_ms(self._h, ms, calls))
+        return {lib.rk_phase_name(i).decode(): (ms[i], calls[i]) for i in range(N_PHASES)}
 
     def classify(self, f: Frags, len_x_hdr: int, len_y_hdr: int, len_ratio: float = 0.3,
                  pos_ratio: float = 0.3) -> ClassifyResult:

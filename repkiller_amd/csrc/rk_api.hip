@@ -36,6 +36,18 @@ struct rk_ctx {
   size_t io_cap = 0;
   rk_stats stats{};
   std::string err;
+  // phase profiling (rk_set_profiling): one event per phase boundary, on the
+  // context stream, accumulated over calls until rk_reset_phases
+  bool profiling = false;
+  hipEvent_t pev[RK_N_PHASES + 1] = {};
+  bool pev_used[RK_N_PHASES + 1] = {};
+  double phase_ms[RK_N_PHASES] = {};
+  uint32_t phase_calls[RK_N_PHASES] = {};
+};
+
+static const char *kPhaseNames[RK_N_PHASES] = {
+    "prep_keys",      "order_csr",  "gather_proc", "occupancy_csr", "sweep_x", "sweep_y",
+    "group_roots",    "member_csr", "group_sort",  "emit",
 };
 
 namespace {
@@ -66,15 +78,17 @@ struct Carve {
 
 struct Plan {
   uint64_t n, vsize, max_x, max_y;
-  uint32_t nbins_p, nbx, nby, maxbins;
+  uint32_t nbx, nby;
 };
 
 struct Work {
-  uint32_t *ctrl;  // [0] err, [1..7] counters
-  uint32_t *pkey, *cnt, *tmp, *poff;
+  uint32_t *ctrl;  // [0] err bits, [1] kept rows, [2..7] counters
+  uint32_t *pkey_in, *tk, *tv;
+  uint32_t *radix;
+  size_t radix_words;
   rk::Proc p;
-  uint32_t *xoff, *xent, *yoff, *yent;
-  uint32_t *isnew, *newrank, *goff, *gmem, *tag;
+  rk::Csr cx, cy;
+  uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag;
   uint64_t *reckey;
   uint32_t *workA, *workB, *big;
   uint32_t *scan;
@@ -84,10 +98,12 @@ struct Work {
 size_t carve(Carve &c, const Plan &pl, Work &w) {
   const size_t n = pl.n + 1;
   w.ctrl = c.take<uint32_t>(64);
-  w.pkey = c.take<uint32_t>(n);
-  w.cnt = c.take<uint32_t>((size_t)pl.maxbins + 1);
-  w.tmp = c.take<uint32_t>(n);
-  w.poff = c.take<uint32_t>((size_t)pl.nbins_p + 1);
+  w.pkey_in = c.take<uint32_t>(n);
+  w.tk = c.take<uint32_t>(n);
+  w.tv = c.take<uint32_t>(n);
+  w.radix_words = rk::radix_scratch_words((uint32_t)n);
+  w.radix = c.take<uint32_t>(w.radix_words);
+  w.p.pkey = c.take<uint32_t>(n);
   w.p.row = c.take<uint32_t>(n);
   w.p.xc = c.take<uint64_t>(n);
   w.p.yc = c.take<uint64_t>(n);
@@ -101,20 +117,25 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.p.ywin = c.take<uint32_t>(n);
   w.p.par = c.take<uint32_t>(n);
   w.p.gid = c.take<uint32_t>(n);
-  w.xoff = c.take<uint32_t>(2 * (size_t)pl.nbx + 1);
-  w.xent = c.take<uint32_t>(n);
-  w.yoff = c.take<uint32_t>(2 * (size_t)pl.nby + 1);
-  w.yent = c.take<uint32_t>(n);
+  for (rk::Csr *cs : {&w.cx, &w.cy}) {
+    cs->key = c.take<uint32_t>(n);
+    cs->ent = c.take<uint32_t>(n);
+    cs->cen = c.take<uint64_t>(n);
+    cs->len = c.take<uint64_t>(n);
+    cs->state = c.take<uint8_t>(n);
+    cs->win = c.take<uint32_t>(n);
+  }
   w.isnew = c.take<uint32_t>(n);
   w.newrank = c.take<uint32_t>(n);
-  w.goff = c.take<uint32_t>(n);
+  w.sgid = c.take<uint32_t>(n);
   w.gmem = c.take<uint32_t>(n);
+  w.goff = c.take<uint32_t>(n);
   w.tag = c.take<uint32_t>(n);
   w.reckey = c.take<uint64_t>(n);
   w.workA = c.take<uint32_t>(n);
   w.workB = c.take<uint32_t>(n);
   w.big = c.take<uint32_t>(n);
-  w.scan_cap = rk::scan_blocks((size_t)pl.maxbins + 2) + 64;
+  w.scan_cap = rk::scan_blocks(n + 1) + 64;
   w.scan = c.take<uint32_t>(w.scan_cap);
   return c.off;
 }
@@ -137,6 +158,30 @@ int ensure_ws(rk_ctx *ctx, const Plan &pl, Work &w) {
   Carve real{(char *)ctx->ws};
   carve(real, pl, w);
   return RK_OK;
+}
+
+// mark the START of phase `ph` (ph == RK_N_PHASES marks the end of the last)
+void mark(rk_ctx *ctx, int ph) {
+  if (!ctx->profiling) return;
+  (void)hipEventRecord(ctx->pev[ph], ctx->stream);
+  ctx->pev_used[ph] = true;
+}
+
+void collect_phases(rk_ctx *ctx) {
+  if (!ctx->profiling) return;
+  (void)hipEventSynchronize(ctx->pev[RK_N_PHASES]);
+  for (int ph = 0; ph < RK_N_PHASES; ++ph) {
+    if (!ctx->pev_used[ph]) continue;
+    int nx = ph + 1;
+    while (nx <= RK_N_PHASES && !ctx->pev_used[nx]) ++nx;
+    if (nx > RK_N_PHASES) break;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->pev[ph], ctx->pev[nx]) == hipSuccess) {
+      ctx->phase_ms[ph] += ms;
+      ctx->phase_calls[ph]++;
+    }
+  }
+  for (auto &u : ctx->pev_used) u = false;
 }
 
 int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count) {
@@ -165,17 +210,16 @@ int err_status(rk_ctx *ctx, uint32_t bits) {
 }
 
 // run sweeps on one axis until no bucket has undecided entries
-int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, const uint32_t *key, Work &w, uint32_t m,
-                 uint32_t nbins, uint32_t *sweeps) {
+int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, uint32_t *sweeps) {
   uint32_t *cnt_dev = w.ctrl + 2, *next_dev = w.ctrl + 3, *big_dev = w.ctrl + 4;
-  rk::nonempty_bins(key, ax.ent, ax.off, nbins, m, w.workA, cnt_dev, ctx->stream);
+  rk::run_starts(ax.key, ax.m, w.workA, cnt_dev, ctx->stream);
   int rc = readback(ctx, cnt_dev, 1);
   if (rc) return rc;
   uint32_t nwork = ctx->host[0];
   uint32_t *cur = w.workA, *nxt = w.workB;
   *sweeps = 0;
   while (nwork) {
-    if (*sweeps > m + 2) {
+    if (*sweeps > ax.m + 2) {
       ctx->err = "occupancy sweeps did not converge";
       return RK_E_INTERNAL;
     }
@@ -216,11 +260,8 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
     ctx->err = "sequence length too large for 32-bit bucket ids";
     return RK_E_ARG;
   }
-  pl.nbins_p = (uint32_t)(pl.vsize - 1);
   pl.nbx = (uint32_t)(pl.max_x + 1);
   pl.nby = (uint32_t)(pl.max_y + 1);
-  pl.maxbins = std::max<uint64_t>(std::max<uint64_t>(pl.nbins_p, 2ull * pl.nbx),
-                                  std::max<uint64_t>(2ull * pl.nby, pl.n + 1));
   Work w;
   int rc = ensure_ws(ctx, pl, w);
   if (rc) return rc;
@@ -232,13 +273,14 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, 64 * sizeof(uint32_t), st));
   rk::fill_dropped(n, out->gid, out->repval, st);
   rk::Frags f{in->x_start, in->y_start, in->length, in->strand, n};
+  mark(ctx, RK_PH_PREP);
 
-  // 1-2: processing order
-  rk::prep_keys(f, pl.vsize, pl.max_x, pl.max_y, w.pkey, w.ctrl, st);
-  rk::counting_sort(w.pkey, n, pl.nbins_p, w.poff, w.p.row, w.cnt, w.tmp, ss, st);
+  // 1-2: processing order = stable sort of rows by xStart/10 (dropped bucket last)
+  rk::prep_keys(f, pl.vsize, pl.max_x, pl.max_y, w.pkey_in, w.ctrl + 1, w.ctrl, st);
+  mark(ctx, RK_PH_ORDER);
+  rk::radix_sort_pairs(w.pkey_in, nullptr, w.p.pkey, w.p.row, w.tk, w.tv, n,
+                       rk::bit_length(pl.vsize - 1), w.radix, w.radix_words, st);
   HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, hipMemcpyAsync(w.ctrl + 1, w.poff + pl.nbins_p, sizeof(uint32_t),
-                             hipMemcpyDeviceToDevice, st));
   if ((rc = readback(ctx, w.ctrl, 2))) return rc;
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
   const uint32_t m = ctx->host[1];
@@ -246,27 +288,41 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   out->n_out = m;
   out->n_groups = 0;
   if (m == 0) {
+    mark(ctx, RK_N_PHASES);
+    collect_phases(ctx);
     HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     return RK_OK;
   }
 
-  // 3-4: processing-order SoA and the two occupancy CSRs
-  rk::gather_proc(f, w.pkey, w.poff, w.p, m, pl.nbx, pl.nby, st);
-  rk::counting_sort(w.p.keyx, m, 2 * pl.nbx, w.xoff, w.xent, w.cnt, w.tmp, ss, st);
-  rk::counting_sort(w.p.keyy, m, 2 * pl.nby, w.yoff, w.yent, w.cnt, w.tmp, ss, st);
+  // 3: processing-order SoA, bucket keys, in-group sort keys
+  mark(ctx, RK_PH_GATHER);
+  rk::gather_proc(f, w.p, m, pl.nbx, pl.nby, st);
+
+  // 4: the two occupancy axes as bucket runs (stable: processing order inside)
+  mark(ctx, RK_PH_OCC_CSR);
+  rk::radix_sort_pairs(w.p.keyx, nullptr, w.cx.key, w.cx.ent, w.tk, w.tv, m,
+                       rk::bit_length(2ull * pl.nbx - 1), w.radix, w.radix_words, st);
+  rk::radix_sort_pairs(w.p.keyy, nullptr, w.cy.key, w.cy.ent, w.tk, w.tv, m,
+                       rk::bit_length(2ull * pl.nby - 1), w.radix, w.radix_words, st);
+  rk::csr_fill(w.cx, w.p.xc, w.p.len, nullptr, false, m, st);
   HIPCHK(ctx, hipGetLastError());
 
   // 5: X, then Y
-  rk::Axis ax{w.xoff, w.xent, w.p.xc, w.p.len, w.p.xstate, w.p.xwin, pl.max_x, pl.nbx,
+  mark(ctx, RK_PH_SWEEP_X);
+  rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, m, pl.max_x,
               prm->len_ratio, prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ax, w.p.keyx, w, m, 2 * pl.nbx, &ctx->stats.x_sweeps))) return rc;
-  rk::init_ystate(w.p, m, st);
-  rk::Axis ay{w.yoff, w.yent, w.p.yc, w.p.len, w.p.ystate, w.p.ywin, pl.max_y, pl.nby,
+  if ((rc = resolve_axis(ctx, ax, w, &ctx->stats.x_sweeps))) return rc;
+  rk::csr_scatter_back(w.cx, w.p.xstate, w.p.xwin, m, st);
+  mark(ctx, RK_PH_SWEEP_Y);
+  rk::csr_fill(w.cy, w.p.yc, w.p.len, w.p.xstate, true, m, st);
+  rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, m, pl.max_y,
               prm->len_ratio, prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ay, w.p.keyy, w, m, 2 * pl.nby, &ctx->stats.y_sweeps))) return rc;
+  if ((rc = resolve_axis(ctx, ay, w, &ctx->stats.y_sweeps))) return rc;
+  rk::csr_scatter_back(w.cy, w.p.ystate, w.p.ywin, m, st);
 
   // 6: group roots and ids
+  mark(ctx, RK_PH_ROOTS);
   rk::make_parents(w.p, m, w.isnew, w.ctrl, st);
   HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
   for (;;) {
@@ -287,14 +343,21 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   ctx->stats.n_groups = G;
   rk::assign_gid(w.p, m, w.newrank, st);
 
-  // 7-9: members, in-group order, flags
-  rk::counting_sort(w.p.gid, m, G, w.goff, w.gmem, w.cnt, w.tmp, ss, st);
+  // 7-9: members (stable by gid => processing order), in-group order, flags
+  mark(ctx, RK_PH_MEMBERS);
+  rk::radix_sort_pairs(w.p.gid, nullptr, w.sgid, w.gmem, w.tk, w.tv, m,
+                       rk::bit_length(G - 1), w.radix, w.radix_words, st);
+  rk::group_offsets(w.sgid, m, G, w.goff, st);
   rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
+  mark(ctx, RK_PH_GROUP_SORT);
   rk::sort_groups(w.goff, G, w.reckey, w.tag, st);
+  mark(ctx, RK_PH_EMIT);
   rk::emit_result(w.tag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval, out->out_order, st);
   HIPCHK(ctx, hipGetLastError());
+  mark(ctx, RK_N_PHASES);
   HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
   if ((rc = readback(ctx, w.ctrl, 1))) return rc;
+  collect_phases(ctx);
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
   float ms = 0;
   HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -324,6 +387,11 @@ extern "C" int rk_create(rk_ctx **out, int device) {
     rk_destroy(ctx);
     return RK_E_HIP;
   }
+  for (auto &e : ctx->pev)
+    if (hipEventCreate(&e) != hipSuccess) {
+    rk_destroy(ctx);
+    return RK_E_HIP;
+  }
   *out = ctx;
   return RK_OK;
 }
@@ -337,11 +405,38 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->host) (void)hipHostFree(ctx->host);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  for (auto &e : ctx->pev)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
 extern "C" const char *rk_last_error(const rk_ctx *ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+extern "C" int rk_set_profiling(rk_ctx *ctx, int enable) {
+  if (!ctx) return RK_E_ARG;
+  ctx->profiling = enable != 0;
+  return RK_OK;
+}
+
+extern "C" int rk_get_phase_ms(const rk_ctx *ctx, double *ms, uint32_t *calls) {
+  if (!ctx || !ms) return RK_E_ARG;
+  for (int i = 0; i < RK_N_PHASES; ++i) {
+    ms[i] = ctx->phase_ms[i];
+    if (calls) calls[i] = ctx->phase_calls[i];
+  }
+  return RK_OK;
+}
+
+extern "C" int rk_reset_phases(rk_ctx *ctx) {
+  if (!ctx) return RK_E_ARG;
+  for (int i = 0; i < RK_N_PHASES; ++i) ctx->phase_ms[i] = 0, ctx->phase_calls[i] = 0;
+  return RK_OK;
+}
+
+extern "C" const char *rk_phase_name(int phase) {
+  return phase >= 0 && phase < RK_N_PHASES ? kPhaseNames[phase] : "";
+}
 
 extern "C" int rk_get_stats(const rk_ctx *ctx, rk_stats *st) {
   if (!ctx || !st) return RK_E_ARG;

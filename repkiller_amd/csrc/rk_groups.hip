@@ -27,12 +27,6 @@
 namespace rk {
 namespace {
 
-inline unsigned grid_for(size_t n, int threads) {
-  size_t g = (n + threads - 1) / threads;
-  if (g > 65536) g = 65536;
-  return (unsigned)(g ? g : 1);
-}
-
 #define GRID_STRIDE(i, n)                                                      \
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n);           \
        i += gridDim.x * blockDim.x)
@@ -46,11 +40,12 @@ __device__ __forceinline__ uint64_t probe_max_bucket(uint64_t c, uint64_t max_in
 }
 
 __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t max_y,
-                            uint32_t *pkey, uint32_t *err) {
+                            uint32_t *pkey, uint32_t *kept, uint32_t *err) {
+  uint32_t mine = 0;
   GRID_STRIDE(i, f.n) {
     const uint64_t x = f.x[i];
     const uint64_t pk = x / 10;
-    uint32_t key = SKIP;
+    uint32_t key = (uint32_t)(vsize - 1);  // the never-iterated last bucket sorts last
     if (pk >= vsize) {
       atomicOr(err, ERRB_UB_BUCKET);
     } else if (pk != vsize - 1) {
@@ -58,32 +53,72 @@ __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t ma
       if (probe_max_bucket(x + h, max_x) > max_x || probe_max_bucket(f.y[i] + h, max_y) > max_y)
         atomicOr(err, ERRB_UB_CENTER);
       key = (uint32_t)pk;
+      ++mine;
     }
     pkey[i] = key;
   }
+  // one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off);
+  if ((threadIdx.x & 63) == 0 && mine) atomicAdd(kept, mine);
 }
 
-__global__ void k_gather_proc(Frags f, const uint32_t *pkey, const uint32_t *poff, Proc p,
-                              uint32_t m, uint32_t nbx, uint32_t nby) {
+__global__ void k_gather_proc(Frags f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
   GRID_STRIDE(k, m) {
     const uint32_t r = p.row[k];
     const uint64_t L = f.len[r], x = f.x[r], y = f.y[r];
     const uint64_t xc = x + L / 2, yc = y + L / 2;
     const uint32_t s = f.strand[r] == 'f' ? 0u : 1u;
-    const uint32_t last = p.row[poff[pkey[r] + 1] - 1];  // last fragment of the xStart/10 bucket
-    const uint64_t d = f.y[last];
     p.xc[k] = xc;
     p.yc[k] = yc;
     p.len[k] = L;
-    p.ha[k] = y > d ? y - d : d - y;
     p.keyx[k] = s * nbx + (uint32_t)(xc / 100);
     p.keyy[k] = s * nby + (uint32_t)(yc / 100);
-    p.xstate[k] = ST_UNKNOWN;
   }
 }
 
-__global__ void k_init_ystate(Proc p, uint32_t m) {
-  GRID_STRIDE(k, m) p.ystate[k] = p.xstate[k] == ST_HIT ? ST_ACTIVE : ST_UNKNOWN;
+// In-group sort key |yStart - diag_func[xStart/10]|: diag_func[b] is the yStart
+// of the LAST fragment of processing bucket b.  The thread at each run end of
+// the sorted processing keys fills its whole run (each element written once).
+__global__ void k_diag_keys(Proc p, uint32_t m) {
+  GRID_STRIDE(k, m) {
+    const uint32_t key = p.pkey[k];
+    if (k + 1 < m && p.pkey[k + 1] == key) continue;
+    const uint64_t d = p.yc[k] - p.len[k] / 2;  // yStart of the last fragment
+    uint32_t j = k;
+    for (;;) {
+      const uint64_t y = p.yc[j] - p.len[j] / 2;
+      p.ha[j] = y > d ? y - d : d - y;
+      if (j == 0 || p.pkey[j - 1] != key) break;
+      --j;
+    }
+  }
+}
+
+__global__ void k_csr_fill(Csr c, const uint64_t *cen, const uint64_t *len,
+                           const uint8_t *xstate, bool for_y, uint32_t m) {
+  GRID_STRIDE(q, m) {
+    const uint32_t k = c.ent[q];
+    c.cen[q] = cen[k];
+    c.len[q] = len[k];
+    c.state[q] = for_y && xstate[k] == ST_HIT ? ST_ACTIVE : ST_UNKNOWN;
+  }
+}
+
+__global__ void k_csr_scatter_back(Csr c, uint8_t *state, uint32_t *win, uint32_t m) {
+  GRID_STRIDE(q, m) {
+    const uint32_t k = c.ent[q];
+    const uint8_t st = c.state[q];
+    state[k] = st;
+    if (st == ST_HIT) win[k] = c.win[q];
+  }
+}
+
+__global__ void k_group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups,
+                                uint32_t *goff) {
+  GRID_STRIDE(q, m) {
+    if (q == 0 || sgid[q] != sgid[q - 1]) goff[sgid[q]] = q;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) goff[ngroups] = m;
 }
 
 __global__ void k_make_parents(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err) {
@@ -274,15 +309,24 @@ __global__ void k_emit(const uint32_t *tag, const uint32_t *gid_proc, const uint
 }  // namespace
 
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
-               uint32_t *err, hipStream_t st) {
-  if (f.n) k_prep_keys<<<grid_for(f.n, 256), 256, 0, st>>>(f, vsize, max_x, max_y, pkey, err);
+               uint32_t *kept, uint32_t *err, hipStream_t st) {
+  if (f.n) k_prep_keys<<<grid_for(f.n, 256), 256, 0, st>>>(f, vsize, max_x, max_y, pkey, kept, err);
 }
-void gather_proc(const Frags &f, const uint32_t *pkey, const uint32_t *poff, Proc p, uint32_t m,
-                 uint32_t nbx, uint32_t nby, hipStream_t st) {
-  if (m) k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(f, pkey, poff, p, m, nbx, nby);
+void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st) {
+  if (!m) return;
+  k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(f, p, m, nbx, nby);
+  k_diag_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m);
 }
-void init_ystate(Proc p, uint32_t m, hipStream_t st) {
-  if (m) k_init_ystate<<<grid_for(m, 256), 256, 0, st>>>(p, m);
+void csr_fill(Csr c, const uint64_t *cen, const uint64_t *len, const uint8_t *xstate, bool for_y,
+              uint32_t m, hipStream_t st) {
+  if (m) k_csr_fill<<<grid_for(m, 256), 256, 0, st>>>(c, cen, len, xstate, for_y, m);
+}
+void csr_scatter_back(Csr c, uint8_t *state, uint32_t *win, uint32_t m, hipStream_t st) {
+  if (m) k_csr_scatter_back<<<grid_for(m, 256), 256, 0, st>>>(c, state, win, m);
+}
+void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
+                   hipStream_t st) {
+  k_group_offsets<<<grid_for(m, 256), 256, 0, st>>>(sgid, m, ngroups, goff);
 }
 void make_parents(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, hipStream_t st) {
   if (m) k_make_parents<<<grid_for(m, 256), 256, 0, st>>>(p, m, isnew, err);

@@ -1,7 +1,8 @@
 // rk_internal.h -- shared declarations of the device pipeline (not part of
-// the public C ABI).  Kernels live in rk_sort.hip / rk_occupancy.hip /
-// rk_groups.hip; each TU exports host-side launchers only, so no relocatable
-// device code is needed.
+// the public C ABI).  Kernels live in rk_sort.hip (scan), rk_radix.hip (stable
+// radix sort), rk_occupancy.hip (bucket sweeps) and rk_groups.hip (processing
+// order, groups, in-group order); each TU exports host-side launchers only, so
+// no relocatable device code is needed.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -16,52 +17,59 @@ enum : uint8_t {
   ST_HIT = 3,          // hit on this axis; winner final
 };
 
-// device error bits (ctx->err word)
+// device error bits (ctrl[0])
 enum : uint32_t {
   ERRB_UB_BUCKET = 1u,
   ERRB_UB_CENTER = 2u,
   ERRB_INTERNAL = 4u,
 };
 
-constexpr uint32_t SKIP = 0xFFFFFFFFu;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
+inline unsigned grid_for(size_t n, int threads, size_t cap = 65536) {
+  size_t g = (n + threads - 1) / threads;
+  if (g > cap) g = cap;
+  return (unsigned)(g ? g : 1);
+}
+
+inline int bit_length(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
+
 // ------------------------------------------------------------ rk_sort.hip --
-// Stable counting sort of indices [0, m) by key[i] in [0, nbins) (key SKIP =
-// leave out).  Histogram (LDS-privatised when a block's keys span a narrow
-// window), DPP wave scan -> block -> device exclusive scan, atomic scatter and
-// an in-bin rank fix that restores ascending index order inside every bin.
-//   off  : nbins + 1 entries (off[nbins] = number kept)
-//   perm : kept indices, bin-major, ascending inside a bin
-//   scratch_cnt : nbins + 1 u32;  scratch_tmp : m u32
+// Device-wide exclusive scan of u32 (DPP wave scan -> block -> tiles).
 struct ScanScratch {
-  uint32_t *block_sums;  // >= scan_blocks(n) + 1
+  uint32_t *block_sums;
   size_t cap;
 };
 size_t scan_blocks(size_t n);
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
                         hipStream_t st);
-void counting_sort(const uint32_t *key, uint32_t m, uint32_t nbins, uint32_t *off, uint32_t *perm,
-                   uint32_t *scratch_cnt, uint32_t *scratch_tmp, ScanScratch ss, hipStream_t st);
-// list of non-empty bins, in no particular order; count -> *d_count
-void nonempty_bins(const uint32_t *key, const uint32_t *perm, const uint32_t *off, uint32_t nbins,
-                   uint32_t m, uint32_t *list, uint32_t *d_count, hipStream_t st);
+
+// ----------------------------------------------------------- rk_radix.hip --
+size_t radix_scratch_words(uint32_t n);
+// stable sort of (key, value) by the low `bits` bits of key; val_in null =>
+// values are input positions.  Inputs must not alias outputs or tmp buffers.
+void radix_sort_pairs(const uint32_t *key_in, const uint32_t *val_in, uint32_t *key_out,
+                      uint32_t *val_out, uint32_t *key_tmp, uint32_t *val_tmp, uint32_t n,
+                      int bits, uint32_t *scratch, size_t scratch_words, hipStream_t st);
 
 // ------------------------------------------------------- rk_occupancy.hip --
-struct Axis {
-  const uint32_t *off;   // bucket CSR offsets, 2 * nbs + 1
-  const uint32_t *ent;   // bucket entries (processing indices, ascending per bucket)
-  const uint64_t *cen;   // centre per processing index
-  const uint64_t *len;   // length per processing index
-  uint8_t *state;        // ST_* per processing index
-  uint32_t *win;         // winner per processing index (valid when ST_HIT)
-  uint64_t max_index;    // seq_size / 100 (SequenceOcupationList.cpp:4)
-  uint32_t nbs;          // buckets per strand = max_index + 1
+struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
+  const uint32_t *key; // bucket key strand * nbs + centre/100, sorted
+  const uint32_t *ent; // processing index of the entry (ascending inside a run)
+  const uint64_t *cen; // centre
+  const uint64_t *len; // length
+  uint8_t *state;      // ST_*
+  uint32_t *win;       // winner's processing index (valid when ST_HIT)
+  uint32_t m;          // entries
+  uint64_t max_index;  // seq_size / 100 (SequenceOcupationList.cpp:4)
   double len_ratio, pos_ratio;
 };
-// one Gauss-Seidel sweep over the buckets in `work`; buckets that still hold
-// undecided entries are appended to next_work (count in *next_count, which the
-// caller zeroes).  big_work/big_count: scratch for the wavefront-per-bucket path.
+// list the run starts of a sorted key array (work items for the first sweep)
+void run_starts(const uint32_t *key, uint32_t m, uint32_t *list, uint32_t *count,
+                hipStream_t st);
+// one sweep over the runs in `work`; runs that keep undecided entries are
+// appended to next_work (*next_count zeroed by the caller).  big_work /
+// big_count: scratch for the wavefront-per-run path.
 void occupancy_sweep(const Axis &ax, const uint32_t *work, uint32_t nwork, uint32_t *next_work,
                      uint32_t *next_count, uint32_t *big_work, uint32_t *big_count,
                      hipStream_t st);
@@ -73,21 +81,34 @@ struct Frags {  // file-order inputs
   uint32_t n;
 };
 struct Proc {  // processing-order working set
-  uint32_t *row;          // proc -> file row
+  uint32_t *pkey;  // sorted xStart/10 key
+  uint32_t *row;   // proc -> file row
   uint64_t *xc, *yc, *len, *ha;
   uint32_t *keyx, *keyy;
   uint8_t *xstate, *ystate;
   uint32_t *xwin, *ywin;
   uint32_t *par, *gid;
 };
+struct Csr {  // one axis in CSR order (see Axis)
+  uint32_t *key, *ent;
+  uint64_t *cen, *len;
+  uint8_t *state;
+  uint32_t *win;
+};
+// processing key per file row (dropped last bucket -> vsize-1, sorts last);
+// counts kept rows into *kept; flags UB into *err
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
-               uint32_t *err, hipStream_t st);
-void gather_proc(const Frags &f, const uint32_t *pkey, const uint32_t *poff, Proc p, uint32_t m,
-                 uint32_t nbx, uint32_t nby, hipStream_t st);
-void init_ystate(Proc p, uint32_t m, hipStream_t st);
+               uint32_t *kept, uint32_t *err, hipStream_t st);
+void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
+// centre/length/state in CSR order; for_y: state from the X result
+void csr_fill(Csr c, const uint64_t *cen, const uint64_t *len, const uint8_t *xstate, bool for_y,
+              uint32_t m, hipStream_t st);
+void csr_scatter_back(Csr c, uint8_t *state, uint32_t *win, uint32_t m, hipStream_t st);
 void make_parents(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, hipStream_t st);
 void jump_round(Proc p, uint32_t m, uint32_t *changed, hipStream_t st);
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st);
+void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
+                   hipStream_t st);
 void build_records(const uint32_t *gmem, const uint64_t *ha, uint32_t m, uint64_t *key,
                    uint32_t *tag, hipStream_t st);
 void sort_groups(const uint32_t *goff, uint32_t ngroups, uint64_t *key, uint32_t *tag,

@@ -1,0 +1,132 @@
+// rk_radix.hip -- stable LSD radix sort of (u32 key, u32 value) pairs (gfx950).
+//
+// Every bucketed structure of the reference becomes a sorted array here: the
+// xStart/10 processing buckets (FragmentsDatabase.cpp:84-97, stable in file
+// order), the 100-bp occupancy buckets (SequenceOcupationList.cpp:5-7,17,95,
+// entries in insertion order) and the group member lists (commonFunctions.cpp:
+// 58,66,73, members in insertion order).  All three need a STABLE sort by a
+// small integer key, which is what LSD radix gives without atomics.
+//
+// One pass per 8-bit digit, three kernels:
+//   k_digit_hist   256-bin histogram of each 4096-key tile in LDS (LDS atomics),
+//                  written digit-major: counts[digit * tiles + tile]
+//   exclusive scan over counts (rk_sort.hip, DPP wave scan)
+//   k_digit_scatter  re-reads the tile in index order, ranks every key among
+//                  equal digits (8 wave ballots -> peer mask -> popcount; wave
+//                  totals through LDS in wave order), scatters key and value.
+// Tiles: 256 threads x 16 keys; key i of the tile is read as round i/256,
+// thread i%256 -- coalesced, and rank order == index order (stability).
+#include "rk_internal.h"
+
+namespace rk {
+namespace {
+
+constexpr int RT = 256;             // threads per block
+constexpr int RITEMS = 16;          // keys per thread
+constexpr int RTILE = RT * RITEMS;  // 4096 keys per tile
+constexpr int RADIX = 256;
+
+__global__ void __launch_bounds__(RT) k_digit_hist(const uint32_t *__restrict__ key, uint32_t n,
+                                                   int shift, uint32_t tiles,
+                                                   uint32_t *__restrict__ counts) {
+  __shared__ uint32_t hist[RADIX];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * (uint32_t)RTILE;
+#pragma unroll
+  for (int r = 0; r < RITEMS; ++r) {
+    const uint32_t i = base + r * RT + threadIdx.x;
+    if (i < n) atomicAdd(&hist[(key[i] >> shift) & (RADIX - 1)], 1u);
+  }
+  __syncthreads();
+  counts[threadIdx.x * tiles + blockIdx.x] = hist[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(RT) k_digit_scatter(const uint32_t *__restrict__ key_in,
+                                                      const uint32_t *__restrict__ val_in,
+                                                      uint32_t n, int shift, uint32_t tiles,
+                                                      const uint32_t *__restrict__ offs,
+                                                      uint32_t *__restrict__ key_out,
+                                                      uint32_t *__restrict__ val_out) {
+  __shared__ uint32_t base[RADIX];
+  __shared__ uint32_t wcount[RT / 64][RADIX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  base[threadIdx.x] = offs[threadIdx.x * tiles + blockIdx.x];
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t tile0 = blockIdx.x * (uint32_t)RTILE;
+  for (int r = 0; r < RITEMS; ++r) {
+#pragma unroll
+    for (int k = 0; k < RT / 64; ++k) wcount[k][threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = tile0 + r * RT + threadIdx.x;
+    const bool live = i < n;
+    uint32_t k = 0, v = 0, d = 0;
+    if (live) {
+      k = key_in[i];
+      v = val_in ? val_in[i] : i;
+      d = (k >> shift) & (RADIX - 1);
+    }
+    uint64_t peer = __ballot(live);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peer &= bit ? bb : ~bb;
+    }
+    const uint32_t wrank = __popcll(peer & lt);
+    if (live && wrank == 0) wcount[w][d] = __popcll(peer);
+    __syncthreads();
+    if (live) {
+      uint32_t pos = base[d] + wrank;
+      for (int k2 = 0; k2 < w; ++k2) pos += wcount[k2][d];
+      key_out[pos] = k;
+      val_out[pos] = v;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int k2 = 0; k2 < RT / 64; ++k2) add += wcount[k2][threadIdx.x];
+    base[threadIdx.x] += add;
+  }
+}
+
+}  // namespace
+
+size_t radix_scratch_words(uint32_t n) {
+  const size_t tiles = (n + RTILE - 1) / RTILE;
+  const size_t cnt = tiles * RADIX + 1;
+  return ((cnt + 3) & ~(size_t)3) + scan_blocks(cnt) + 64;
+}
+
+// Sorts by the low `bits` bits of key.  key_in/val_in are not modified unless
+// they alias the ping-pong buffers; the result lands in key_out/val_out.
+// key_tmp/val_tmp: n-word ping-pong buffers.  val_in == nullptr => values are
+// the input positions 0..n-1.
+void radix_sort_pairs(const uint32_t *key_in, const uint32_t *val_in, uint32_t *key_out,
+                      uint32_t *val_out, uint32_t *key_tmp, uint32_t *val_tmp, uint32_t n,
+                      int bits, uint32_t *scratch, size_t scratch_words, hipStream_t st) {
+  if (n == 0) return;
+  if (bits < 1) bits = 1;
+  const int passes = (bits + 7) / 8;
+  const uint32_t tiles = (n + RTILE - 1) / RTILE;
+  const size_t cnt = (size_t)tiles * RADIX + 1;
+  uint32_t *counts = scratch;
+  ScanScratch ss{scratch + ((cnt + 3) & ~(size_t)3),
+                 scratch_words - ((cnt + 3) & ~(size_t)3)};
+  // ping-pong so that the last pass writes key_out/val_out
+  const uint32_t *ki = key_in, *vi = val_in;
+  for (int p = 0; p < passes; ++p) {
+    const bool last = p == passes - 1;
+    // pass p writes out when (passes-1-p) is even, tmp otherwise
+    uint32_t *ko = ((passes - 1 - p) % 2 == 0) ? key_out : key_tmp;
+    uint32_t *vo = ((passes - 1 - p) % 2 == 0) ? val_out : val_tmp;
+    (void)last;
+    k_digit_hist<<<tiles, RT, 0, st>>>(ki, n, 8 * p, tiles, counts);
+    exclusive_scan_u32(counts, counts, (size_t)tiles * RADIX, ss, st);
+    k_digit_scatter<<<tiles, RT, 0, st>>>(ki, vi, n, 8 * p, tiles, counts, ko, vo);
+    ki = ko;
+    vi = vo;
+  }
+}
+
+}  // namespace rk

@@ -1,11 +1,8 @@
-// rk_sort.hip -- device exclusive scan and stable counting sort (gfx950).
+// rk_sort.hip -- device-wide exclusive scan of u32 (gfx950).
 //
-// These are the "coverage histogram + scan" kernels of the design: every
-// bucketed structure of the reference -- the xStart/10 processing buckets of
-// FragmentsDatabase (FragmentsDatabase.cpp:84-97), the 100-bp occupancy
-// buckets of SequenceOcupationList (SequenceOcupationList.cpp:5-7,17) and the
-// FragsGroup member lists (commonFunctions.cpp:58,66,73) -- becomes a CSR
-// built by: histogram -> exclusive scan -> scatter -> in-bin rank fix.
+// Used by the radix sort (digit offsets, rk_radix.hip) and for the new-group
+// ranks (gid = exclusive scan of "opens a group" flags in processing order,
+// the creation order of commonFunctions.cpp:72-74).
 //
 // Scan: 256-thread blocks, 4096 u32 per tile (4 rows of 1024; each row one
 // coalesced uint4 per lane), wave inclusive scan in DPP (row_shr 1/2/4/8 then
@@ -110,52 +107,6 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const uint32_t *in,
   }
 }
 
-__global__ void k_hist(const uint32_t *key, uint32_t m, uint32_t *cnt) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-    uint32_t k = key[i];
-    if (k != SKIP) atomicAdd(&cnt[k], 1u);
-  }
-}
-
-__global__ void k_scatter(const uint32_t *key, uint32_t m, uint32_t *cursor, uint32_t *tmp) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-    uint32_t k = key[i];
-    if (k != SKIP) tmp[atomicAdd(&cursor[k], 1u)] = i;
-  }
-}
-
-// Restore ascending index order inside every bin: the element at scattered
-// slot p moves to off[k] + (#bin members with a smaller index).
-__global__ void k_rankfix(const uint32_t *key, const uint32_t *off, uint32_t nbins,
-                          const uint32_t *tmp, uint32_t *perm) {
-  const uint32_t total = off[nbins];
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total;
-       p += gridDim.x * blockDim.x) {
-    uint32_t i = tmp[p];
-    uint32_t k = key[i];
-    uint32_t b = off[k], e = off[k + 1];
-    uint32_t r = 0;
-    for (uint32_t q = b; q < e; ++q) r += tmp[q] < i;
-    perm[b + r] = i;
-  }
-}
-
-__global__ void k_nonempty(const uint32_t *key, const uint32_t *perm, const uint32_t *off,
-                           uint32_t nbins, uint32_t *list, uint32_t *count) {
-  const uint32_t total = off[nbins];
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total;
-       p += gridDim.x * blockDim.x) {
-    uint32_t k = key[perm[p]];
-    if (off[k] == p) list[atomicAdd(count, 1u)] = k;
-  }
-}
-
-inline unsigned grid_for(size_t n, int threads) {
-  size_t g = (n + threads - 1) / threads;
-  if (g > 65536) g = 65536;
-  return (unsigned)(g ? g : 1);
-}
-
 }  // namespace
 
 size_t scan_blocks(size_t n) {
@@ -181,25 +132,6 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch
   k_reduce_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, n, sums);
   exclusive_scan_u32(sums, sums, nb, rest, st);
   k_scan_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, out, n, sums);
-}
-
-void counting_sort(const uint32_t *key, uint32_t m, uint32_t nbins, uint32_t *off, uint32_t *perm,
-                   uint32_t *cnt, uint32_t *tmp, ScanScratch ss, hipStream_t st) {
-  (void)hipMemsetAsync(cnt, 0, ((size_t)nbins + 1) * sizeof(uint32_t), st);
-  if (m) k_hist<<<grid_for(m, 256), 256, 0, st>>>(key, m, cnt);
-  exclusive_scan_u32(cnt, off, (size_t)nbins + 1, ss, st);
-  (void)hipMemcpyAsync(cnt, off, ((size_t)nbins + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
-  if (m) {
-    k_scatter<<<grid_for(m, 256), 256, 0, st>>>(key, m, cnt, tmp);
-    // kept count is off[nbins] (device value): the kernel bounds itself by it
-    k_rankfix<<<grid_for(m, 256), 256, 0, st>>>(key, off, nbins, tmp, perm);
-  }
-}
-
-void nonempty_bins(const uint32_t *key, const uint32_t *perm, const uint32_t *off, uint32_t nbins,
-                   uint32_t m, uint32_t *list, uint32_t *d_count, hipStream_t st) {
-  (void)hipMemsetAsync(d_count, 0, sizeof(uint32_t), st);
-  if (m) k_nonempty<<<grid_for(m, 256), 256, 0, st>>>(key, perm, off, nbins, list, d_count);
 }
 
 }  // namespace rk
