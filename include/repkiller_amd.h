@@ -99,6 +99,13 @@ int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params 
 
 int rk_get_stats(const rk_ctx *ctx, rk_stats *st);
 
+/* The in-group ordering primitive on its own: libstdc++ 11 std::sort (the
+ * exact permutation, ties included -- commonFunctions.cpp:158) of every
+ * segment [seg_off[s], seg_off[s+1]) of `keys`, on the device.  perm[x] =
+ * index (into keys) of the element that ends at position x.  Host buffers. */
+int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t n, const uint32_t *seg_off,
+                         uint32_t nseg, uint32_t *perm);
+
 /* Phase profiling: when enabled, HIP events are recorded on the context
  * stream at every phase boundary of rk_classify*; rk_get_phase_ms returns the
  * accumulated device milliseconds (and call counts) per phase. */

@@ -41,7 +41,7 @@ STATUS = {
 # every symbol include/repkiller_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "rk_create", "rk_destroy", "rk_last_error", "rk_classify", "rk_classify_device",
-    "rk_get_stats", "rk_set_profiling", "rk_get_phase_ms", "rk_reset_phases", "rk_phase_name",
+    "rk_get_stats", "rk_std_sort_segments", "rk_set_profiling", "rk_get_phase_ms", "rk_reset_phases", "rk_phase_name",
     "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
     "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
     "rk_synth_write_csv",
@@ -119,6 +119,8 @@ def load_library() -> ctypes.CDLL:
                                               ctypes.POINTER(Params), ctypes.POINTER(Result)]),
         "rk_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(Stats)]),
         "rk_set_profiling": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rk_std_sort_segments": (ctypes.c_int, [vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32,
+                                                vp]),
         "rk_get_phase_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), _u32p]),
         "rk_reset_phases": (ctypes.c_int, [vp]),
         "rk_phase_name": (ctypes.c_char_p, [ctypes.c_int]),
@@ -322,6 +324,17 @@ class Context:
         calls = (ctypes.c_uint32 * N_PHASES)()
         _check(lib.rk_get_phase_ms(self._h, ms, calls))
         return {lib.rk_phase_name(i).decode(): (ms[i], calls[i]) for i in range(N_PHASES)}
+
+    def std_sort_segments(self, keys: np.ndarray, seg_off: np.ndarray) -> np.ndarray:
+        """libstdc++ std::sort permutation of every segment of `keys`, on the GPU."""
+        k = np.ascontiguousarray(keys, np.uint64)
+        off = np.ascontiguousarray(seg_off, np.uint32)
+        perm = np.empty(k.shape[0], np.uint32)
+        rc = load_library().rk_std_sort_segments(self._h, _ptr(k), k.shape[0], _ptr(off),
+                                                 off.shape[0] - 1, _ptr(perm))
+        if rc != RK_OK:
+            raise RkError(rc, self.last_error())
+        return perm
 
     def classify(self, f: Frags, len_x_hdr: int, len_y_hdr: int, len_ratio: float = 0.3,
                  pos_ratio: float = 0.3) -> ClassifyResult:

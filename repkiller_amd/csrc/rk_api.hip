@@ -88,16 +88,17 @@ struct Work {
   size_t radix_words;
   rk::Proc p;
   rk::Csr cx, cy;
-  uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag;
+  uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag, *otag;
+  void *gsort;
   uint64_t *reckey;
-  uint32_t *workA, *workB, *big;
+  uint32_t *rpend, *rbeg, *rlen, *runs, *rlen_at, *rbeg_at;
   uint32_t *scan;
   size_t scan_cap;
 };
 
 size_t carve(Carve &c, const Plan &pl, Work &w) {
   const size_t n = pl.n + 1;
-  w.ctrl = c.take<uint32_t>(64);
+  w.ctrl = c.take<uint32_t>(64 + rk::PEND_WORDS);
   w.pkey_in = c.take<uint32_t>(n);
   w.tk = c.take<uint32_t>(n);
   w.tv = c.take<uint32_t>(n);
@@ -105,9 +106,8 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.radix = c.take<uint32_t>(w.radix_words);
   w.p.pkey = c.take<uint32_t>(n);
   w.p.row = c.take<uint32_t>(n);
-  w.p.xc = c.take<uint64_t>(n);
-  w.p.yc = c.take<uint64_t>(n);
-  w.p.len = c.take<uint64_t>(n);
+  w.p.xrec = c.take<ulonglong2>(n);
+  w.p.yrec = c.take<ulonglong2>(n);
   w.p.ha = c.take<uint64_t>(n);
   w.p.keyx = c.take<uint32_t>(n);
   w.p.keyy = c.take<uint32_t>(n);
@@ -131,10 +131,15 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.gmem = c.take<uint32_t>(n);
   w.goff = c.take<uint32_t>(n);
   w.tag = c.take<uint32_t>(n);
+  w.otag = c.take<uint32_t>(n);
+  w.gsort = c.take<uint8_t>(rk::groupsort_scratch_bytes((uint32_t)n));
   w.reckey = c.take<uint64_t>(n);
-  w.workA = c.take<uint32_t>(n);
-  w.workB = c.take<uint32_t>(n);
-  w.big = c.take<uint32_t>(n);
+  w.rpend = c.take<uint32_t>(n / 4 + 1);
+  w.rbeg = c.take<uint32_t>(n);
+  w.rlen = c.take<uint32_t>(n);
+  w.runs = c.take<uint32_t>(rk::runs_scratch_words((uint32_t)n));
+  w.rlen_at = c.take<uint32_t>(n);
+  w.rbeg_at = c.take<uint32_t>(n);
   w.scan_cap = rk::scan_blocks(n + 1) + 64;
   w.scan = c.take<uint32_t>(w.scan_cap);
   return c.off;
@@ -210,27 +215,29 @@ int err_status(rk_ctx *ctx, uint32_t bits) {
 }
 
 // run sweeps on one axis until no bucket has undecided entries
-int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, uint32_t *sweeps) {
-  uint32_t *cnt_dev = w.ctrl + 2, *next_dev = w.ctrl + 3, *big_dev = w.ctrl + 4;
-  rk::run_starts(ax.key, ax.m, w.workA, cnt_dev, ctx->stream);
-  int rc = readback(ctx, cnt_dev, 1);
-  if (rc) return rc;
-  uint32_t nwork = ctx->host[0];
-  uint32_t *cur = w.workA, *nxt = w.workB;
+int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss,
+                 uint32_t *sweeps) {
+  uint32_t *counters = w.ctrl + 64;
+  uint8_t *rpend = reinterpret_cast<uint8_t *>(w.rpend);
+  rk::RunList rl{w.rbeg, w.rlen, 0, 0};
+  rk::build_runs(ax, rl, w.runs, w.tk, w.tv, w.radix, w.radix_words, ss, w.ctrl + 2,
+                 ctx->host + 128, ctx->stream);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));
   *sweeps = 0;
-  while (nwork) {
+  for (;;) {
     if (*sweeps > ax.m + 2) {
       ctx->err = "occupancy sweeps did not converge";
       return RK_E_INTERNAL;
     }
-    HIPCHK(ctx, hipMemsetAsync(next_dev, 0, sizeof(uint32_t), ctx->stream));
-    rk::occupancy_sweep(ax, cur, nwork, nxt, next_dev, w.big, big_dev, ctx->stream);
+    rk::occupancy_sweep(ax, rl, rpend, counters, ctx->stream);
     HIPCHK(ctx, hipGetLastError());
-    rc = readback(ctx, next_dev, 1);
-    if (rc) return rc;
-    nwork = ctx->host[0];
-    std::swap(cur, nxt);
     ++*sweeps;
+    int rc = readback(ctx, counters, rk::PEND_WORDS);
+    if (rc) return rc;
+    uint64_t pending = 0;
+    for (uint32_t k = 0; k < rk::PEND_WORDS; ++k) pending += ctx->host[k];
+    if (!pending) break;
   }
   return RK_OK;
 }
@@ -270,7 +277,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   ctx->stats.n_in = n;
 
   HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
-  HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, 64 * sizeof(uint32_t), st));
+  HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));
   rk::fill_dropped(n, out->gid, out->repval, st);
   rk::Frags f{in->x_start, in->y_start, in->length, in->strand, n};
   mark(ctx, RK_PH_PREP);
@@ -305,20 +312,22 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
                        rk::bit_length(2ull * pl.nbx - 1), w.radix, w.radix_words, st);
   rk::radix_sort_pairs(w.p.keyy, nullptr, w.cy.key, w.cy.ent, w.tk, w.tv, m,
                        rk::bit_length(2ull * pl.nby - 1), w.radix, w.radix_words, st);
-  rk::csr_fill(w.cx, w.p.xc, w.p.len, nullptr, false, m, st);
+  rk::csr_fill(w.cx, w.p.xrec, nullptr, false, m, st);
   HIPCHK(ctx, hipGetLastError());
 
   // 5: X, then Y
   mark(ctx, RK_PH_SWEEP_X);
-  rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, m, pl.max_x,
+  rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, w.rlen_at,
+              w.rbeg_at, m, pl.max_x,
               prm->len_ratio, prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ax, w, &ctx->stats.x_sweeps))) return rc;
+  if ((rc = resolve_axis(ctx, ax, w, ss, &ctx->stats.x_sweeps))) return rc;
   rk::csr_scatter_back(w.cx, w.p.xstate, w.p.xwin, m, st);
   mark(ctx, RK_PH_SWEEP_Y);
-  rk::csr_fill(w.cy, w.p.yc, w.p.len, w.p.xstate, true, m, st);
-  rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, m, pl.max_y,
+  rk::csr_fill(w.cy, w.p.yrec, w.p.xstate, true, m, st);
+  rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.rlen_at,
+              w.rbeg_at, m, pl.max_y,
               prm->len_ratio, prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ay, w, &ctx->stats.y_sweeps))) return rc;
+  if ((rc = resolve_axis(ctx, ay, w, ss, &ctx->stats.y_sweeps))) return rc;
   rk::csr_scatter_back(w.cy, w.p.ystate, w.p.ywin, m, st);
 
   // 6: group roots and ids
@@ -350,9 +359,11 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   rk::group_offsets(w.sgid, m, G, w.goff, st);
   rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
   mark(ctx, RK_PH_GROUP_SORT);
-  rk::sort_groups(w.goff, G, w.reckey, w.tag, st);
+  rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
+                        ctx->host + 128, st);
   mark(ctx, RK_PH_EMIT);
-  rk::emit_result(w.tag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval, out->out_order, st);
+  rk::emit_result(w.otag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval, out->out_order,
+                  st);
   HIPCHK(ctx, hipGetLastError());
   mark(ctx, RK_N_PHASES);
   HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
@@ -382,7 +393,7 @@ extern "C" int rk_create(rk_ctx **out, int device) {
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
-      hipHostMalloc((void **)&ctx->host, 64 * sizeof(uint32_t), hipHostMallocDefault) !=
+      hipHostMalloc((void **)&ctx->host, 256 * sizeof(uint32_t), hipHostMallocDefault) !=
           hipSuccess) {
     rk_destroy(ctx);
     return RK_E_HIP;
@@ -454,6 +465,50 @@ extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const
     ctx->err = "unexpected C++ exception";
     return RK_E_INTERNAL;
   }
+}
+
+extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t n,
+                                    const uint32_t *seg_off, uint32_t nseg, uint32_t *perm) {
+  if (!ctx || (n && (!keys || !perm)) || !seg_off || n >= 0xFFFFFFFFull) return RK_E_ARG;
+  if (seg_off[0] != 0 || seg_off[nseg] != n) return RK_E_ARG;
+  for (uint32_t s = 0; s < nseg; ++s)
+    if (seg_off[s + 1] <= seg_off[s]) return RK_E_ARG;  // segments must be non-empty
+  if (!n) return RK_OK;
+  ctx->err.clear();
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const uint32_t m = (uint32_t)n;
+  std::vector<uint32_t> sg(m), tags(m);
+  for (uint32_t s = 0; s < nseg; ++s)
+    for (uint32_t x = seg_off[s]; x < seg_off[s + 1]; ++x) sg[x] = s, tags[x] = x;
+  const size_t gs = rk::groupsort_scratch_bytes(m), sc = rk::scan_blocks(nseg + 2) + 64;
+  const size_t bytes = align_up(m * 8 + 16) + align_up(m * 4 + 16) * 3 +
+                       align_up((nseg + 1) * 4 + 16) + align_up(gs) + align_up(sc * 4);
+  void *buf = nullptr;
+  HIPCHK(ctx, hipMalloc(&buf, bytes));
+  Carve c{(char *)buf};
+  uint64_t *dk = c.take<uint64_t>(m);
+  uint32_t *dt = c.take<uint32_t>(m), *dot = c.take<uint32_t>(m), *dg = c.take<uint32_t>(m);
+  uint32_t *doff = c.take<uint32_t>(nseg + 1);
+  void *dgs = c.take<uint8_t>(gs);
+  uint32_t *dsc = c.take<uint32_t>(sc);
+  hipStream_t st = ctx->stream;
+  int rc = RK_OK;
+  if (hipMemcpyAsync(dk, keys, m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dt, tags.data(), m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dg, sg.data(), m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(doff, seg_off, (nseg + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+    rc = RK_E_HIP;
+  } else {
+    rk::sort_groups_exact(dg, doff, nseg, m, dk, dt, dot, dgs, rk::ScanScratch{dsc, sc},
+                          ctx->host + 128, st);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(perm, dot, m * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      rc = RK_E_HIP;
+  }
+  (void)hipFree(buf);
+  if (rc) ctx->err = "rk_std_sort_segments: HIP failure";
+  return rc;
 }
 
 extern "C" int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p,

@@ -1,0 +1,425 @@
+// rk_groupsort.hip -- sort_groups (commonFunctions.cpp:148-159) on gfx950.
+//
+// The reference std::sort()s every group with more than one member by
+// |yStart - diag_func[xStart/10]|.  std::sort is libstdc++'s unstable introsort
+// and the keys have many ties, so the exact permutation -- which member is
+// written first and gets repeat flag 1 -- depends on every median-of-three
+// choice and every Hoare swap.  This file reproduces libstdc++ 11 exactly
+// (bits/stl_algo.h __sort / __introsort_loop / __unguarded_partition_pivot /
+// __final_insertion_sort, bits/stl_heap.h for the depth-limit heapsort),
+// restated in oracle/rk_oracle.c and pinned against std::sort by
+// tests/test_oracle.py.
+//
+// Parallel form:
+//   * Hoare partition of [f,l) with pivot p at f: the left scan stops at
+//     "L-stoppers" (key >= p, positions > f), the right scan at "R-stoppers"
+//     (key <= p, the pivot itself included).  Because every swap only touches
+//     positions the scans have already passed, the k-th swap exchanges the
+//     k-th L-stopper (from the left) with the k-th R-stopper (from the right)
+//     of the ORIGINAL segment, for every k < K where K is the first k with
+//     Lpos[k] >= Rpos[k]; the returned cut is min(Lpos[K], Rpos[K-1]) (Lpos[0]
+//     when K == 0).  A wavefront computes both lists with ballots, finds K and
+//     does the K swaps in parallel.
+//   * After the loop every leaf segment (<= 16) is mutually ordered with its
+//     neighbours, so __final_insertion_sort == a stable sort inside each leaf:
+//     every element's final slot is its stable rank inside its leaf.
+//
+// Tiers (chosen per group by size): 1..16 members -> one thread per member
+// (insertion sort == stable rank); 17..512 and 513..2048 -> one wavefront per
+// group with the group staged in LDS (12 KB / 45 KB per wave); larger -> the
+// same wavefront code on global memory.
+// In every tier the result goes to `otag` (member order, group-major).
+#include "rk_internal.h"
+
+namespace rk {
+namespace {
+
+constexpr int THRESH = 16;  // libstdc++ _S_threshold
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// global-memory tier: stores by one lane must be visible to the other lanes
+__device__ __forceinline__ void wave_sync_global() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+template <bool GLOBAL>
+__device__ __forceinline__ void sync_mem() {
+  if (GLOBAL) wave_sync_global();
+  else wave_sync();
+}
+
+struct View {
+  uint64_t *K;
+  uint32_t *T;
+  uint32_t *PL, *PR;  // stopper position lists (capacity n)
+  uint8_t *B;         // 1 = leaf start, 2 = inside a heap-sorted segment
+};
+
+__device__ __forceinline__ void vswap(const View &v, uint32_t a, uint32_t b) {
+  const uint64_t k = v.K[a];
+  v.K[a] = v.K[b];
+  v.K[b] = k;
+  const uint32_t t = v.T[a];
+  v.T[a] = v.T[b];
+  v.T[b] = t;
+}
+
+// __move_median_to_first(result=f, a=f+1, b=mid, c=l-1)
+__device__ __forceinline__ void median_to_first(const View &v, uint32_t f, uint32_t l) {
+  const uint32_t a = f + 1, b = f + (l - f) / 2, c = l - 1;
+  const uint64_t ka = v.K[a], kb = v.K[b], kc = v.K[c];
+  uint32_t m;
+  if (ka < kb) m = kb < kc ? b : (ka < kc ? c : a);
+  else m = ka < kc ? a : (kb < kc ? c : b);
+  vswap(v, f, m);
+}
+
+// __adjust_heap + __push_heap on v.K/T[base ..)
+__device__ void adjust_heap(const View &v, uint32_t base, long hole, long len, uint64_t vk,
+                            uint32_t vt) {
+  const long top = hole;
+  long child = hole;
+  uint64_t *K = v.K + base;
+  uint32_t *T = v.T + base;
+  while (child < (len - 1) / 2) {
+    child = 2 * (child + 1);
+    if (K[child] < K[child - 1]) child--;
+    K[hole] = K[child];
+    T[hole] = T[child];
+    hole = child;
+  }
+  if ((len & 1) == 0 && child == (len - 2) / 2) {
+    child = 2 * (child + 1);
+    K[hole] = K[child - 1];
+    T[hole] = T[child - 1];
+    hole = child - 1;
+  }
+  long parent = (hole - 1) / 2;
+  while (hole > top && K[parent] < vk) {
+    K[hole] = K[parent];
+    T[hole] = T[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  K[hole] = vk;
+  T[hole] = vt;
+}
+
+// __partial_sort(first, last, last): __make_heap + __sort_heap; marks B = 2
+__device__ void heap_sort_segment(const View &v, uint32_t f, uint32_t l) {
+  const long len = (long)(l - f);
+  if (len >= 2) {
+    for (long parent = (len - 2) / 2;; --parent) {
+      adjust_heap(v, f, parent, len, v.K[f + parent], v.T[f + parent]);
+      if (parent == 0) break;
+    }
+  }
+  for (long last = len; last > 1;) {
+    --last;
+    const uint64_t vk = v.K[f + last];
+    const uint32_t vt = v.T[f + last];
+    v.K[f + last] = v.K[f];
+    v.T[f + last] = v.T[f];
+    adjust_heap(v, f, 0, last, vk, vt);
+  }
+  for (uint32_t x = f; x < l; ++x) v.B[x] = 2;
+}
+
+// Sequential __introsort_loop on a small segment (one lane).  Frames pushed
+// are > 16 and disjoint, so a segment of <= 64 never holds more than 3.
+__device__ void seq_introsort(const View &v, uint32_t f0, uint32_t l0, int d0) {
+  uint32_t sf[8], sl[8];
+  int sd[8];
+  int sp = 0;
+  sf[0] = f0, sl[0] = l0, sd[0] = d0, sp = 1;
+  while (sp) {
+    --sp;
+    uint32_t f = sf[sp], l = sl[sp];
+    int d = sd[sp];
+    bool heap = false;
+    while (l - f > THRESH) {
+      if (d == 0) {
+        heap_sort_segment(v, f, l);
+        heap = true;
+        break;
+      }
+      --d;
+      median_to_first(v, f, l);
+      const uint64_t p = v.K[f];
+      uint32_t i = f + 1, j = l;
+      for (;;) {  // __unguarded_partition
+        while (v.K[i] < p) ++i;
+        --j;
+        while (p < v.K[j]) --j;
+        if (!(i < j)) break;
+        vswap(v, i, j);
+        ++i;
+      }
+      if (l - i > THRESH) {
+        sf[sp] = i, sl[sp] = l, sd[sp] = d, ++sp;
+      } else {
+        v.B[i] = 1;  // right part is a leaf
+      }
+      l = i;
+    }
+    if (!heap) v.B[f] = 1;
+  }
+}
+
+// wavefront-parallel __unguarded_partition_pivot on [f, l); returns the cut
+template <bool GLOBAL>
+__device__ uint32_t wave_partition(const View &v, uint32_t f, uint32_t l, uint32_t lane) {
+  if (lane == 0) median_to_first(v, f, l);
+  sync_mem<GLOBAL>();
+  const uint64_t p = v.K[f];
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t nL = 0, nR = 0;
+  for (uint32_t c = f; c < l; c += 64) {
+    const uint32_t x = c + lane;
+    const bool in = x < l;
+    const uint64_t k = in ? v.K[x] : 0;
+    const bool lf = in && x > f && !(k < p);
+    const bool rf = in && !(p < k);
+    const uint64_t bl = __ballot(lf), br = __ballot(rf);
+    if (lf) v.PL[nL + __popcll(bl & lt)] = x;
+    if (rf) v.PR[nR + __popcll(br & lt)] = x;
+    nL += __popcll(bl);
+    nR += __popcll(br);
+  }
+  sync_mem<GLOBAL>();
+  // K = first k with Lpos[k] >= Rpos[k]; Rpos[k] = PR[nR-1-k] (k-th from the right)
+  const uint32_t lim = nL < nR ? nL : nR;
+  uint32_t K = lim;
+  for (uint32_t c = 0; c < lim; c += 64) {
+    const uint32_t k = c + lane;
+    const bool stop = k < lim && v.PL[k] >= v.PR[nR - 1 - k];
+    const uint64_t b = __ballot(stop);
+    if (b) {
+      K = c + (uint32_t)__ffsll((unsigned long long)b) - 1;
+      break;
+    }
+  }
+  for (uint32_t c = 0; c < K; c += 64) {
+    const uint32_t k = c + lane;
+    if (k < K) vswap(v, v.PL[k], v.PR[nR - 1 - k]);
+  }
+  uint32_t cut;
+  if (K == 0) {
+    cut = v.PL[0];
+  } else {
+    cut = v.PR[nR - K];
+    if (K < nL && v.PL[K] < cut) cut = v.PL[K];
+  }
+  sync_mem<GLOBAL>();
+  return cut;
+}
+
+struct Frame {
+  uint32_t f, l;
+  int d;
+};
+
+// the whole libstdc++ std::sort of one group [0, n) of view v, then stable
+// leaf ranks written to out[0..n) (tags only)
+template <bool GLOBAL>
+__device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *stack,
+                              Frame *smallq, Frame *heapq, uint32_t lane) {
+  for (uint32_t x = lane; x < n; x += 64) v.B[x] = 0;
+  int sp = 0, nsmall = 0, nheap = 0;
+  if (lane == 0) stack[0] = {0u, n, 2 * (31 - __clz((int)n))};
+  sp = 1;
+  sync_mem<GLOBAL>();
+  while (sp) {
+    Frame fr = stack[--sp];
+    uint32_t f = fr.f, l = fr.l;
+    int d = fr.d;
+    bool final_leaf = true;
+    while (l - f > THRESH) {
+      if (d == 0) {  // heapsort fallback, done lane-parallel below
+        if (lane == 0) heapq[nheap] = {f, l, 0};
+        ++nheap;
+        final_leaf = false;
+        break;
+      }
+      if (l - f <= 64) {  // small: a single lane finishes this subtree
+        if (lane == 0) smallq[nsmall] = {f, l, d};
+        ++nsmall;
+        final_leaf = false;
+        break;
+      }
+      --d;
+      const uint32_t cut = wave_partition<GLOBAL>(v, f, l, lane);
+      if (lane == 0) stack[sp] = {cut, l, d};
+      ++sp;
+      l = cut;
+    }
+    if (final_leaf && lane == 0) v.B[f] = 1;
+    sync_mem<GLOBAL>();
+  }
+  for (int q = (int)lane; q < nsmall; q += 64) seq_introsort(v, smallq[q].f, smallq[q].l, smallq[q].d);
+  for (int q = (int)lane; q < nheap; q += 64) heap_sort_segment(v, heapq[q].f, heapq[q].l);
+  sync_mem<GLOBAL>();
+  // __final_insertion_sort == stable sort inside every leaf
+  for (uint32_t x = lane; x < n; x += 64) {
+    if (v.B[x] == 2) {
+      out[x] = v.T[x];
+      continue;
+    }
+    uint32_t s = x;
+    while (v.B[s] == 0) --s;
+    uint32_t e = x + 1;
+    while (e < n && v.B[e] == 0) ++e;
+    const uint64_t kx = v.K[x];
+    uint32_t r = 0;
+    for (uint32_t y = s; y < e; ++y) {
+      const uint64_t ky = v.K[y];
+      r += (ky < kx) || (ky == kx && y < x);
+    }
+    out[s + r] = v.T[x];
+  }
+}
+
+// LDS tier: one wavefront (block of 64) per group of 17..cap members
+__global__ void __launch_bounds__(64) k_sort_groups_lds(const uint32_t *list, uint32_t nlist,
+                                                        const uint32_t *goff, const uint64_t *key,
+                                                        const uint32_t *tag, uint32_t *otag,
+                                                        uint32_t cap) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nfr = cap / (THRESH + 1) + 2;
+  uint64_t *K = reinterpret_cast<uint64_t *>(smem);
+  uint32_t *T = reinterpret_cast<uint32_t *>(K + cap);
+  uint32_t *PL = T + cap;
+  uint32_t *PR = PL + cap;
+  Frame *stack = reinterpret_cast<Frame *>(PR + cap);
+  Frame *smallq = stack + 72;
+  Frame *heapq = smallq + nfr;
+  uint8_t *B = reinterpret_cast<uint8_t *>(heapq + nfr);
+  const View v{K, T, PL, PR, B};
+  for (uint32_t w = blockIdx.x; w < nlist; w += gridDim.x) {
+    const uint32_t g = list[w];
+    const uint32_t b = goff[g], n = goff[g + 1] - b;
+    for (uint32_t x = lane; x < n; x += 64) {
+      K[x] = key[b + x];
+      T[x] = tag[b + x];
+    }
+    wave_sync();
+    wave_std_sort<false>(v, n, otag + b, stack, smallq, heapq, lane);
+    wave_sync();
+  }
+}
+
+// global tier: same code on the group's own slices of global scratch.  Frame
+// storage of the w-th listed group starts at (b >> 3) + 80 * w: regions of
+// consecutive listed groups never overlap (a group of n members needs at most
+// 72 + 2 * (n / 17 + 2) frames).
+__global__ void __launch_bounds__(64) k_sort_groups_global(const uint32_t *list, uint32_t nlist,
+                                                           const uint32_t *goff, uint64_t *key,
+                                                           uint32_t *tag, uint32_t *otag,
+                                                           uint32_t *pl, uint32_t *pr,
+                                                           uint8_t *bnd, Frame *frames) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t w = blockIdx.x; w < nlist; w += gridDim.x) {
+    const uint32_t g = list[w];
+    const uint32_t b = goff[g], n = goff[g + 1] - b;
+    Frame *fr = frames + (b >> 3) + (size_t)80 * w;
+    const uint32_t nfr = n / (THRESH + 1) + 2;
+    const View v{key + b, tag + b, pl + b, pr + b, bnd + b};
+    wave_std_sort<true>(v, n, otag + b, fr, fr + 72, fr + 72 + nfr, lane);
+    wave_sync_global();
+  }
+}
+
+// groups of 1..16 members: insertion sort == stable rank; one thread per member
+__global__ void k_sort_small(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t m,
+                             const uint64_t *key, const uint32_t *tag, uint32_t *otag) {
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
+    const uint32_t g = gid_sorted[x];
+    const uint32_t b = goff[g], e = goff[g + 1];
+    if (e - b > (uint32_t)THRESH) continue;
+    const uint64_t kx = key[x];
+    uint32_t r = 0;
+    for (uint32_t y = b; y < e; ++y) {
+      const uint64_t ky = key[y];
+      r += (ky < kx) || (ky == kx && y < x);
+    }
+    otag[b + r] = tag[x];
+  }
+}
+
+// flags for the tier lists: 1 = LDS tier, 2 = global tier
+__global__ void k_tier_flags(const uint32_t *goff, uint32_t ngroups, uint32_t cap, uint32_t cap2,
+                             uint32_t *f1, uint32_t *f2, uint32_t *f3) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
+       g += gridDim.x * blockDim.x) {
+    const uint32_t n = goff[g + 1] - goff[g];
+    f1[g] = n > (uint32_t)THRESH && n <= cap;
+    f2[g] = n > cap && n <= cap2;
+    f3[g] = n > cap2;
+  }
+}
+
+__global__ void k_compact(const uint32_t *flag, const uint32_t *pos, uint32_t n, uint32_t *list) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < n; g += gridDim.x * blockDim.x)
+    if (flag[g]) list[pos[g]] = g;
+}
+
+size_t lds_bytes(uint32_t cap) {
+  const uint32_t nfr = cap / (THRESH + 1) + 2;
+  return (size_t)cap * (8 + 4 + 4 + 4) + (72 + 2 * nfr) * sizeof(Frame) + cap + 16;
+}
+
+}  // namespace
+
+constexpr uint32_t LDS_CAP = 512;    // groups up to this size: small LDS tier
+constexpr uint32_t LDS_CAP2 = 2048;  // up to this size: large LDS tier (3 waves / CU)
+
+size_t groupsort_scratch_bytes(uint32_t n) {
+  const size_t g1 = (size_t)n + 1;
+  const size_t frames = (size_t)n / 8 + 80 * ((size_t)n / (LDS_CAP2 + 1) + 1) + 80;
+  return (size_t)n * 4 * 2 + g1 * 4 * 9 + (size_t)n + 64 + frames * sizeof(Frame) + 256;
+}
+
+void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
+                       uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
+                       ScanScratch ss, uint32_t *host_words, hipStream_t st) {
+  if (!m) return;
+  const size_t g1 = (size_t)ngroups + 1;
+  uint32_t *pl = reinterpret_cast<uint32_t *>(scratch);
+  uint32_t *pr = pl + m;
+  uint32_t *f1 = pr + m, *f2 = f1 + g1, *f3 = f2 + g1, *p1 = f3 + g1, *p2 = p1 + g1,
+           *p3 = p2 + g1, *l1 = p3 + g1, *l2 = l1 + g1, *l3 = l2 + g1;
+  uint8_t *bnd = reinterpret_cast<uint8_t *>(l3 + g1);
+  Frame *frames = reinterpret_cast<Frame *>(
+      (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
+  k_sort_small<<<grid_for(m, 256), 256, 0, st>>>(gid_sorted, goff, m, key, tag, otag);
+  k_tier_flags<<<grid_for(ngroups, 256), 256, 0, st>>>(goff, ngroups, LDS_CAP, LDS_CAP2, f1, f2,
+                                                       f3);
+  uint32_t *fl[3] = {f1, f2, f3}, *ps[3] = {p1, p2, p3}, *ls[3] = {l1, l2, l3};
+  for (int t = 0; t < 3; ++t) {
+    (void)hipMemsetAsync(fl[t] + ngroups, 0, 4, st);
+    exclusive_scan_u32(fl[t], ps[t], g1, ss, st);
+    k_compact<<<grid_for(ngroups, 256), 256, 0, st>>>(fl[t], ps[t], ngroups, ls[t]);
+    (void)hipMemcpyAsync(host_words + t, ps[t] + ngroups, 4, hipMemcpyDeviceToHost, st);
+  }
+  (void)hipStreamSynchronize(st);
+  const uint32_t n1 = host_words[0], n2 = host_words[1], n3 = host_words[2];
+  if (n1)
+    k_sort_groups_lds<<<n1 < 16384 ? n1 : 16384, 64, lds_bytes(LDS_CAP), st>>>(
+        l1, n1, goff, key, tag, otag, LDS_CAP);
+  if (n2)
+    k_sort_groups_lds<<<n2 < 2048 ? n2 : 2048, 64, lds_bytes(LDS_CAP2), st>>>(
+        l2, n2, goff, key, tag, otag, LDS_CAP2);
+  if (n3)
+    k_sort_groups_global<<<n3 < 1024 ? n3 : 1024, 64, 0, st>>>(l3, n3, goff, key, tag, otag, pl,
+                                                               pr, bnd, frames);
+}
+
+}  // namespace rk

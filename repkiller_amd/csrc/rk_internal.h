@@ -60,18 +60,28 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   const uint64_t *len; // length
   uint8_t *state;      // ST_*
   uint32_t *win;       // winner's processing index (valid when ST_HIT)
+  uint32_t *rlen_at;   // run length, stored at each run's first position
+  uint32_t *rbeg_at;   // run start, stored at each run's last position
   uint32_t m;          // entries
   uint64_t max_index;  // seq_size / 100 (SequenceOcupationList.cpp:4)
   double len_ratio, pos_ratio;
 };
-// list the run starts of a sorted key array (work items for the first sweep)
-void run_starts(const uint32_t *key, uint32_t m, uint32_t *list, uint32_t *count,
-                hipStream_t st);
-// one sweep over the runs in `work`; runs that keep undecided entries are
-// appended to next_work (*next_count zeroed by the caller).  big_work /
-// big_count: scratch for the wavefront-per-run path.
-void occupancy_sweep(const Axis &ax, const uint32_t *work, uint32_t nwork, uint32_t *next_work,
-                     uint32_t *next_count, uint32_t *big_work, uint32_t *big_count,
+// The axis' bucket runs as a dense list sorted by length (short runs first):
+// beg/len (len exact below 255, clamped above), nshort = runs < WAVE_MIN (one
+// lane each), the rest one wavefront each.
+struct RunList {
+  uint32_t *beg, *len;
+  uint32_t nruns, nshort;
+};
+size_t runs_scratch_words(uint32_t m);
+void build_runs(const Axis &ax, RunList &rl, uint32_t *scratch, uint32_t *radix_k_tmp,
+                uint32_t *radix_v_tmp, uint32_t *radix_scratch, size_t radix_words,
+                ScanScratch ss, uint32_t *dev_words, uint32_t *host_words, hipStream_t st);
+// One sweep.  rpend[p] (run start p) = run still has undecided entries; set
+// to 1 everywhere before the first sweep.  counters: PEND_WORDS words, their
+// sum is the number of runs still pending after the sweep.
+constexpr uint32_t PEND_WORDS = 64;
+void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
                      hipStream_t st);
 
 // ---------------------------------------------------------- rk_groups.hip --
@@ -83,7 +93,8 @@ struct Frags {  // file-order inputs
 struct Proc {  // processing-order working set
   uint32_t *pkey;  // sorted xStart/10 key
   uint32_t *row;   // proc -> file row
-  uint64_t *xc, *yc, *len, *ha;
+  ulonglong2 *xrec, *yrec;  // {centre, length} on each axis (one 16-B gather each)
+  uint64_t *ha;
   uint32_t *keyx, *keyy;
   uint8_t *xstate, *ystate;
   uint32_t *xwin, *ywin;
@@ -101,8 +112,8 @@ void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, u
                uint32_t *kept, uint32_t *err, hipStream_t st);
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
 // centre/length/state in CSR order; for_y: state from the X result
-void csr_fill(Csr c, const uint64_t *cen, const uint64_t *len, const uint8_t *xstate, bool for_y,
-              uint32_t m, hipStream_t st);
+void csr_fill(Csr c, const ulonglong2 *rec, const uint8_t *xstate, bool for_y, uint32_t m,
+              hipStream_t st);
 void csr_scatter_back(Csr c, uint8_t *state, uint32_t *win, uint32_t m, hipStream_t st);
 void make_parents(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, hipStream_t st);
 void jump_round(Proc p, uint32_t m, uint32_t *changed, hipStream_t st);
@@ -111,8 +122,13 @@ void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t 
                    hipStream_t st);
 void build_records(const uint32_t *gmem, const uint64_t *ha, uint32_t m, uint64_t *key,
                    uint32_t *tag, hipStream_t st);
-void sort_groups(const uint32_t *goff, uint32_t ngroups, uint64_t *key, uint32_t *tag,
-                 hipStream_t st);
+// ------------------------------------------------------- rk_groupsort.hip --
+size_t groupsort_scratch_bytes(uint32_t n);
+// libstdc++ std::sort of every group's (key, tag) records; sorted tags -> otag.
+// gid_sorted: group id of every record; host_words: >= 2 pinned words.
+void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
+                       uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
+                       ScanScratch ss, uint32_t *host_words, hipStream_t st);
 void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
                  const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st);

@@ -45,7 +45,7 @@
 namespace rk {
 namespace {
 
-constexpr uint32_t WAVE_MIN = 48;  // runs at least this long get a whole wavefront
+constexpr uint32_t WAVE_MIN = 48;  // runs at least this long get a whole wavefront (<= 64)
 
 __device__ __forceinline__ double deviation(uint64_t c, uint64_t L, uint64_t oc, uint64_t oL,
                                             double lr, double pr) {
@@ -66,12 +66,13 @@ __device__ __forceinline__ int neighbour_dir(uint64_t c, uint64_t max_index) {
   return 0;
 }
 
-__device__ __forceinline__ uint8_t load_state(const uint8_t *s) {
-  return __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_state(uint8_t *s, uint8_t v) {
-  __hip_atomic_store(s, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// States only move UNKNOWN -> decided (and HIT_PENDING -> HIT), so a stale
+// read of another run's state is always conservative: it can only postpone a
+// decision to the next sweep, never change one.  Plain loads and stores are
+// therefore enough (agent-scope sc1 byte stores are one fabric write each);
+// every sweep is its own launch, which makes all states coherent between sweeps.
+__device__ __forceinline__ uint8_t load_state(const uint8_t *s) { return *(const volatile uint8_t *)s; }
+__device__ __forceinline__ void store_state(uint8_t *s, uint8_t v) { *s = v; }
 
 struct Scan {
   double best;
@@ -102,95 +103,115 @@ __device__ __forceinline__ uint8_t decide(const Scan &s) {
   return s.any_active ? ST_HIT : ST_ACTIVE;
 }
 
-// Append `item` to list when pred; called by EVERY thread of the block (uniform
-// control flow).  One global atomic per block instead of one per item: a single
-// hot counter serialises at ~88 increments/us (MI355X_MICROARCH.md "dequeue").
-__device__ __forceinline__ void block_append(uint32_t *list, uint32_t *count, uint32_t item,
-                                             bool pred) {
-  __shared__ uint32_t wtot[16];
-  __shared__ uint32_t gbase;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  const uint64_t b = __ballot(pred);
-  if (lane == 0) wtot[w] = __popcll(b);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int k = 0; k < nw; ++k) {
-      const uint32_t c = wtot[k];
-      wtot[k] = t;
-      t += c;
-    }
-    gbase = t ? atomicAdd(count, t) : 0u;
-  }
-  __syncthreads();
-  if (pred) list[gbase + wtot[w] + __popcll(b & ((1ull << lane) - 1ull))] = item;
-  __syncthreads();
-}
-
-// bounds of the run holding key +-1 adjacent to [beg, end) on side `dir`
+// bounds of the run holding key +-1 adjacent to [beg, end) on side `dir`:
+// one lookup each in the per-position run tables (rlen_at at run starts,
+// rbeg_at at run ends) instead of a walk over the neighbour's keys
 __device__ __forceinline__ bool neighbour_run(const Axis &ax, uint32_t beg, uint32_t end,
                                               uint32_t key, int dir, uint32_t &nb,
                                               uint32_t &ne) {
   if (dir < 0) {
     if (beg == 0 || ax.key[beg - 1] != key - 1) return false;
     ne = beg;
-    nb = beg - 1;
-    while (nb > 0 && ax.key[nb - 1] == key - 1) --nb;
+    nb = ax.rbeg_at[beg - 1];
     return true;
   }
   if (end >= ax.m || ax.key[end] != key + 1) return false;
   nb = end;
-  ne = end + 1;
-  while (ne < ax.m && ax.key[ne] == key + 1) ++ne;
+  ne = end + ax.rlen_at[end];
   return true;
 }
 
+__device__ __forceinline__ bool run_start(const Axis &ax, uint32_t p) {
+  return p == 0 || ax.key[p] != ax.key[p - 1];
+}
+
+// pending-run counters are spread over PEND_WORDS words (one hot word
+// serialises at ~88 atomics/us); the host sums them
+constexpr uint32_t PEND_SLOTS = PEND_WORDS;
+
+__device__ __forceinline__ void count_pending(uint32_t *counters, bool pending) {
+  const uint64_t b = __ballot(pending);
+  if ((threadIdx.x & 63) == 0 && b)
+    atomicAdd(&counters[(blockIdx.x * 4 + (threadIdx.x >> 6)) % PEND_SLOTS], (uint32_t)__popcll(b));
+}
+
 // ---- one lane walks one run ----------------------------------------------
-__global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *work, uint32_t nwork,
-                                                    uint32_t *next_work, uint32_t *next_count,
-                                                    uint32_t *big_work, uint32_t *big_count) {
+// Work items: the short runs (< WAVE_MIN <= 64 entries), sorted by length so
+// the 64 lanes of a wave walk runs of (nearly) equal length.  The run's own
+// states live in two 64-bit masks (bit t = entry beg+t): `act` = in the list,
+// `unk` = undecided.  A candidate scan then visits only set bits -- entries
+// that already hit cost nothing -- so the walk is O(len * active) instead of
+// O(len^2) memory reads.
+__global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *run_beg,
+                                                    const uint32_t *run_len, uint32_t nruns,
+                                                    uint8_t *rpend, uint32_t *counters) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  bool pending = false, big = false;
-  uint32_t beg = 0;
-  if (w < nwork) {
-    beg = work[w];
-    const uint32_t key = ax.key[beg];
-    uint32_t end = beg + 1;
-    while (end < ax.m && ax.key[end] == key) ++end;
-    if (end - beg >= WAVE_MIN) {
-      big = true;
-    } else {
+  bool pending = false;
+  if (w < nruns) {
+    const uint32_t beg = run_beg[w];
+    if (rpend[beg]) {
+      const uint32_t len = run_len[w];
+      const uint32_t key = ax.key[beg];
+      uint64_t act = 0, unk = 0, todo = 0;
+      for (uint32_t t = 0; t < len; ++t) {
+        const uint8_t st = ax.state[beg + t];
+        const uint64_t bit = 1ull << t;
+        if (st == ST_ACTIVE) act |= bit;
+        else if (st == ST_UNKNOWN) unk |= bit, todo |= bit;
+        else if (st == ST_HIT_PENDING) todo |= bit;
+      }
       // neighbour runs, found lazily: 0 = not looked up, 1 = absent, 2 = present
       int lo_st = 0, hi_st = 0;
       uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
-      for (uint32_t t = beg; t < end; ++t) {
-        const uint8_t st = ax.state[t];
-        if (st == ST_ACTIVE || st == ST_HIT) continue;
-        const uint64_t c = ax.cen[t], L = ax.len[t];
+      while (todo) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(todo);
+        const uint64_t bit = 1ull << t;
+        todo &= todo - 1;
+        const uint32_t q0 = beg + t;
+        const uint64_t c = ax.cen[q0], L = ax.len[q0];
         Scan s{0.0, NONE, 0, false, false};
-        for (uint32_t q = t; q-- > beg;) consider(ax, s, q, c, L);
+        uint64_t cand = (act | unk) & (bit - 1);
+        while (cand) {  // newest first
+          const uint32_t u = 63 - (uint32_t)__builtin_clzll(cand);
+          cand &= ~(1ull << u);
+          const uint32_t q = beg + u;
+          const double d = deviation(c, L, ax.cen[q], ax.len[q], ax.len_ratio, ax.pos_ratio);
+          if (!(d > 0)) continue;
+          if ((act >> u) & 1ull) {
+            s.any_active = true;
+            if (d > s.best) {
+              s.best = d;
+              s.win = q;
+            }
+          } else {
+            s.any_unknown = true;
+          }
+        }
         const int dir = neighbour_dir(c, ax.max_index);
         if (dir) {
           int &nst = dir < 0 ? lo_st : hi_st;
           uint32_t &nb = dir < 0 ? lo_b : hi_b;
           uint32_t &ne = dir < 0 ? lo_e : hi_e;
-          if (nst == 0) nst = neighbour_run(ax, beg, end, key, dir, nb, ne) ? 2 : 1;
+          if (nst == 0) nst = neighbour_run(ax, beg, beg + len, key, dir, nb, ne) ? 2 : 1;
           if (nst == 2) {
-            const uint32_t i = ax.ent[t];
-            uint32_t q = ne;
-            while (q > nb && ax.ent[q - 1] > i) --q;  // only entries inserted before i
-            while (q-- > nb) consider(ax, s, q, c, L);
+            const uint32_t i = ax.ent[q0];
+            for (uint32_t q = ne; q-- > nb;)  // newest first, only entries inserted before i
+              if (ax.ent[q] < i) consider(ax, s, q, c, L);
           }
         }
         const uint8_t ns = decide(s);
-        if (ns == ST_HIT) ax.win[t] = ax.ent[s.win];
-        if (ns != st) store_state(&ax.state[t], ns);
+        if (ns == ST_HIT) ax.win[q0] = ax.ent[s.win];
+        if (ns != ST_UNKNOWN) {
+          unk &= ~bit;
+          if (ns == ST_ACTIVE) act |= bit;
+          store_state(&ax.state[q0], ns);
+        }
         pending |= ns == ST_UNKNOWN || ns == ST_HIT_PENDING;
       }
+      rpend[beg] = pending;
     }
   }
-  block_append(big_work, big_count, beg, big);
-  block_append(next_work, next_count, beg, pending);
+  count_pending(counters, pending);
 }
 
 // ---- one wavefront walks one long run --------------------------------------
@@ -232,17 +253,16 @@ __device__ __forceinline__ void wave_combine(Scan &s) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *work,
-                                                    const uint32_t *nwork_ptr, uint32_t *next_work,
-                                                    uint32_t *next_count) {
-  const uint32_t nwork = *nwork_ptr;
+__global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big, uint32_t nbig,
+                                                    uint8_t *rpend, uint32_t *counters) {
+  // big = starts of the runs of >= WAVE_MIN entries
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nwork;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nbig;
        w += (gridDim.x * blockDim.x) >> 6) {
-    const uint32_t beg = work[w];
+    const uint32_t beg = big[w];
+    if (!rpend[beg]) continue;
     const uint32_t key = ax.key[beg];
-    uint32_t end = beg + 1;
-    while (end < ax.m && ax.key[end] == key) ++end;
+    const uint32_t end = beg + ax.rlen_at[beg];
     uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
     const bool has_lo = neighbour_run(ax, beg, end, key, -1, lo_b, lo_e);
     const bool has_hi = neighbour_run(ax, beg, end, key, 1, hi_b, hi_e);
@@ -274,41 +294,93 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *wor
       }
       pending |= ns == ST_UNKNOWN || ns == ST_HIT_PENDING;
     }
-    if (pending && lane == 0) next_work[atomicAdd(next_count, 1u)] = beg;
+    if (lane == 0) {
+      rpend[beg] = pending;
+      if (pending) atomicAdd(&counters[w % PEND_SLOTS], 1u);
+    }
   }
 }
 
-// run starts of a sorted key array: p == 0 || key[p] != key[p-1]
-__global__ void __launch_bounds__(256) k_run_starts(const uint32_t *key, uint32_t m,
-                                                    uint32_t *list, uint32_t *count) {
-  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < m; b0 += gridDim.x * blockDim.x) {
-    const uint32_t p = b0 + threadIdx.x;
-    const bool start = p < m && (p == 0 || key[p] != key[p - 1]);
-    block_append(list, count, p, start);
+__global__ void k_run_flags(Axis ax, uint32_t *flag) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < ax.m; p += gridDim.x * blockDim.x)
+    flag[p] = run_start(ax, p);
+}
+
+// run r starts at p (rank from the scan); its length key is filled next
+__global__ void k_run_emit(Axis ax, const uint32_t *flag, const uint32_t *rank, uint32_t *beg) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < ax.m; p += gridDim.x * blockDim.x)
+    if (flag[p]) beg[rank[p]] = p;
+}
+
+// length key (exact below 256, clamped above); counts runs shorter than
+// WAVE_MIN (one atomic per block)
+__global__ void __launch_bounds__(256) k_run_len(const uint32_t *beg, uint32_t nruns, uint32_t m,
+                                                 uint32_t *lenkey, uint32_t *nshort) {
+  uint32_t mine = 0;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nruns;
+       r += gridDim.x * blockDim.x) {
+    const uint32_t len = (r + 1 < nruns ? beg[r + 1] : m) - beg[r];
+    lenkey[r] = len < 255 ? len : 255;
+    mine += len < WAVE_MIN;
+  }
+  __shared__ uint32_t part[4];
+  for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0 && part[0] + part[1] + part[2] + part[3])
+    atomicAdd(nshort, part[0] + part[1] + part[2] + part[3]);
+}
+
+// per-position run tables: length at each run start, start at each run end
+__global__ void k_run_tables(Axis ax, const uint32_t *beg, uint32_t nruns, uint32_t *rlen_at,
+                             uint32_t *rbeg_at) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nruns;
+       r += gridDim.x * blockDim.x) {
+    const uint32_t b = beg[r], e = r + 1 < nruns ? beg[r + 1] : ax.m;
+    rlen_at[b] = e - b;
+    rbeg_at[e - 1] = b;
   }
 }
 
 }  // namespace
 
-void run_starts(const uint32_t *key, uint32_t m, uint32_t *list, uint32_t *count,
-                hipStream_t st) {
-  (void)hipMemsetAsync(count, 0, sizeof(uint32_t), st);
-  if (!m) return;
-  uint32_t g = (m + 255) / 256;
-  if (g > 8192) g = 8192;
-  k_run_starts<<<g, 256, 0, st>>>(key, m, list, count);
+size_t runs_scratch_words(uint32_t m) { return 4 * ((size_t)m + 1) + 64; }
+
+void build_runs(const Axis &ax, RunList &rl, uint32_t *scratch, uint32_t *radix_k_tmp,
+                uint32_t *radix_v_tmp, uint32_t *radix_scratch, size_t radix_words,
+                ScanScratch ss, uint32_t *dev_words, uint32_t *host_words, hipStream_t st) {
+  rl.nruns = rl.nshort = 0;
+  if (!ax.m) return;
+  const size_t m1 = (size_t)ax.m + 1;
+  uint32_t *flag = scratch, *rank = scratch + m1, *beg = rank + m1, *lenkey = beg + m1;
+  k_run_flags<<<grid_for(ax.m, 256), 256, 0, st>>>(ax, flag);
+  (void)hipMemsetAsync(flag + ax.m, 0, 4, st);
+  exclusive_scan_u32(flag, rank, m1, ss, st);
+  k_run_emit<<<grid_for(ax.m, 256), 256, 0, st>>>(ax, flag, rank, beg);
+  (void)hipMemcpyAsync(host_words, rank + ax.m, 4, hipMemcpyDeviceToHost, st);
+  (void)hipStreamSynchronize(st);
+  rl.nruns = host_words[0];
+  (void)hipMemsetAsync(dev_words, 0, 4, st);
+  k_run_len<<<grid_for(rl.nruns, 256, 2048), 256, 0, st>>>(beg, rl.nruns, ax.m, lenkey, dev_words);
+  k_run_tables<<<grid_for(rl.nruns, 256), 256, 0, st>>>(ax, beg, rl.nruns, ax.rlen_at, ax.rbeg_at);
+  // ascending length: short runs first, grouped by length; long runs last
+  radix_sort_pairs(lenkey, beg, rl.len, rl.beg, radix_k_tmp, radix_v_tmp, rl.nruns, 8,
+                   radix_scratch, radix_words, st);
+  (void)hipMemcpyAsync(host_words, dev_words, 4, hipMemcpyDeviceToHost, st);
+  (void)hipStreamSynchronize(st);
+  rl.nshort = host_words[0];
 }
 
-void occupancy_sweep(const Axis &ax, const uint32_t *work, uint32_t nwork, uint32_t *next_work,
-                     uint32_t *next_count, uint32_t *big_work, uint32_t *big_count,
+void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
                      hipStream_t st) {
-  if (!nwork) return;
-  (void)hipMemsetAsync(big_count, 0, sizeof(uint32_t), st);
-  k_sweep_lane<<<(nwork + 255) / 256, 256, 0, st>>>(ax, work, nwork, next_work, next_count,
-                                                     big_work, big_count);
-  unsigned blocks = (nwork + 3) / 4;  // one wave per long run (upper bound), grid-strided
-  if (blocks > 2048) blocks = 2048;
-  k_sweep_wave<<<blocks, 256, 0, st>>>(ax, big_work, big_count, next_work, next_count);
+  (void)hipMemsetAsync(counters, 0, PEND_SLOTS * sizeof(uint32_t), st);
+  if (rl.nshort)
+    k_sweep_lane<<<(rl.nshort + 255) / 256, 256, 0, st>>>(ax, rl.beg, rl.len, rl.nshort, rpend,
+                                                          counters);
+  const uint32_t nbig = rl.nruns - rl.nshort;
+  if (nbig)
+    k_sweep_wave<<<grid_for(nbig, 4, 2048), 256, 0, st>>>(ax, rl.beg + rl.nshort, nbig, rpend,
+                                                          counters);
 }
 
 }  // namespace rk

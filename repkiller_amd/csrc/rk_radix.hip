@@ -13,7 +13,9 @@
 //   exclusive scan over counts (rk_sort.hip, DPP wave scan)
 //   k_digit_scatter  re-reads the tile in index order, ranks every key among
 //                  equal digits (8 wave ballots -> peer mask -> popcount; wave
-//                  totals through LDS in wave order), scatters key and value.
+//                  totals through LDS in wave order), places it at its tile-local
+//                  sorted slot in LDS, then writes the tile out slot by slot
+//                  (coalesced per digit segment).
 // Tiles: 256 threads x 16 keys; key i of the tile is read as round i/256,
 // thread i%256 -- coalesced, and rank order == index order (stability).
 #include "rk_internal.h"
@@ -42,30 +44,63 @@ __global__ void __launch_bounds__(RT) k_digit_hist(const uint32_t *__restrict__ 
   counts[threadIdx.x * tiles + blockIdx.x] = hist[threadIdx.x];
 }
 
+// Stable scatter of one tile through LDS: ranks are computed in index order
+// (round r = keys r*256 .. r*256+255 of the tile, wave-major), each key is
+// first placed at its tile-local sorted slot lbase[d] + rank, then the tile is
+// written out slot by slot, so consecutive lanes write consecutive addresses
+// of the same digit segment (coalesced instead of 256 scattered streams).
 __global__ void __launch_bounds__(RT) k_digit_scatter(const uint32_t *__restrict__ key_in,
                                                       const uint32_t *__restrict__ val_in,
                                                       uint32_t n, int shift, uint32_t tiles,
                                                       const uint32_t *__restrict__ offs,
                                                       uint32_t *__restrict__ key_out,
                                                       uint32_t *__restrict__ val_out) {
-  __shared__ uint32_t base[RADIX];
+  __shared__ uint32_t sk[RTILE];
+  __shared__ uint32_t sv[RTILE];
+  __shared__ uint32_t lbase[RADIX];  // tile-local start of digit d
+  __shared__ uint32_t run[RADIX];    // keys of digit d placed so far
   __shared__ uint32_t wcount[RT / 64][RADIX];
+  __shared__ uint32_t wsum[RT / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  base[threadIdx.x] = offs[threadIdx.x * tiles + blockIdx.x];
   const uint64_t lt = (1ull << lane) - 1ull;
   const uint32_t tile0 = blockIdx.x * (uint32_t)RTILE;
+  const uint32_t cnt = n - tile0 < (uint32_t)RTILE ? n - tile0 : (uint32_t)RTILE;
+
+  // tile histogram -> lbase (exclusive), reusing `run` as the counter
+  run[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t kk[RITEMS];
+#pragma unroll
+  for (int r = 0; r < RITEMS; ++r) {
+    const uint32_t i = r * RT + threadIdx.x;
+    kk[r] = i < cnt ? key_in[tile0 + i] : 0u;
+    if (i < cnt) atomicAdd(&run[(kk[r] >> shift) & (RADIX - 1)], 1u);
+  }
+  __syncthreads();
+  {
+    const uint32_t c = run[threadIdx.x];
+    uint32_t inc = c;  // block scan over the 256 digits (one per thread)
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(inc, off);
+      if (lane >= off) inc += o;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k2 = 0; k2 < w; ++k2) pre += wsum[k2];
+    lbase[threadIdx.x] = pre + inc - c;
+    run[threadIdx.x] = 0;
+  }
+  __syncthreads();
+
   for (int r = 0; r < RITEMS; ++r) {
 #pragma unroll
-    for (int k = 0; k < RT / 64; ++k) wcount[k][threadIdx.x] = 0;
+    for (int k2 = 0; k2 < RT / 64; ++k2) wcount[k2][threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t i = tile0 + r * RT + threadIdx.x;
-    const bool live = i < n;
-    uint32_t k = 0, v = 0, d = 0;
-    if (live) {
-      k = key_in[i];
-      v = val_in ? val_in[i] : i;
-      d = (k >> shift) & (RADIX - 1);
-    }
+    const uint32_t i = r * RT + threadIdx.x;
+    const bool live = i < cnt;
+    const uint32_t k = kk[r];
+    const uint32_t d = live ? (k >> shift) & (RADIX - 1) : 0u;
     uint64_t peer = __ballot(live);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -77,16 +112,25 @@ __global__ void __launch_bounds__(RT) k_digit_scatter(const uint32_t *__restrict
     if (live && wrank == 0) wcount[w][d] = __popcll(peer);
     __syncthreads();
     if (live) {
-      uint32_t pos = base[d] + wrank;
+      uint32_t pos = lbase[d] + run[d] + wrank;
       for (int k2 = 0; k2 < w; ++k2) pos += wcount[k2][d];
-      key_out[pos] = k;
-      val_out[pos] = v;
+      sk[pos] = k;
+      sv[pos] = val_in ? val_in[tile0 + i] : tile0 + i;
     }
     __syncthreads();
     uint32_t add = 0;
 #pragma unroll
     for (int k2 = 0; k2 < RT / 64; ++k2) add += wcount[k2][threadIdx.x];
-    base[threadIdx.x] += add;
+    run[threadIdx.x] += add;
+  }
+  __syncthreads();
+  // write out in local sorted order; gbase(d) = offs[d * tiles + tile]
+  for (uint32_t j = threadIdx.x; j < cnt; j += RT) {
+    const uint32_t k = sk[j];
+    const uint32_t d = (k >> shift) & (RADIX - 1);
+    const uint32_t gpos = offs[d * tiles + blockIdx.x] + (j - lbase[d]);
+    key_out[gpos] = k;
+    val_out[gpos] = sv[j];
   }
 }
 
@@ -116,11 +160,9 @@ void radix_sort_pairs(const uint32_t *key_in, const uint32_t *val_in, uint32_t *
   // ping-pong so that the last pass writes key_out/val_out
   const uint32_t *ki = key_in, *vi = val_in;
   for (int p = 0; p < passes; ++p) {
-    const bool last = p == passes - 1;
     // pass p writes out when (passes-1-p) is even, tmp otherwise
     uint32_t *ko = ((passes - 1 - p) % 2 == 0) ? key_out : key_tmp;
     uint32_t *vo = ((passes - 1 - p) % 2 == 0) ? val_out : val_tmp;
-    (void)last;
     k_digit_hist<<<tiles, RT, 0, st>>>(ki, n, 8 * p, tiles, counts);
     exclusive_scan_u32(counts, counts, (size_t)tiles * RADIX, ss, st);
     k_digit_scatter<<<tiles, RT, 0, st>>>(ki, vi, n, 8 * p, tiles, counts, ko, vo);

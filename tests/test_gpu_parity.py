@@ -171,3 +171,19 @@ def test_cli_matches_reference(tmp_path):
         assert out.read_bytes() == f.read()  # last pair wins (E10)
     p = subprocess.run([rk.CLI_PATH, str(inp), str(out), "0.3"], capture_output=True, text=True)
     assert p.returncode == 1  # odd ratio count: usage error (E9)
+
+
+def test_std_sort_segments_vs_restatement(gpu_ctx):
+    """The device introsort on adversarial segments: ties, sorted/reversed runs,
+    a median-of-3 killer (depth-limit heapsort), and segments past the LDS tier."""
+    from sort_cases import sort_cases
+    rng = np.random.default_rng(11)
+    segs = [c for c in sort_cases() if c.size > 0]
+    segs += [rng.integers(0, 3, n).astype(np.uint64) for n in (600, 2000, 9000)]
+    segs += [rng.integers(0, 1 << 20, 20000).astype(np.uint64)]
+    keys = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
+    perm = gpu_ctx.std_sort_segments(keys, off)
+    for a, b, s in zip(off[:-1], off[1:], segs):
+        want = ro.std_sort(s) + a
+        assert np.array_equal(perm[a:b], want), (int(a), s.size)

@@ -14,6 +14,7 @@ import pytest
 
 from conftest import EDGE, GOLDEN, ROOT, edge_cases
 from oracle import rk_oracle as ro
+from sort_cases import heap_fallbacks, mcilroy_killer, sort_cases
 
 
 @pytest.mark.parametrize("name,case", edge_cases(), ids=[n for n, _ in edge_cases()])
@@ -58,24 +59,6 @@ int main() {
 """
 
 
-def sort_cases():
-    rng = np.random.default_rng(7)
-    cases = [np.array([], np.uint64), np.array([5], np.uint64)]
-    for n in (2, 3, 16, 17, 18, 31, 64, 100, 257, 1000, 5000):
-        cases.append(rng.integers(0, 4, n).astype(np.uint64))        # heavy ties
-        cases.append(rng.integers(0, 1 << 40, n).astype(np.uint64))  # distinct
-    cases.append(np.zeros(300, np.uint64))
-    cases.append(np.arange(400, dtype=np.uint64)[::-1].copy())
-    # median-of-3 killer (Musser) to drive the heapsort fallback
-    k = 512
-    a = np.zeros(k, np.uint64)
-    for i in range(k // 2):
-        a[2 * i] = i + 1
-        a[2 * i + 1] = k // 2 + i + 1
-    cases.append(a)
-    return cases
-
-
 def test_std_sort_restatement_matches_libstdcxx(tmp_path):
     src = tmp_path / "h.cpp"
     src.write_text(HARNESS)
@@ -89,3 +72,8 @@ def test_std_sort_restatement_matches_libstdcxx(tmp_path):
         want = np.array([int(t) for t in line.split()], np.uint32)
         got = ro.std_sort(c)
         assert np.array_equal(got, want), len(c)
+
+
+def test_killer_reaches_heapsort():
+    for n in (100, 512, 1000, 3000):
+        assert heap_fallbacks(mcilroy_killer(n)) >= 1
