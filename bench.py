@@ -12,8 +12,9 @@ each classifying its OWN independent 50M-fragment set (weak scaling, no data-pat
 collective -- DESIGN.md "Multi-GPU"); a gloo barrier brackets the timed region and
 the max time over ranks is reported.
 
-Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the dominant device
-phase (algorithmic bytes / HIP-event time measured inside the timed steps),
+Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the dominant streaming
+kernel (the stable radix scatter: algorithmic bytes per launch / HIP-event launch
+time measured inside the timed steps; PMC HBM traffic from profiles/traffic.json),
 `cpu_baseline` (the reference built from its sources, oracle/_ref/ref_driver, on
 a bounded sample, 1 core), `phases_ms` (per-step device time per phase).
 """
@@ -46,20 +47,6 @@ CONFIGS = {
                  desc="cfg3: 50M fragments, 3 Gbp human-scale self-comparison"),
 }
 
-# Algorithmic bytes per processed fragment of each device phase: the minimum
-# HBM traffic the phase's job needs (DESIGN.md "Roofline accounting").
-PHASE_BYTES = {
-    "prep_keys": 8 + 8 + 8 + 4,          # x, y, len in; processing key out
-    "order_csr": 4 + 4 + 4 + 4,          # key in (hist + scatter), row out, rank fix
-    "gather_proc": 4 + 25 + 8 * 4 + 4 * 2 + 1,
-    "occupancy_csr": 2 * (4 + 4 + 4 + 4),
-    "sweep_x": 4 + 8 + 8 + 1 + 1 + 4,    # entry id, centre, length, state r/w, winner
-    "sweep_y": 4 + 8 + 8 + 1 + 1 + 4,
-    "group_roots": 1 + 1 + 4 + 4 + 4 * 2 + 4,
-    "member_csr": 4 + 4 + 4 + 4 + 8 + 4,
-    "group_sort": 2 * (8 + 4),           # (key, tag) read once and written once, in place
-    "emit": 4 + 4 + 4 + 4 + 4 + 1,
-}
 
 
 def dist_setup():
@@ -139,7 +126,7 @@ def load_traffic(kernel: str):
     try:
         with open(path) as fh:
             t = json.load(fh)
-        return t.get(kernel, {}).get("hbm_bytes_per_launch")
+        return t.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -208,15 +195,20 @@ def main():
     if rank != 0:
         return
     per_step = {k: v[0] / max(1, v[1]) for k, v in phases.items()}
-    dom = max(per_step, key=per_step.get)
-    dom_ms = per_step[dom]
-    achieved = PHASE_BYTES[dom] * st["n_proc"] / (dom_ms * 1e-3) / 1e9
-    traffic = load_traffic(dom)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                "traffic": traffic, "kernel": dom,
-                "algorithmic_bytes_per_fragment": PHASE_BYTES[dom],
-                "launch_ms": round(dom_ms, 4)}
+    # roofline of the dominant streaming kernel (the stable radix scatter: 17
+    # launches per step at cfg3), HIP events around each launch on the
+    # library's stream, inside the timed steps
+    kt = ctx.kernel_timing()
+    launch_ms = kt["total_ms"] / max(1, kt["launches"])
+    bytes_per_launch = kt["algo_bytes"] / max(1, kt["launches"])
+    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms else 0.0
+    traffic = load_traffic(kt["kernel"])
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic, "kernel": kt["kernel"],
+                "algorithmic_bytes_per_launch": round(bytes_per_launch),
+                "launch_ms": round(launch_ms, 4), "launches_per_step": kt["launches"] // args.steps,
+                "kernel_ms_per_step": round(kt["total_ms"] / args.steps, 3)}
     value = frags_total * args.steps / dt_max
     line = {
         "metric": METRIC,

@@ -70,9 +70,14 @@ typedef struct {
 } rk_params;
 
 typedef struct {
-  uint32_t *gid;       /* [n] group id per input row; UINT32_MAX = row in the dropped last bucket */
-  uint8_t *repval;     /* [n] 0 singleton / 1 representative / 2 repeated; 0xFF = dropped */
-  uint32_t *out_order; /* [n] input rows in the reference's output order; first n_out valid */
+  /* All three arrays are in OUTPUT order (the order of the reference's CSV
+   * rows, commonFunctions.cpp:126-128): entry k describes the k-th row written.
+   * Caller-allocated with n entries; the first n_out are filled.  Rows of the
+   * never-iterated last xStart/10 bucket (FragmentsDatabase.h:29-31) are not
+   * written. */
+  uint32_t *out_order; /* input row written k-th */
+  uint32_t *gid;       /* its group id: the `block` column, creation order */
+  uint8_t *repval;     /* its repeat flag: 0 singleton / 1 representative / 2 repeated */
   uint64_t n_out;      /* set by rk_classify*: rows written (= rows grouped) */
   uint64_t n_groups;   /* set by rk_classify*: groups created */
 } rk_result;
@@ -126,6 +131,12 @@ int rk_set_profiling(rk_ctx *ctx, int enable);
 int rk_get_phase_ms(const rk_ctx *ctx, double *ms /* [RK_N_PHASES] */,
                     uint32_t *calls /* nullable */);
 int rk_reset_phases(rk_ctx *ctx);
+/* Launch-level timing of the dominant streaming kernel (the stable radix
+ * scatter, k_digit_scatter) while profiling: summed HIP-event milliseconds,
+ * algorithmic bytes (16 B per element: key and value read once and written
+ * once) and number of launches since the last rk_reset_phases. */
+int rk_get_kernel_timing(const rk_ctx *ctx, double *total_ms, double *algo_bytes,
+                         uint64_t *launches);
 const char *rk_phase_name(int phase);
 
 /* ---- host ingress: FragmentsDatabase (FragmentsDatabase.cpp:17-101) ---- */

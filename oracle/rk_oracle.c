@@ -501,11 +501,8 @@ int rko_classify(uint64_t n, const uint64_t *x_start, const uint64_t *y_start,
   /* sequence lengths are header value + 1 (FragmentsDatabase.cpp:62,65) */
   const uint64_t len_x = len_x_hdr + 1, len_y = len_y_hdr + 1;
   const uint64_t vsize = 1 + len_x / 10; /* FragmentsDatabase.cpp:84 */
-  for (uint64_t i = 0; i < n; ++i) {
-    gid[i] = 0xFFFFFFFFu;
-    repval[i] = 0xFF;
+  for (uint64_t i = 0; i < n; ++i)
     if (x_start[i] / 10 >= vsize) return RKO_E_UB_BUCKET; /* :96-97 out of bounds */
-  }
   /* processing order: buckets xStart/10 in file order; end() stops before
    * bucket vsize-1 (FragmentsDatabase.h:29-31) */
   uint64_t *pk = (uint64_t *)malloc(n * sizeof *pk + 1);
@@ -624,10 +621,10 @@ int rko_classify(uint64_t n, const uint64_t *x_start, const uint64_t *y_start,
       rko_rec *a = mem + gstart[g];
       size_t sz = (size_t)(gstart[g + 1] - gstart[g]);
       if (sz > 1) rko_std_sort(a, sz);
-      for (size_t t = 0; t < sz; ++t) {
-        gid[a[t].tag] = g;
-        repval[a[t].tag] = sz == 1 ? 0 : (t == 0 ? 1 : 2);
-        out_order[w++] = a[t].tag;
+      for (size_t t = 0; t < sz; ++t, ++w) {
+        out_order[w] = a[t].tag;
+        gid[w] = g;
+        repval[w] = sz == 1 ? 0 : (t == 0 ? 1 : 2);
       }
     }
     *n_out = w;
@@ -665,10 +662,10 @@ int rko_write_csv(const char *path, const rko_db *db, const uint32_t *gid,
     fprintf(f, "Frag,%llu,%llu,%llu,%llu,%c,%llu,%llu,%llu,%llu,%g,%g,0,%u\n",
             (unsigned long long)db->x_start[i], (unsigned long long)db->y_start[i],
             (unsigned long long)db->x_end[i], (unsigned long long)db->y_end[i],
-            (char)db->strand[i], (unsigned long long)gid[i],
+            (char)db->strand[i], (unsigned long long)gid[k],
             (unsigned long long)db->length[i], (unsigned long long)db->score[i],
             (unsigned long long)db->ident[i], (double)db->similarity[i], (double)identity,
-            (unsigned)repval[i]);
+            (unsigned)repval[k]);
   }
   return fclose(f) == 0 ? RKO_OK : RKO_E_IO;
 }

@@ -46,9 +46,10 @@ int rko_load_csv(const char *path, rko_db *db);
 void rko_free_db(rko_db *db);
 
 /* Classify n fragments given in FILE order.  Outputs (caller-allocated, n
- * entries each): gid[i] / repval[i] per file row (UINT32_MAX / 0xFF for rows
- * in the dropped last xStart/10 bucket); out_order[k] = file row written k-th.
- * *n_out = rows written, *n_groups = groups created. */
+ * entries each, the first *n_out valid), all in OUTPUT order: out_order[k] =
+ * file row written k-th, gid[k] its group id (block column), repval[k] its
+ * repeat flag.  Rows of the dropped last xStart/10 bucket are not written.
+ * *n_groups = groups created. */
 int rko_classify(uint64_t n, const uint64_t *x_start, const uint64_t *y_start,
                  const uint64_t *length, const uint8_t *strand, uint64_t len_x_hdr,
                  uint64_t len_y_hdr, double len_ratio, double pos_ratio, uint32_t *gid,

@@ -59,7 +59,8 @@ def _p(a: np.ndarray) -> int:
 
 def classify(x_start, y_start, length, strand, len_x_hdr: int, len_y_hdr: int,
              len_ratio: float = 0.3, pos_ratio: float = 0.3):
-    """Returns (rc, gid, repval, out_order, n_groups) -- same contract as rk_classify."""
+    """Returns (rc, gid, repval, out_order, n_groups) -- same contract as rk_classify
+    (all three arrays in output order, length n_out)."""
     x = np.ascontiguousarray(x_start, np.uint64)
     y = np.ascontiguousarray(y_start, np.uint64)
     ln = np.ascontiguousarray(length, np.uint64)
@@ -72,7 +73,8 @@ def classify(x_start, y_start, length, strand, len_x_hdr: int, len_y_hdr: int,
     rc = lib().rko_classify(n, _p(x), _p(y), _p(ln), _p(s), len_x_hdr, len_y_hdr, len_ratio,
                             pos_ratio, _p(gid), _p(rep), _p(order), ctypes.byref(n_out),
                             ctypes.byref(n_groups))
-    return rc, gid, rep, order[:n_out.value].copy(), int(n_groups.value)
+    k = n_out.value
+    return rc, gid[:k].copy(), rep[:k].copy(), order[:k].copy(), int(n_groups.value)
 
 
 REC = np.dtype([("key", np.uint64), ("tag", np.uint32), ("pad", np.uint32)])

@@ -42,6 +42,7 @@ STATUS = {
 EXPORTS = (
     "rk_create", "rk_destroy", "rk_last_error", "rk_classify", "rk_classify_device",
     "rk_get_stats", "rk_std_sort_segments", "rk_set_profiling", "rk_get_phase_ms", "rk_reset_phases", "rk_phase_name",
+    "rk_get_kernel_timing",
     "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
     "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
     "rk_synth_write_csv",
@@ -70,8 +71,8 @@ class Params(ctypes.Structure):
 
 
 class Result(ctypes.Structure):
-    _fields_ = [("gid", ctypes.c_void_p), ("repval", ctypes.c_void_p),
-                ("out_order", ctypes.c_void_p), ("n_out", ctypes.c_uint64),
+    _fields_ = [("out_order", ctypes.c_void_p), ("gid", ctypes.c_void_p),
+                ("repval", ctypes.c_void_p), ("n_out", ctypes.c_uint64),
                 ("n_groups", ctypes.c_uint64)]
 
 
@@ -123,6 +124,8 @@ def load_library() -> ctypes.CDLL:
                                                 vp]),
         "rk_get_phase_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), _u32p]),
         "rk_reset_phases": (ctypes.c_int, [vp]),
+        "rk_get_kernel_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_double), _u64p]),
         "rk_phase_name": (ctypes.c_char_p, [ctypes.c_int]),
         "rk_db_load_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(vp)]),
         "rk_db_free": (None, [vp]),
@@ -193,13 +196,15 @@ def write_input_csv(path: str, f: Frags, len_x_hdr: int, len_y_hdr: int) -> None
 
 @dataclass
 class ClassifyResult:
-    gid: np.ndarray        # uint32 per input row; 0xFFFFFFFF = dropped (last xStart/10 bucket)
-    repval: np.ndarray     # uint8 per input row: 0/1/2; 0xFF = dropped
-    out_order: np.ndarray  # uint32 input rows in output order (length n_out)
+    """All arrays in OUTPUT order (length n_out): row k of the reference's CSV is
+    input row out_order[k], with group id gid[k] and repeat flag repval[k]."""
+    gid: np.ndarray        # uint32 group id (block column, creation order)
+    repval: np.ndarray     # uint8 0 singleton / 1 representative / 2 repeated
+    out_order: np.ndarray  # uint32 input row
     n_groups: int
 
     def as_struct(self) -> Result:
-        return Result(_ptr(self.gid), _ptr(self.repval), _ptr(self.out_order),
+        return Result(_ptr(self.out_order), _ptr(self.gid), _ptr(self.repval),
                       int(self.out_order.shape[0]), self.n_groups)
 
 
@@ -336,6 +341,14 @@ class Context:
             raise RkError(rc, self.last_error())
         return perm
 
+    def kernel_timing(self) -> dict:
+        """HIP-event timing of the radix scatter launches while profiling."""
+        ms, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        _check(load_library().rk_get_kernel_timing(self._h, ctypes.byref(ms), ctypes.byref(by),
+                                                   ctypes.byref(n)))
+        return {"kernel": "k_digit_scatter", "total_ms": ms.value, "algo_bytes": by.value,
+                "launches": n.value}
+
     def classify(self, f: Frags, len_x_hdr: int, len_y_hdr: int, len_ratio: float = 0.3,
                  pos_ratio: float = 0.3) -> ClassifyResult:
         """Host arrays in, host arrays out (rk_classify)."""
@@ -347,24 +360,26 @@ class Context:
         gid = np.empty(n, np.uint32)
         rep = np.empty(n, np.uint8)
         order = np.empty(n, np.uint32)
-        res = Result(_ptr(gid), _ptr(rep), _ptr(order), 0, 0)
+        res = Result(_ptr(order), _ptr(gid), _ptr(rep), 0, 0)
         prm = Params(len_x_hdr, len_y_hdr, len_ratio, pos_ratio)
         rc = load_library().rk_classify(self._h, ctypes.byref(soa), ctypes.byref(prm),
                                         ctypes.byref(res))
         if rc != RK_OK:
             raise RkError(rc, self.last_error())
-        return ClassifyResult(gid, rep, order[:res.n_out].copy(), int(res.n_groups))
+        k = res.n_out
+        return ClassifyResult(gid[:k].copy(), rep[:k].copy(), order[:k].copy(), int(res.n_groups))
 
     def classify_device(self, x, y, length, strand, gid, repval, out_order, len_x_hdr: int,
                         len_y_hdr: int, len_ratio: float = 0.3, pos_ratio: float = 0.3):
         """Device tensors (torch, on this context's GPU) in and out (rk_classify_device).
 
         Returns (n_out, n_groups).  Inputs: uint64/int64 x, y, length and uint8 strand;
-        outputs: int32/uint32 gid and out_order, uint8 repval, all of length n.
+        outputs: int32/uint32 gid and out_order, uint8 repval, all of length n, the
+        first n_out entries filled in output order.
         """
         n = int(x.shape[0])
         soa = FragsSoA(x.data_ptr(), y.data_ptr(), length.data_ptr(), strand.data_ptr(), n)
-        res = Result(gid.data_ptr(), repval.data_ptr(), out_order.data_ptr(), 0, 0)
+        res = Result(out_order.data_ptr(), gid.data_ptr(), repval.data_ptr(), 0, 0)
         prm = Params(len_x_hdr, len_y_hdr, len_ratio, pos_ratio)
         rc = load_library().rk_classify_device(self._h, ctypes.byref(soa), ctypes.byref(prm),
                                                ctypes.byref(res))

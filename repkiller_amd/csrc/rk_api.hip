@@ -43,6 +43,9 @@ struct rk_ctx {
   bool pev_used[RK_N_PHASES + 1] = {};
   double phase_ms[RK_N_PHASES] = {};
   uint32_t phase_calls[RK_N_PHASES] = {};
+  rk::KernelTimer kt{};   // radix scatter launches of the current call
+  double kt_ms = 0, kt_bytes = 0;
+  uint64_t kt_launches = 0;
 };
 
 static const char *kPhaseNames[RK_N_PHASES] = {
@@ -88,7 +91,7 @@ struct Work {
   size_t radix_words;
   rk::Proc p;
   rk::Csr cx, cy;
-  uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag, *otag;
+  uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag, *otag, *xres;
   void *gsort;
   uint64_t *reckey;
   uint32_t *rpend, *rbeg, *rlen, *runs, *rlen_at, *rbeg_at;
@@ -104,17 +107,17 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.tv = c.take<uint32_t>(n);
   w.radix_words = rk::radix_scratch_words((uint32_t)n);
   w.radix = c.take<uint32_t>(w.radix_words);
+  w.p.rec = c.take<ulonglong2>(2 * n);
+  w.p.ys = c.take<uint64_t>(n);
   w.p.pkey = c.take<uint32_t>(n);
   w.p.row = c.take<uint32_t>(n);
   w.p.xrec = c.take<ulonglong2>(n);
   w.p.yrec = c.take<ulonglong2>(n);
+  w.p.xres = c.take<uint32_t>(n);
   w.p.ha = c.take<uint64_t>(n);
   w.p.keyx = c.take<uint32_t>(n);
   w.p.keyy = c.take<uint32_t>(n);
-  w.p.xstate = c.take<uint8_t>(n);
-  w.p.ystate = c.take<uint8_t>(n);
-  w.p.xwin = c.take<uint32_t>(n);
-  w.p.ywin = c.take<uint32_t>(n);
+  w.xres = c.take<uint32_t>(n);
   w.p.par = c.take<uint32_t>(n);
   w.p.gid = c.take<uint32_t>(n);
   for (rk::Csr *cs : {&w.cx, &w.cy}) {
@@ -168,12 +171,27 @@ int ensure_ws(rk_ctx *ctx, const Plan &pl, Work &w) {
 // mark the START of phase `ph` (ph == RK_N_PHASES marks the end of the last)
 void mark(rk_ctx *ctx, int ph) {
   if (!ctx->profiling) return;
+  if (ph == RK_PH_PREP) {
+    ctx->kt.n = 0;
+    rk::g_ktimer = &ctx->kt;
+  }
   (void)hipEventRecord(ctx->pev[ph], ctx->stream);
   ctx->pev_used[ph] = true;
 }
 
 void collect_phases(rk_ctx *ctx) {
   if (!ctx->profiling) return;
+  rk::g_ktimer = nullptr;
+  if (ctx->kt.n) (void)hipEventSynchronize(ctx->kt.ev[2 * ctx->kt.n - 1]);
+  for (int i = 0; i < ctx->kt.n; ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->kt.ev[2 * i], ctx->kt.ev[2 * i + 1]) == hipSuccess) {
+      ctx->kt_ms += ms;
+      ctx->kt_bytes += 16.0 * (double)ctx->kt.elems[i];  // key+value read once, written once
+      ctx->kt_launches++;
+    }
+  }
+  ctx->kt.n = 0;
   (void)hipEventSynchronize(ctx->pev[RK_N_PHASES]);
   for (int ph = 0; ph < RK_N_PHASES; ++ph) {
     if (!ctx->pev_used[ph]) continue;
@@ -278,12 +296,11 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
 
   HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
   HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));
-  rk::fill_dropped(n, out->gid, out->repval, st);
   rk::Frags f{in->x_start, in->y_start, in->length, in->strand, n};
   mark(ctx, RK_PH_PREP);
 
   // 1-2: processing order = stable sort of rows by xStart/10 (dropped bucket last)
-  rk::prep_keys(f, pl.vsize, pl.max_x, pl.max_y, w.pkey_in, w.ctrl + 1, w.ctrl, st);
+  rk::prep_keys(f, pl.vsize, pl.max_x, pl.max_y, w.pkey_in, w.p.rec, w.ctrl + 1, w.ctrl, st);
   mark(ctx, RK_PH_ORDER);
   rk::radix_sort_pairs(w.pkey_in, nullptr, w.p.pkey, w.p.row, w.tk, w.tv, n,
                        rk::bit_length(pl.vsize - 1), w.radix, w.radix_words, st);
@@ -312,31 +329,28 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
                        rk::bit_length(2ull * pl.nbx - 1), w.radix, w.radix_words, st);
   rk::radix_sort_pairs(w.p.keyy, nullptr, w.cy.key, w.cy.ent, w.tk, w.tv, m,
                        rk::bit_length(2ull * pl.nby - 1), w.radix, w.radix_words, st);
-  rk::csr_fill(w.cx, w.p.xrec, nullptr, false, m, st);
+  rk::csr_fill_x(w.cx, w.p.xrec, m, st);
   HIPCHK(ctx, hipGetLastError());
 
-  // 5: X, then Y
+  // 5: X, then Y (X hits join the Y lists; X misses query Y)
   mark(ctx, RK_PH_SWEEP_X);
   rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, w.rlen_at,
-              w.rbeg_at, m, pl.max_x,
-              prm->len_ratio, prm->pos_ratio};
+              w.rbeg_at, m, pl.max_x, prm->len_ratio, prm->pos_ratio};
   if ((rc = resolve_axis(ctx, ax, w, ss, &ctx->stats.x_sweeps))) return rc;
-  rk::csr_scatter_back(w.cx, w.p.xstate, w.p.xwin, m, st);
+  rk::x_results(w.cx, w.p.xres, m, w.ctrl, st);
   mark(ctx, RK_PH_SWEEP_Y);
-  rk::csr_fill(w.cy, w.p.yrec, w.p.xstate, true, m, st);
+  rk::csr_fill_y(w.cy, w.p.yrec, w.p.xres, w.xres, m, st);
   rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.rlen_at,
-              w.rbeg_at, m, pl.max_y,
-              prm->len_ratio, prm->pos_ratio};
+              w.rbeg_at, m, pl.max_y, prm->len_ratio, prm->pos_ratio};
   if ((rc = resolve_axis(ctx, ay, w, ss, &ctx->stats.y_sweeps))) return rc;
-  rk::csr_scatter_back(w.cy, w.p.ystate, w.p.ywin, m, st);
 
   // 6: group roots and ids
   mark(ctx, RK_PH_ROOTS);
-  rk::make_parents(w.p, m, w.isnew, w.ctrl, st);
+  rk::y_parents(w.cy, w.xres, w.p.par, m, w.ctrl, st);
   HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
   for (;;) {
     HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
-    rk::jump_round(w.p, m, w.ctrl + 5, st);
+    rk::jump_round(w.p, m, w.ctrl + 5, ctx->stats.jump_rounds == 0 ? w.isnew : nullptr, st);
     if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
     ctx->stats.jump_rounds++;
     if (!ctx->host[0]) break;
@@ -398,6 +412,11 @@ extern "C" int rk_create(rk_ctx **out, int device) {
     rk_destroy(ctx);
     return RK_E_HIP;
   }
+  for (auto &e : ctx->kt.ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      rk_destroy(ctx);
+      return RK_E_HIP;
+    }
   for (auto &e : ctx->pev)
     if (hipEventCreate(&e) != hipSuccess) {
     rk_destroy(ctx);
@@ -417,6 +436,8 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   for (auto &e : ctx->pev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto &e : ctx->kt.ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -439,8 +460,19 @@ extern "C" int rk_get_phase_ms(const rk_ctx *ctx, double *ms, uint32_t *calls) {
   return RK_OK;
 }
 
+extern "C" int rk_get_kernel_timing(const rk_ctx *ctx, double *total_ms, double *algo_bytes,
+                                    uint64_t *launches) {
+  if (!ctx) return RK_E_ARG;
+  if (total_ms) *total_ms = ctx->kt_ms;
+  if (algo_bytes) *algo_bytes = ctx->kt_bytes;
+  if (launches) *launches = ctx->kt_launches;
+  return RK_OK;
+}
+
 extern "C" int rk_reset_phases(rk_ctx *ctx) {
   if (!ctx) return RK_E_ARG;
+  ctx->kt_ms = ctx->kt_bytes = 0;
+  ctx->kt_launches = 0;
   for (int i = 0; i < RK_N_PHASES; ++i) ctx->phase_ms[i] = 0, ctx->phase_calls[i] = 0;
   return RK_OK;
 }
@@ -459,12 +491,15 @@ extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const
                                   rk_result *out_dev) {
   if (!ctx) return RK_E_ARG;
   ctx->err.clear();
+  int rc;
   try {
-    return classify_device(ctx, in_dev, p, out_dev);
+    rc = classify_device(ctx, in_dev, p, out_dev);
   } catch (...) {
     ctx->err = "unexpected C++ exception";
-    return RK_E_INTERNAL;
+    rc = RK_E_INTERNAL;
   }
+  rk::g_ktimer = nullptr;  // never leave the radix timer pointing at this context
+  return rc;
 }
 
 extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t n,
@@ -542,16 +577,17 @@ extern "C" int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params 
     HIPCHK(ctx, hipMemcpyAsync(ds, in->strand, n, hipMemcpyHostToDevice, st));
   }
   rk_frags_soa din{dx, dy, dl, ds, n};
-  rk_result dres{dgid, drep, dord, 0, 0};
+  rk_result dres{dord, dgid, drep, 0, 0};
   int rc = rk_classify_device(ctx, &din, p, &dres);
   if (rc) return rc;
   out->n_out = dres.n_out;
   out->n_groups = dres.n_groups;
   if (n) {
-    HIPCHK(ctx, hipMemcpyAsync(out->gid, dgid, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(out->repval, drep, n, hipMemcpyDeviceToHost, st));
-    if (dres.n_out)
+    if (dres.n_out) {
       HIPCHK(ctx, hipMemcpyAsync(out->out_order, dord, dres.n_out * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(out->gid, dgid, dres.n_out * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(out->repval, drep, dres.n_out, hipMemcpyDeviceToHost, st));
+    }
     HIPCHK(ctx, hipStreamSynchronize(st));
   }
   return RK_OK;

@@ -119,7 +119,7 @@ int main(int argc, char **argv) {
   double t_class = 0, dev_ms = 0;
   for (auto &pr : params) {
     rk_params p{lx, ly, pr.first, pr.second};
-    rk_result res{gid.data(), rep.data(), order.data(), 0, 0};
+    rk_result res{order.data(), gid.data(), rep.data(), 0, 0};
     double a = now_s();
     rc = rk_classify(ctx, &soa, &p, &res);
     t_class += now_s() - a;

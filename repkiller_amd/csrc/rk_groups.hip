@@ -36,11 +36,15 @@ __device__ __forceinline__ uint64_t probe_max_bucket(uint64_t c, uint64_t max_in
 }
 
 __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t max_y,
-                            uint32_t *pkey, uint32_t *kept, uint32_t *err) {
+                            uint32_t *pkey, ulonglong2 *rec, uint32_t *kept, uint32_t *err) {
   uint32_t mine = 0;
   GRID_STRIDE(i, f.n) {
     const uint64_t x = f.x[i];
     const uint64_t pk = x / 10;
+    // pack the row once, coalesced, so the processing-order gather is one
+    // 32-B read per row instead of four scattered reads
+    rec[2 * (size_t)i] = make_ulonglong2(x, f.y[i]);
+    rec[2 * (size_t)i + 1] = make_ulonglong2(f.len[i], f.strand[i]);
     uint32_t key = (uint32_t)(vsize - 1);  // the never-iterated last bucket sorts last
     if (pk >= vsize) {
       atomicOr(err, ERRB_UB_BUCKET);
@@ -64,44 +68,94 @@ __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t ma
   }
 }
 
-// Processing-order SoA, bucket keys and the in-group sort key
-// |yStart - diag_func[xStart/10]|: diag_func[b] is the yStart of the LAST
-// fragment of processing bucket b, i.e. of the end of k's run of equal keys.
-__global__ void k_gather_proc(Frags f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
+// Processing-order SoA and bucket keys (one 32-B record gather per row).
+__global__ void k_gather_proc(Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
   GRID_STRIDE(k, m) {
     const uint32_t r = p.row[k];
-    const uint64_t L = f.len[r], x = f.x[r], y = f.y[r];
+    const ulonglong2 a = p.rec[2 * (size_t)r], b = p.rec[2 * (size_t)r + 1];
+    const uint64_t x = a.x, y = a.y, L = b.x;
     const uint64_t xc = x + L / 2, yc = y + L / 2;
-    const uint32_t s = f.strand[r] == 'f' ? 0u : 1u;
-    const uint32_t key = p.pkey[k];
-    uint32_t e = k;
-    while (e + 1 < m && p.pkey[e + 1] == key) ++e;
-    const uint64_t d = e == k ? y : f.y[p.row[e]];
+    const uint32_t s = b.y == 'f' ? 0u : 1u;
+    p.ys[k] = y;
     p.xrec[k] = make_ulonglong2(xc, L);
     p.yrec[k] = make_ulonglong2(yc, L);
-    p.ha[k] = y > d ? y - d : d - y;
     p.keyx[k] = s * nbx + (uint32_t)(xc / 100);
     p.keyy[k] = s * nby + (uint32_t)(yc / 100);
   }
 }
 
-__global__ void k_csr_fill(Csr c, const ulonglong2 *rec, const uint8_t *xstate, bool for_y,
-                           uint32_t m) {
-  GRID_STRIDE(q, m) {
-    const uint32_t k = c.ent[q];
-    const ulonglong2 r = rec[k];
-    c.cen[q] = r.x;
-    c.len[q] = r.y;
-    c.state[q] = for_y && xstate[k] == ST_HIT ? ST_ACTIVE : ST_UNKNOWN;
+// In-group sort key |yStart - diag_func[xStart/10]|: diag_func[b] is the yStart
+// of the LAST fragment of processing bucket b, i.e. of the end of k's run of
+// equal processing keys.  Run ends inside the wavefront come from a ballot and
+// a shuffle; only runs that cross the wave's end read further.
+__global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; base < m;
+       base += gridDim.x * blockDim.x) {
+    const uint32_t k = base + lane;
+    const bool in = k < m;
+    const uint32_t key = in ? p.pkey[k] : 0u;
+    const uint64_t y = in ? p.ys[k] : 0ull;
+    const bool end = in && (k + 1 == m || p.pkey[k + 1] != key);
+    const uint64_t ends = __ballot(end) & ~((1ull << lane) - 1ull);
+    const int src = ends ? __ffsll((unsigned long long)ends) - 1 : 63;
+    uint64_t d = __shfl(y, src);
+    if (in && !ends) {  // the run continues past this wave
+      uint32_t e = base + 63;
+      while (e + 1 < m && p.pkey[e + 1] == key) ++e;
+      d = p.ys[e];
+    }
+    if (in) p.ha[k] = y > d ? y - d : d - y;
   }
 }
 
-__global__ void k_csr_scatter_back(Csr c, uint8_t *state, uint32_t *win, uint32_t m) {
+__global__ void k_csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m) {
   GRID_STRIDE(q, m) {
-    const uint32_t k = c.ent[q];
+    const ulonglong2 r = xrec[c.ent[q]];
+    c.cen[q] = r.x;
+    c.len[q] = r.y;
+    c.state[q] = ST_UNKNOWN;
+  }
+}
+
+// X-CSR order is nearly processing order, so these writes stay local
+__global__ void k_x_results(Csr c, uint32_t *xres_proc, uint32_t m, uint32_t *err) {
+  GRID_STRIDE(q, m) {
     const uint8_t st = c.state[q];
-    state[k] = st;
-    if (st == ST_HIT) win[k] = c.win[q];
+    if (st != ST_HIT && st != ST_ACTIVE) atomicOr(err, ERRB_INTERNAL);
+    xres_proc[c.ent[q]] = st == ST_HIT ? c.win[q] : NONE;
+  }
+}
+
+__global__ void k_csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *xres_proc,
+                             uint32_t *xres, uint32_t m) {
+  GRID_STRIDE(q, m) {
+    const size_t k = c.ent[q];
+    const ulonglong2 a = yrec[k];
+    const uint32_t xr = xres_proc[k];
+    c.cen[q] = a.x;
+    c.len[q] = a.y;
+    c.state[q] = xr != NONE ? ST_ACTIVE : ST_UNKNOWN;  // X hits are inserted into Y
+    xres[q] = xr;
+  }
+}
+
+// generate_fragment_groups (commonFunctions.cpp:55-76): X hit -> X winner's
+// group; else Y hit -> Y winner's group; else a new group
+__global__ void k_y_parents(Csr c, const uint32_t *xres, uint32_t *par, uint32_t m,
+                            uint32_t *err) {
+  GRID_STRIDE(q, m) {
+    const uint32_t k = c.ent[q], xr = xres[q];
+    const uint8_t st = c.state[q];
+    uint32_t pa = k;
+    if (xr != NONE) pa = xr;
+    else if (st == ST_HIT) pa = c.win[q];
+    else if (st != ST_ACTIVE) atomicOr(err, ERRB_INTERNAL);
+    if (pa > k) {  // winners are always earlier; never let a bad id reach the gathers
+      atomicOr(err, ERRB_INTERNAL);
+      pa = k;
+    }
+    par[k] = pa;
   }
 }
 
@@ -113,27 +167,11 @@ __global__ void k_group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngrou
   if (blockIdx.x == 0 && threadIdx.x == 0) goff[ngroups] = m;
 }
 
-__global__ void k_make_parents(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err) {
-  GRID_STRIDE(k, m) {
-    const uint8_t xs = p.xstate[k], ys = p.ystate[k];
-    uint32_t par = k, nw = 0;
-    if (xs == ST_HIT) par = p.xwin[k];
-    else if (xs == ST_ACTIVE && ys == ST_HIT) par = p.ywin[k];
-    else if (xs == ST_ACTIVE && ys == ST_ACTIVE) nw = 1;
-    else atomicOr(err, ERRB_INTERNAL);
-    if (par > k) {  // winners are always earlier; never let a bad id reach the gathers
-      atomicOr(err, ERRB_INTERNAL);
-      par = k;
-    }
-    p.par[k] = par;
-    isnew[k] = nw;
-  }
-}
-
-__global__ void k_jump(Proc p, uint32_t m, uint32_t *changed) {
+__global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew) {
   bool ch = false;
   GRID_STRIDE(k, m) {
     const uint32_t a = p.par[k];
+    if (isnew) isnew[k] = a == k;
     const uint32_t b = p.par[a];
     if (a != b) {
       p.par[k] = b;
@@ -165,38 +203,45 @@ __global__ void k_emit(const uint32_t *tag, const uint32_t *gid_proc, const uint
     const uint32_t b = goff[g], e = goff[g + 1];
     const uint32_t r = row[k];
     out_order[t] = r;
-    out_gid[r] = g;
-    out_rep[r] = e - b == 1 ? 0 : (t == b ? 1 : 2);
+    out_gid[t] = g;
+    out_rep[t] = e - b == 1 ? 0 : (t == b ? 1 : 2);
   }
 }
 
 }  // namespace
 
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
-               uint32_t *kept, uint32_t *err, hipStream_t st) {
+               ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st) {
   if (f.n)
-    k_prep_keys<<<grid_for(f.n, 256, 2048), 256, 0, st>>>(f, vsize, max_x, max_y, pkey, kept, err);
+    k_prep_keys<<<grid_for(f.n, 256, 2048), 256, 0, st>>>(f, vsize, max_x, max_y, pkey, rec, kept,
+                                                           err);
 }
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st) {
   if (!m) return;
-  k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(f, p, m, nbx, nby);
+  (void)f;
+  k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(p, m, nbx, nby);
+  k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m);
 }
-void csr_fill(Csr c, const ulonglong2 *rec, const uint8_t *xstate, bool for_y, uint32_t m,
-              hipStream_t st) {
-  if (m) k_csr_fill<<<grid_for(m, 256), 256, 0, st>>>(c, rec, xstate, for_y, m);
+void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, hipStream_t st) {
+  if (m) k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m);
 }
-void csr_scatter_back(Csr c, uint8_t *state, uint32_t *win, uint32_t m, hipStream_t st) {
-  if (m) k_csr_scatter_back<<<grid_for(m, 256), 256, 0, st>>>(c, state, win, m);
+void x_results(Csr c, uint32_t *xres_proc, uint32_t m, uint32_t *err, hipStream_t st) {
+  if (m) k_x_results<<<grid_for(m, 256), 256, 0, st>>>(c, xres_proc, m, err);
+}
+void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *xres_proc, uint32_t *xres,
+                uint32_t m, hipStream_t st) {
+  if (m) k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, xres_proc, xres, m);
+}
+void y_parents(Csr c, const uint32_t *xres, uint32_t *par, uint32_t m, uint32_t *err,
+               hipStream_t st) {
+  if (m) k_y_parents<<<grid_for(m, 256), 256, 0, st>>>(c, xres, par, m, err);
 }
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st) {
   k_group_offsets<<<grid_for(m, 256), 256, 0, st>>>(sgid, m, ngroups, goff);
 }
-void make_parents(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, hipStream_t st) {
-  if (m) k_make_parents<<<grid_for(m, 256), 256, 0, st>>>(p, m, isnew, err);
-}
-void jump_round(Proc p, uint32_t m, uint32_t *changed, hipStream_t st) {
-  if (m) k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed);
+void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, hipStream_t st) {
+  if (m) k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed, isnew);
 }
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {
   if (m) k_assign_gid<<<grid_for(m, 256), 256, 0, st>>>(p, m, newrank);
@@ -211,10 +256,6 @@ void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *
   if (m)
     k_emit<<<grid_for(m, 256), 256, 0, st>>>(tag, gid_proc, goff, row, m, out_gid, out_rep,
                                              out_order);
-}
-void fill_dropped(uint32_t n, uint32_t *out_gid, uint8_t *out_rep, hipStream_t st) {
-  (void)hipMemsetAsync(out_gid, 0xFF, (size_t)n * sizeof(uint32_t), st);
-  (void)hipMemsetAsync(out_rep, 0xFF, (size_t)n, st);
 }
 
 }  // namespace rk

@@ -379,7 +379,7 @@ int write_csv(const rk_db *db, const char *path, const uint32_t *gid, const uint
             bad = true;
             break;
           }
-          o = format_row(o, db, i, gid[i], rep[i]);
+          o = format_row(o, db, i, gid[k], rep[k]);
         }
         s.resize((size_t)(o - s.data()));
       }
@@ -458,8 +458,9 @@ extern "C" int rk_saver_add(rk_saver *sq, const char *path, const rk_result *res
   if (!sq || !path || !res) return RK_E_ARG;
   rk_saver::Req r;
   r.path = path;
-  r.gid.assign(res->gid, res->gid + n);
-  r.rep.assign(res->repval, res->repval + n);
+  (void)n;
+  r.gid.assign(res->gid, res->gid + res->n_out);
+  r.rep.assign(res->repval, res->repval + res->n_out);
   r.order.assign(res->out_order, res->out_order + res->n_out);
   r.n_out = res->n_out;
   {

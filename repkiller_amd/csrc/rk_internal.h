@@ -44,6 +44,17 @@ size_t scan_blocks(size_t n);
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
                         hipStream_t st);
 
+// Launch-level HIP-event timer for the radix scatter kernel (the pipeline's
+// dominant streaming kernel), active only while a context profiles
+// (rk_set_profiling); set per thread by rk_classify_device.
+struct KernelTimer {
+  static constexpr int MAX = 96;
+  hipEvent_t ev[2 * MAX];
+  uint64_t elems[MAX];
+  int n;
+};
+extern thread_local KernelTimer *g_ktimer;
+
 // ----------------------------------------------------------- rk_radix.hip --
 size_t radix_scratch_words(uint32_t n);
 // stable sort of (key, value) by the low `bits` bits of key; val_in null =>
@@ -66,9 +77,9 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   uint64_t max_index;  // seq_size / 100 (SequenceOcupationList.cpp:4)
   double len_ratio, pos_ratio;
 };
-// The axis' bucket runs as a dense list sorted by length (short runs first):
-// beg/len (len exact below 255, clamped above), nshort = runs < WAVE_MIN (one
-// lane each), the rest one wavefront each.
+// The axis' bucket runs as a dense list sorted by length class (short runs
+// first): beg (+ len = class key), nshort = runs < WAVE_MIN (one lane each),
+// the rest one wavefront each.
 struct RunList {
   uint32_t *beg, *len;
   uint32_t nruns, nshort;
@@ -91,13 +102,15 @@ struct Frags {  // file-order inputs
   uint32_t n;
 };
 struct Proc {  // processing-order working set
+  ulonglong2 *rec; // FILE order: {xStart, yStart}, {length, strand} (one 32-B gather per row)
+  uint64_t *ys;    // yStart in processing order
   uint32_t *pkey;  // sorted xStart/10 key
   uint32_t *row;   // proc -> file row
-  ulonglong2 *xrec, *yrec;  // {centre, length} on each axis (one 16-B gather each)
+  ulonglong2 *xrec;  // {x centre, length}
+  ulonglong2 *yrec;  // {y centre, length}
+  uint32_t *xres;    // X result per fragment: X winner (X hit) or NONE (X miss)
   uint64_t *ha;
   uint32_t *keyx, *keyy;
-  uint8_t *xstate, *ystate;
-  uint32_t *xwin, *ywin;
   uint32_t *par, *gid;
 };
 struct Csr {  // one axis in CSR order (see Axis)
@@ -109,14 +122,21 @@ struct Csr {  // one axis in CSR order (see Axis)
 // processing key per file row (dropped last bucket -> vsize-1, sorts last);
 // counts kept rows into *kept; flags UB into *err
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
-               uint32_t *kept, uint32_t *err, hipStream_t st);
+               ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st);
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
-// centre/length/state in CSR order; for_y: state from the X result
-void csr_fill(Csr c, const ulonglong2 *rec, const uint8_t *xstate, bool for_y, uint32_t m,
-              hipStream_t st);
-void csr_scatter_back(Csr c, uint8_t *state, uint32_t *win, uint32_t m, hipStream_t st);
-void make_parents(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, hipStream_t st);
-void jump_round(Proc p, uint32_t m, uint32_t *changed, hipStream_t st);
+// X axis in CSR order: centre/length, state UNKNOWN
+void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, hipStream_t st);
+// X results (X-CSR order, i.e. nearly processing order) -> p.xres
+void x_results(Csr c, uint32_t *xres_proc, uint32_t m, uint32_t *err, hipStream_t st);
+// Y axis in CSR order: centre/length, state ACTIVE for X hits (they sit in the
+// Y list) else UNKNOWN; xres[q] = the entry's X result
+void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *xres_proc, uint32_t *xres,
+                uint32_t m, hipStream_t st);
+// parent of every fragment: X winner, else Y winner, else itself (new group)
+void y_parents(Csr c, const uint32_t *xres, uint32_t *par, uint32_t m, uint32_t *err,
+               hipStream_t st);
+// one pointer-jumping round; the first also writes isnew[k] = (par[k] == k)
+void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, hipStream_t st);
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st);
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st);
@@ -132,6 +152,5 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
 void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
                  const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st);
-void fill_dropped(uint32_t n, uint32_t *out_gid, uint8_t *out_rep, hipStream_t st);
 
 }  // namespace rk

@@ -136,21 +136,25 @@ __device__ __forceinline__ void count_pending(uint32_t *counters, bool pending) 
 }
 
 // ---- one lane walks one run ----------------------------------------------
-// Work items: the short runs (< WAVE_MIN <= 64 entries), sorted by length so
-// the 64 lanes of a wave walk runs of (nearly) equal length.  The run's own
+// Work items: the short runs (< WAVE_MIN <= 64 entries), sorted by length
+// class so the 64 lanes of a wave walk runs of similar length.  The run's own
 // states live in two 64-bit masks (bit t = entry beg+t): `act` = in the list,
-// `unk` = undecided.  A candidate scan then visits only set bits -- entries
-// that already hit cost nothing -- so the walk is O(len * active) instead of
-// O(len^2) memory reads.
+// `unk` = undecided, so entries that already hit are never touched again.
+// While the run holds at most ACACHE list entries their centre and length
+// stay in registers too: the typical run (a repeat copy's fragments -- one
+// list entry, every later fragment hits it) then reads each entry from memory
+// exactly once.
+constexpr int ACACHE = 4;
+
 __global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *run_beg,
-                                                    const uint32_t *run_len, uint32_t nruns,
-                                                    uint8_t *rpend, uint32_t *counters) {
+                                                    uint32_t nruns, uint8_t *rpend,
+                                                    uint32_t *counters) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   bool pending = false;
   if (w < nruns) {
     const uint32_t beg = run_beg[w];
     if (rpend[beg]) {
-      const uint32_t len = run_len[w];
+      const uint32_t len = ax.rlen_at[beg];
       const uint32_t key = ax.key[beg];
       uint64_t act = 0, unk = 0, todo = 0;
       for (uint32_t t = 0; t < len; ++t) {
@@ -159,6 +163,27 @@ __global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *run
         if (st == ST_ACTIVE) act |= bit;
         else if (st == ST_UNKNOWN) unk |= bit, todo |= bit;
         else if (st == ST_HIT_PENDING) todo |= bit;
+      }
+      // register cache of the list entries (ascending position)
+      uint32_t cp[ACACHE];
+      uint64_t cc[ACACHE], cl[ACACHE];
+      int nc = 0;
+      bool ovf = __popcll(act) > ACACHE;
+#pragma unroll
+      for (int j = 0; j < ACACHE; ++j) cp[j] = 64, cc[j] = 0, cl[j] = 0;
+      if (!ovf) {
+        uint64_t a = act;
+#pragma unroll
+        for (int j = 0; j < ACACHE; ++j) {
+          if (a) {
+            const uint32_t u = (uint32_t)__builtin_ctzll(a);
+            a &= a - 1;
+            cp[j] = u;
+            cc[j] = ax.cen[beg + u];
+            cl[j] = ax.len[beg + u];
+            nc = j + 1;
+          }
+        }
       }
       // neighbour runs, found lazily: 0 = not looked up, 1 = absent, 2 = present
       int lo_st = 0, hi_st = 0;
@@ -170,21 +195,39 @@ __global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *run
         const uint32_t q0 = beg + t;
         const uint64_t c = ax.cen[q0], L = ax.len[q0];
         Scan s{0.0, NONE, 0, false, false};
-        uint64_t cand = (act | unk) & (bit - 1);
-        while (cand) {  // newest first
-          const uint32_t u = 63 - (uint32_t)__builtin_clzll(cand);
-          cand &= ~(1ull << u);
-          const uint32_t q = beg + u;
-          const double d = deviation(c, L, ax.cen[q], ax.len[q], ax.len_ratio, ax.pos_ratio);
-          if (!(d > 0)) continue;
-          if ((act >> u) & 1ull) {
-            s.any_active = true;
-            if (d > s.best) {
-              s.best = d;
-              s.win = q;
+        const uint64_t below = bit - 1;
+        if (!ovf && (unk & below) == 0) {
+          // every candidate is a cached list entry: newest first
+#pragma unroll
+          for (int j = ACACHE - 1; j >= 0; --j) {
+            if (j < nc && cp[j] < t) {
+              const double d = deviation(c, L, cc[j], cl[j], ax.len_ratio, ax.pos_ratio);
+              if (d > 0) {
+                s.any_active = true;
+                if (d > s.best) {
+                  s.best = d;
+                  s.win = beg + cp[j];
+                }
+              }
             }
-          } else {
-            s.any_unknown = true;
+          }
+        } else {
+          uint64_t cand = (act | unk) & below;
+          while (cand) {  // newest first
+            const uint32_t u = 63 - (uint32_t)__builtin_clzll(cand);
+            cand &= ~(1ull << u);
+            const uint32_t q = beg + u;
+            const double d = deviation(c, L, ax.cen[q], ax.len[q], ax.len_ratio, ax.pos_ratio);
+            if (!(d > 0)) continue;
+            if ((act >> u) & 1ull) {
+              s.any_active = true;
+              if (d > s.best) {
+                s.best = d;
+                s.win = q;
+              }
+            } else {
+              s.any_unknown = true;
+            }
           }
         }
         const int dir = neighbour_dir(c, ax.max_index);
@@ -203,7 +246,26 @@ __global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *run
         if (ns == ST_HIT) ax.win[q0] = ax.ent[s.win];
         if (ns != ST_UNKNOWN) {
           unk &= ~bit;
-          if (ns == ST_ACTIVE) act |= bit;
+          if (ns == ST_ACTIVE) {
+            act |= bit;
+            // the cache must stay in ascending position (newest-first scans);
+            // in a re-walk an entry may be decided behind a cached later one,
+            // and a fifth list entry does not fit: both switch to memory reads
+            if (!ovf) {
+              uint32_t last = 0;
+#pragma unroll
+              for (int j = 0; j < ACACHE; ++j)
+                if (j + 1 == nc) last = cp[j];
+              if (nc < ACACHE && (nc == 0 || last < t)) {
+#pragma unroll
+                for (int j = 0; j < ACACHE; ++j)
+                  if (j == nc) cp[j] = t, cc[j] = c, cl[j] = L;
+                ++nc;
+              } else {
+                ovf = true;
+              }
+            }
+          }
           store_state(&ax.state[q0], ns);
         }
         pending |= ns == ST_UNKNOWN || ns == ST_HIT_PENDING;
@@ -312,15 +374,18 @@ __global__ void k_run_emit(Axis ax, const uint32_t *flag, const uint32_t *rank, 
     if (flag[p]) beg[rank[p]] = p;
 }
 
-// length key (exact below 256, clamped above); counts runs shorter than
-// WAVE_MIN (one atomic per block)
+// length CLASS key (1, 2, 3-4, 5-8, ..., 33-47, >= WAVE_MIN): a stable sort by
+// class keeps runs in position order inside a class, so the lanes of a wave
+// walk runs of similar length that also sit close together in memory (a sort
+// by exact length scatters them and every lane drags in its own cache lines).
+// Counts runs shorter than WAVE_MIN (one atomic per block).
 __global__ void __launch_bounds__(256) k_run_len(const uint32_t *beg, uint32_t nruns, uint32_t m,
                                                  uint32_t *lenkey, uint32_t *nshort) {
   uint32_t mine = 0;
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nruns;
        r += gridDim.x * blockDim.x) {
     const uint32_t len = (r + 1 < nruns ? beg[r + 1] : m) - beg[r];
-    lenkey[r] = len < 255 ? len : 255;
+    lenkey[r] = len >= WAVE_MIN ? 7u : (uint32_t)(32 - __clz((int)(len - 1)));  // ceil(log2)
     mine += len < WAVE_MIN;
   }
   __shared__ uint32_t part[4];
@@ -363,8 +428,8 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *scratch, uint32_t *radix_
   (void)hipMemsetAsync(dev_words, 0, 4, st);
   k_run_len<<<grid_for(rl.nruns, 256, 2048), 256, 0, st>>>(beg, rl.nruns, ax.m, lenkey, dev_words);
   k_run_tables<<<grid_for(rl.nruns, 256), 256, 0, st>>>(ax, beg, rl.nruns, ax.rlen_at, ax.rbeg_at);
-  // ascending length: short runs first, grouped by length; long runs last
-  radix_sort_pairs(lenkey, beg, rl.len, rl.beg, radix_k_tmp, radix_v_tmp, rl.nruns, 8,
+  // ascending class: short runs first, long runs (class 7) last
+  radix_sort_pairs(lenkey, beg, rl.len, rl.beg, radix_k_tmp, radix_v_tmp, rl.nruns, 3,
                    radix_scratch, radix_words, st);
   (void)hipMemcpyAsync(host_words, dev_words, 4, hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
@@ -375,7 +440,7 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
                      hipStream_t st) {
   (void)hipMemsetAsync(counters, 0, PEND_SLOTS * sizeof(uint32_t), st);
   if (rl.nshort)
-    k_sweep_lane<<<(rl.nshort + 255) / 256, 256, 0, st>>>(ax, rl.beg, rl.len, rl.nshort, rpend,
+    k_sweep_lane<<<(rl.nshort + 255) / 256, 256, 0, st>>>(ax, rl.beg, rl.nshort, rpend,
                                                           counters);
   const uint32_t nbig = rl.nruns - rl.nshort;
   if (nbig)
