@@ -21,7 +21,7 @@ int main(int argc, char **argv) {
     return 2;
   }
   double lr = atof(argv[3]), pr = atof(argv[4]);
-  if (!(lr > 0) || !(pr > 0)) {
+  if (lr <= 0 || pr <= 0) {  /* commonFunctions.cpp:26-27: NaN passes */
     fprintf(stderr, "ratios must be greater than zero\n");
     return 1;
   }

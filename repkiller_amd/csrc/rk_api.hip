@@ -94,7 +94,8 @@ struct Work {
   uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag, *otag, *xres;
   void *gsort;
   uint64_t *reckey;
-  uint32_t *rpend, *rbeg, *rlen, *runs, *rlen_at, *rbeg_at;
+  uint32_t *rpend, *runs, *rlen_at, *rbeg_at;
+  uint8_t *wpend;
   uint32_t *scan;
   size_t scan_cap;
 };
@@ -138,8 +139,7 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.gsort = c.take<uint8_t>(rk::groupsort_scratch_bytes((uint32_t)n));
   w.reckey = c.take<uint64_t>(n);
   w.rpend = c.take<uint32_t>(n / 4 + 1);
-  w.rbeg = c.take<uint32_t>(n);
-  w.rlen = c.take<uint32_t>(n);
+  w.wpend = c.take<uint8_t>(n / 64 + 1);
   w.runs = c.take<uint32_t>(rk::runs_scratch_words((uint32_t)n));
   w.rlen_at = c.take<uint32_t>(n);
   w.rbeg_at = c.take<uint32_t>(n);
@@ -237,9 +237,8 @@ int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss,
                  uint32_t *sweeps) {
   uint32_t *counters = w.ctrl + 64;
   uint8_t *rpend = reinterpret_cast<uint8_t *>(w.rpend);
-  rk::RunList rl{w.rbeg, w.rlen, 0, 0};
-  rk::build_runs(ax, rl, w.runs, w.tk, w.tv, w.radix, w.radix_words, ss, w.ctrl + 2,
-                 ctx->host + 128, ctx->stream);
+  rk::RunList rl{w.runs, w.wpend, 0, 0};
+  rk::build_runs(ax, rl, w.ctrl + 2, ctx->host + 128, ctx->stream);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));
   *sweeps = 0;
@@ -263,7 +262,7 @@ int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss,
 int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, rk_result *out) {
   if (!ctx || !in || !prm || !out) return RK_E_ARG;
   if (in->n >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
-  if (!(prm->len_ratio > 0) || !(prm->pos_ratio > 0)) {
+  if (prm->len_ratio <= 0 || prm->pos_ratio <= 0) {  // NaN passes, as in the reference
     ctx->err = "ratios must be greater than zero (commonFunctions.cpp:26-27)";
     return RK_E_ARG;
   }

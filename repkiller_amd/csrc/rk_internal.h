@@ -77,20 +77,20 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   uint64_t max_index;  // seq_size / 100 (SequenceOcupationList.cpp:4)
   double len_ratio, pos_ratio;
 };
-// The axis' bucket runs as a dense list sorted by length class (short runs
-// first): beg (+ len = class key), nshort = runs < WAVE_MIN (one lane each),
-// the rest one wavefront each.
+// The axis' bucket runs: the 64-position windows (wpend[w] = window w still
+// owns undecided entries) and the runs longer than 64 entries (big, nbig),
+// which take a wavefront each.  build_runs also fills Axis::rlen_at/rbeg_at.
 struct RunList {
-  uint32_t *beg, *len;
-  uint32_t nruns, nshort;
+  uint32_t *big;
+  uint8_t *wpend;
+  uint32_t nbig, nwin;
 };
 size_t runs_scratch_words(uint32_t m);
-void build_runs(const Axis &ax, RunList &rl, uint32_t *scratch, uint32_t *radix_k_tmp,
-                uint32_t *radix_v_tmp, uint32_t *radix_scratch, size_t radix_words,
-                ScanScratch ss, uint32_t *dev_words, uint32_t *host_words, hipStream_t st);
-// One sweep.  rpend[p] (run start p) = run still has undecided entries; set
-// to 1 everywhere before the first sweep.  counters: PEND_WORDS words, their
-// sum is the number of runs still pending after the sweep.
+void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host_words,
+                hipStream_t st);
+// One sweep.  rpend[p] (start p of a long run) = run still has undecided
+// entries; set to 1 before the first sweep.  counters: PEND_WORDS words, their
+// sum is the number of waves/runs still pending after the sweep.
 constexpr uint32_t PEND_WORDS = 64;
 void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
                      hipStream_t st);

@@ -27,8 +27,9 @@
 // before / after it when non-empty.  Centre, length, state and winner live in
 // that CSR order, so a bucket walk reads contiguous memory.
 //
-// Each sweep walks every listed run in processing order (one lane per run, or
-// one wavefront per run of >= WAVE_MIN entries), deciding an entry when the
+// Each sweep walks every run in processing order (the short runs of a
+// 64-position window by one wavefront, k_sweep_tile; each run longer than
+// LONG_RUN by a wavefront of its own, k_sweep_wave), deciding an entry when the
 // states of all its candidates with deviation > 0 are known: any ACTIVE
 // candidate => HIT (winner = first strict maximum in scan order), else all
 // candidates inactive => ACTIVE.  Own-run candidates are decided earlier in the
@@ -45,8 +46,6 @@
 namespace rk {
 namespace {
 
-constexpr uint32_t WAVE_MIN = 48;  // runs at least this long get a whole wavefront (<= 64)
-
 __device__ __forceinline__ double deviation(uint64_t c, uint64_t L, uint64_t oc, uint64_t oL,
                                             double lr, double pr) {
   uint64_t dl = L > oL ? L - oL : oL - L;
@@ -56,6 +55,42 @@ __device__ __forceinline__ double deviation(uint64_t c, uint64_t L, uint64_t oc,
   double sp = -fabs((double)dc / ((double)L * pr)) + 1.0;
   if (sp < 0) return 0.0;
   return sl * 0.4 + sp * 0.6;
+}
+
+// "deviation > 0" without the two divisions.  For a double a >= 0 (an exactly
+// converted integer) and a double b > 0, fl(a/b) > 1 exactly when a > b and
+// fl(a/b) == 1 exactly when a == b: two doubles that differ have a quotient at
+// least 2^-53 (relative) away from 1, which never rounds to 1.  So with
+// bl = fl(L*lr): sl < 0 <=> (double)dl > bl and sl == 0 <=> (double)dl == bl,
+// likewise for sp, and d = 0.4*sl + 0.6*sp > 0 <=> sl >= 0, sp >= 0 and not
+// both zero.  A zero query length or a NaN ratio makes every reference
+// quotient inf/NaN, and such a query never matches.
+struct Query {
+  uint64_t c, L;
+  uint64_t tl, tc;  // floor(bl), floor(bc) when both are < 2^53 (`fast`)
+  double bl, bc;
+  bool ok, fast, eq;  // eq: bl and bc are both integral
+};
+__device__ __forceinline__ Query make_query(uint64_t c, uint64_t L, double lr, double pr) {
+  Query q;
+  q.c = c;
+  q.L = L;
+  q.bl = (double)L * lr;
+  q.bc = (double)L * pr;
+  q.ok = L != 0 && q.bl == q.bl && q.bc == q.bc;
+  // below 2^53 every integer converts exactly: (double)d <= b <=> d <= floor(b)
+  q.fast = q.bl < 9007199254740992.0 && q.bc < 9007199254740992.0;
+  q.tl = q.fast ? (uint64_t)q.bl : 0;
+  q.tc = q.fast ? (uint64_t)q.bc : 0;
+  q.eq = q.fast && (double)q.tl == q.bl && (double)q.tc == q.bc;
+  return q;
+}
+__device__ __forceinline__ bool matches(const Query &q, uint64_t oc, uint64_t oL) {
+  const uint64_t dl = q.L > oL ? q.L - oL : oL - q.L;
+  const uint64_t dc = q.c > oc ? q.c - oc : oc - q.c;
+  if (q.fast) return q.ok && dl <= q.tl && dc <= q.tc && !(q.eq && dl == q.tl && dc == q.tc);
+  const double al = (double)dl, ac = (double)dc;
+  return q.ok && al <= q.bl && ac <= q.bc && !(al == q.bl && ac == q.bc);
 }
 
 // -1: bucket B-1, +1: bucket B+1, 0: none
@@ -81,14 +116,14 @@ struct Scan {
   bool any_active, any_unknown;
 };
 
-__device__ __forceinline__ void consider(const Axis &ax, Scan &s, uint32_t q, uint64_t c,
-                                         uint64_t L) {
+__device__ __forceinline__ void consider(const Axis &ax, Scan &s, uint32_t q, const Query &qy) {
   const uint8_t sj = load_state(&ax.state[q]);
   if (sj >= ST_HIT_PENDING) return;  // not in the list
-  const double d = deviation(c, L, ax.cen[q], ax.len[q], ax.len_ratio, ax.pos_ratio);
-  if (!(d > 0)) return;
+  const uint64_t oc = ax.cen[q], oL = ax.len[q];
+  if (!matches(qy, oc, oL)) return;
   if (sj == ST_ACTIVE) {
     s.any_active = true;
+    const double d = deviation(qy.c, qy.L, oc, oL, ax.len_ratio, ax.pos_ratio);
     if (d > s.best) {
       s.best = d;
       s.win = q;
@@ -121,9 +156,6 @@ __device__ __forceinline__ bool neighbour_run(const Axis &ax, uint32_t beg, uint
   return true;
 }
 
-__device__ __forceinline__ bool run_start(const Axis &ax, uint32_t p) {
-  return p == 0 || ax.key[p] != ax.key[p - 1];
-}
 
 // pending-run counters are spread over PEND_WORDS words (one hot word
 // serialises at ~88 atomics/us); the host sums them
@@ -135,143 +167,211 @@ __device__ __forceinline__ void count_pending(uint32_t *counters, bool pending) 
     atomicAdd(&counters[(blockIdx.x * 4 + (threadIdx.x >> 6)) % PEND_SLOTS], (uint32_t)__popcll(b));
 }
 
-// ---- one lane walks one run ----------------------------------------------
-// Work items: the short runs (< WAVE_MIN <= 64 entries), sorted by length
-// class so the 64 lanes of a wave walk runs of similar length.  The run's own
-// states live in two 64-bit masks (bit t = entry beg+t): `act` = in the list,
-// `unk` = undecided, so entries that already hit are never touched again.
-// While the run holds at most ACACHE list entries their centre and length
-// stay in registers too: the typical run (a repeat copy's fragments -- one
-// list entry, every later fragment hits it) then reads each entry from memory
-// exactly once.
-constexpr int ACACHE = 4;
+// ---- one wavefront decides the short runs that start in a 64-position window
+// Window w = positions [64w, 64w+64).  The wave OWNS every run of at most
+// LONG_RUN entries that starts in its window, so everything it owns lies in
+// [64w, 64w+128): lane l holds slot 0 (position 64w+l) and slot 1 (64w+64+l).
+// Loads are coalesced, and each entry's centre/length/id sit in LDS for the
+// other lanes.  Every undecided owned entry first records its candidates with
+// deviation > 0 as bit masks over the 128 window positions: earlier entries
+// of its own run, and the entries inserted before it of the neighbour run when
+// that run is owned by the wave too.  A neighbour run owned elsewhere (an
+// earlier window's run, a later window's run, or a long run) is scanned once
+// from global memory into a fixed summary.  Decisions then proceed in rounds
+// of four ballots: an entry with an ACTIVE candidate has hit (it leaves the
+// list); one whose candidates are all decided is final -- a hit takes the
+// first strict maximum in scan order (own run newest first, then the
+// neighbour run newest first), a miss becomes ACTIVE.  Rounds repeat while
+// anything changes; what is still open waits for the next sweep.
+constexpr uint32_t LONG_RUN = 64;  // runs longer than this take a whole wavefront each
 
-__global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *run_beg,
-                                                    uint32_t nruns, uint8_t *rpend,
+struct M128 {
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ void set_bit(M128 &m, int u) {
+  if (u < 64) m.lo |= 1ull << u;
+  else m.hi |= 1ull << (u - 64);
+}
+__device__ __forceinline__ bool any_and(const M128 &a, const M128 &b) {
+  return ((a.lo & b.lo) | (a.hi & b.hi)) != 0;
+}
+// highest set bit <= P (-1 if none) / lowest set bit > P (128 if none)
+__device__ __forceinline__ int hs_le(uint64_t s0, uint64_t s1, int P) {
+  if (P >= 64) {
+    const uint64_t m = s1 & ((2ull << (P - 64)) - 1ull);
+    if (m) return 127 - __clzll(m);
+    P = 63;
+  }
+  const uint64_t m = s0 & ((2ull << P) - 1ull);
+  return m ? 63 - __clzll(m) : -1;
+}
+__device__ __forceinline__ int ls_gt(uint64_t s0, uint64_t s1, int P) {
+  if (P < 64) {
+    const uint64_t m = s0 & ~((2ull << P) - 1ull);
+    if (m) return __builtin_ctzll(m);
+    return s1 ? 64 + __builtin_ctzll(s1) : 128;
+  }
+  const uint64_t m = s1 & ~((2ull << (P - 64)) - 1ull);
+  return m ? 64 + __builtin_ctzll(m) : 128;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(256) k_sweep_tile(Axis ax, uint8_t *wpend, uint32_t nwin,
                                                     uint32_t *counters) {
-  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint64_t s_cen[4][128], s_len[4][128];
+  __shared__ uint32_t s_ent[4][128], s_key[4][128];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.x * 4 + wv;
   bool pending = false;
-  if (w < nruns) {
-    const uint32_t beg = run_beg[w];
-    if (rpend[beg]) {
-      const uint32_t len = ax.rlen_at[beg];
-      const uint32_t key = ax.key[beg];
-      uint64_t act = 0, unk = 0, todo = 0;
-      for (uint32_t t = 0; t < len; ++t) {
-        const uint8_t st = ax.state[beg + t];
-        const uint64_t bit = 1ull << t;
-        if (st == ST_ACTIVE) act |= bit;
-        else if (st == ST_UNKNOWN) unk |= bit, todo |= bit;
-        else if (st == ST_HIT_PENDING) todo |= bit;
-      }
-      // register cache of the list entries (ascending position)
-      uint32_t cp[ACACHE];
-      uint64_t cc[ACACHE], cl[ACACHE];
-      int nc = 0;
-      bool ovf = __popcll(act) > ACACHE;
+  if (w < nwin && wpend[w]) {
+    uint64_t *cen = s_cen[wv], *len = s_len[wv];
+    uint32_t *ent = s_ent[wv], *key = s_key[wv];
+    const uint32_t base = w * 64, m = ax.m;
+    // run starts over the 128 positions (positions >= m count as starts)
+    uint64_t S[2];
 #pragma unroll
-      for (int j = 0; j < ACACHE; ++j) cp[j] = 64, cc[j] = 0, cl[j] = 0;
-      if (!ovf) {
-        uint64_t a = act;
-#pragma unroll
-        for (int j = 0; j < ACACHE; ++j) {
-          if (a) {
-            const uint32_t u = (uint32_t)__builtin_ctzll(a);
-            a &= a - 1;
-            cp[j] = u;
-            cc[j] = ax.cen[beg + u];
-            cl[j] = ax.len[beg + u];
-            nc = j + 1;
-          }
-        }
-      }
-      // neighbour runs, found lazily: 0 = not looked up, 1 = absent, 2 = present
-      int lo_st = 0, hi_st = 0;
-      uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
-      while (todo) {
-        const uint32_t t = (uint32_t)__builtin_ctzll(todo);
-        const uint64_t bit = 1ull << t;
-        todo &= todo - 1;
-        const uint32_t q0 = beg + t;
-        const uint64_t c = ax.cen[q0], L = ax.len[q0];
-        Scan s{0.0, NONE, 0, false, false};
-        const uint64_t below = bit - 1;
-        if (!ovf && (unk & below) == 0) {
-          // every candidate is a cached list entry: newest first
-#pragma unroll
-          for (int j = ACACHE - 1; j >= 0; --j) {
-            if (j < nc && cp[j] < t) {
-              const double d = deviation(c, L, cc[j], cl[j], ax.len_ratio, ax.pos_ratio);
-              if (d > 0) {
-                s.any_active = true;
-                if (d > s.best) {
-                  s.best = d;
-                  s.win = beg + cp[j];
-                }
-              }
-            }
-          }
-        } else {
-          uint64_t cand = (act | unk) & below;
-          while (cand) {  // newest first
-            const uint32_t u = 63 - (uint32_t)__builtin_clzll(cand);
-            cand &= ~(1ull << u);
-            const uint32_t q = beg + u;
-            const double d = deviation(c, L, ax.cen[q], ax.len[q], ax.len_ratio, ax.pos_ratio);
-            if (!(d > 0)) continue;
-            if ((act >> u) & 1ull) {
-              s.any_active = true;
-              if (d > s.best) {
-                s.best = d;
-                s.win = q;
-              }
-            } else {
-              s.any_unknown = true;
-            }
-          }
-        }
-        const int dir = neighbour_dir(c, ax.max_index);
-        if (dir) {
-          int &nst = dir < 0 ? lo_st : hi_st;
-          uint32_t &nb = dir < 0 ? lo_b : hi_b;
-          uint32_t &ne = dir < 0 ? lo_e : hi_e;
-          if (nst == 0) nst = neighbour_run(ax, beg, beg + len, key, dir, nb, ne) ? 2 : 1;
-          if (nst == 2) {
-            const uint32_t i = ax.ent[q0];
-            for (uint32_t q = ne; q-- > nb;)  // newest first, only entries inserted before i
-              if (ax.ent[q] < i) consider(ax, s, q, c, L);
-          }
-        }
-        const uint8_t ns = decide(s);
-        if (ns == ST_HIT) ax.win[q0] = ax.ent[s.win];
-        if (ns != ST_UNKNOWN) {
-          unk &= ~bit;
-          if (ns == ST_ACTIVE) {
-            act |= bit;
-            // the cache must stay in ascending position (newest-first scans);
-            // in a re-walk an entry may be decided behind a cached later one,
-            // and a fifth list entry does not fit: both switch to memory reads
-            if (!ovf) {
-              uint32_t last = 0;
-#pragma unroll
-              for (int j = 0; j < ACACHE; ++j)
-                if (j + 1 == nc) last = cp[j];
-              if (nc < ACACHE && (nc == 0 || last < t)) {
-#pragma unroll
-                for (int j = 0; j < ACACHE; ++j)
-                  if (j == nc) cp[j] = t, cc[j] = c, cl[j] = L;
-                ++nc;
-              } else {
-                ovf = true;
-              }
-            }
-          }
-          store_state(&ax.state[q0], ns);
-        }
-        pending |= ns == ST_UNKNOWN || ns == ST_HIT_PENDING;
-      }
-      rpend[beg] = pending;
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t p = base + 64 * s + lane;
+      const uint32_t k = p < m ? ax.key[p] : NONE;
+      key[64 * s + lane] = k;
+      S[s] = __ballot(p >= m || p == 0 || ax.key[p - 1] != k);
     }
+    // ownership: the run starts in [0, 64) and ends within LONG_RUN entries
+    bool own[2];
+    int rs[2], re[2];
+    uint8_t st[2], st0[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int P = 64 * s + lane;
+      rs[s] = hs_le(S[0], S[1], P);
+      re[s] = ls_gt(S[0], S[1], P);
+      own[s] = base + P < m && rs[s] >= 0 && rs[s] < 64 && re[s] - rs[s] <= (int)LONG_RUN;
+      st[s] = ST_HIT;
+      if (own[s]) {
+        const uint32_t p = base + P;
+        cen[P] = ax.cen[p];
+        len[P] = ax.len[p];
+        ent[P] = ax.ent[p];
+        st[s] = ax.state[p];
+      }
+      st0[s] = st[s];
+    }
+    wave_sync_lds();
+    // candidates (deviation > 0) of every undecided owned entry, as masks:
+    // earlier entries of its own run (rown), entries of an owned neighbour
+    // run inserted before it (rnb, a prefix: ids ascend inside a run); a
+    // foreign neighbour run is scanned once from global memory into fs
+    M128 rown[2], rnb[2];
+    Query qy[2];
+    Scan fs[2];
+    uint32_t fwin_ent[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      rown[s] = rnb[s] = M128{0, 0};
+      fs[s] = Scan{0.0, NONE, 0, false, false};
+      fwin_ent[s] = NONE;
+      if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
+      const int P = 64 * s + lane;
+      const uint64_t c = cen[P], L = len[P];
+      const uint32_t i = ent[P], k = key[P];
+      qy[s] = make_query(c, L, ax.len_ratio, ax.pos_ratio);
+      for (int u = rs[s]; u < P; ++u)
+        if (matches(qy[s], cen[u], len[u])) set_bit(rown[s], u);
+      const int dir = neighbour_dir(c, ax.max_index);
+      if (!dir) continue;
+      uint32_t gb = 0, ge = 0;
+      bool foreign = false;
+      int nb = -1, ne = -1;
+      if (dir < 0) {
+        const int q = rs[s] - 1;
+        if (q >= 0) {
+          if (key[q] == k - 1) {
+            const int b2 = hs_le(S[0], S[1], q);
+            if (b2 >= 0) nb = b2, ne = rs[s];
+            else foreign = true, ge = base + rs[s], gb = ax.rbeg_at[ge - 1];
+          }
+        } else if (base > 0 && ax.key[base - 1] == k - 1) {
+          foreign = true, ge = base, gb = ax.rbeg_at[base - 1];
+        }
+      } else {
+        const int q = re[s];
+        const uint32_t gq = base + q;
+        if (gq < m) {
+          const uint32_t kq = q < 128 ? key[q] : ax.key[gq];
+          if (kq == k + 1) {
+            const int e2 = q < 127 ? ls_gt(S[0], S[1], q) : 128;
+            if (q < 64 && e2 - q <= (int)LONG_RUN && e2 < 128) nb = q, ne = e2;
+            else foreign = true, gb = gq, ge = gq + ax.rlen_at[gq];
+          }
+        }
+      }
+      if (nb >= 0) {
+        for (int u = nb; u < ne && ent[u] < i; ++u)
+          if (matches(qy[s], cen[u], len[u])) set_bit(rnb[s], u);
+      } else if (foreign) {
+        for (uint32_t q = ge; q-- > gb;)  // newest first, only entries inserted before i
+          if (ax.ent[q] < i) consider(ax, fs[s], q, qy[s]);
+        if (fs[s].win != NONE) fwin_ent[s] = ax.ent[fs[s].win];
+      }
+    }
+    // rounds of ballots: an ACTIVE candidate means a hit; an UNKNOWN one
+    // blocks the final decision (it may still become ACTIVE and win)
+    for (;;) {
+      const M128 A{__ballot(own[0] && st[0] == ST_ACTIVE), __ballot(own[1] && st[1] == ST_ACTIVE)};
+      const M128 U{__ballot(own[0] && st[0] == ST_UNKNOWN), __ballot(own[1] && st[1] == ST_UNKNOWN)};
+      bool changed = false;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
+        const bool has_act = any_and(rown[s], A) || any_and(rnb[s], A) || fs[s].any_active;
+        const bool has_unk = any_and(rown[s], U) || any_and(rnb[s], U) || fs[s].any_unknown;
+        if (st[s] == ST_UNKNOWN) {
+          if (has_act) st[s] = ST_HIT_PENDING, changed = true;
+          else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
+        }
+        if (st[s] == ST_HIT_PENDING && !has_unk) st[s] = ST_HIT, changed = true;
+      }
+      if (!__ballot(changed)) break;
+    }
+    const M128 A{__ballot(own[0] && st[0] == ST_ACTIVE), __ballot(own[1] && st[1] == ST_ACTIVE)};
+    // winners (the matching ACTIVE candidates in scan order) and write-back
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (!own[s]) continue;
+      pending |= st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING;
+      if (st[s] == st0[s]) continue;
+      const int P = 64 * s + lane;
+      const uint32_t p = base + P;
+      if (st[s] == ST_HIT) {
+        const uint64_t c = cen[P], L = len[P];
+        double best = 0.0;
+        uint32_t win = NONE;
+#pragma unroll
+        for (int part = 0; part < 2; ++part) {  // own run newest first, then the neighbour's
+          const M128 r = part ? rnb[s] : rown[s];
+          uint64_t b[2] = {A.lo & r.lo, A.hi & r.hi};
+          for (int half = 1; half >= 0; --half) {
+            while (b[half]) {
+              const int v = 63 - __clzll(b[half]);
+              b[half] &= ~(1ull << v);
+              const int u = v + 64 * half;
+              const double d = deviation(c, L, cen[u], len[u], ax.len_ratio, ax.pos_ratio);
+              if (d > best) best = d, win = ent[u];
+            }
+          }
+        }
+        if (fs[s].any_active && fs[s].best > best) best = fs[s].best, win = fwin_ent[s];
+        ax.win[p] = win;
+      }
+      store_state(&ax.state[p], st[s]);
+    }
+    const bool wp = __ballot(pending) != 0;
+    if (lane == 0) wpend[w] = wp;
   }
   count_pending(counters, pending);
 }
@@ -281,13 +381,14 @@ __global__ void __launch_bounds__(256) k_sweep_lane(Axis ax, const uint32_t *run
 // 64 lanes split each entry's candidate scan and combine with a wave argmax
 // that keeps the reference's tie rule (earliest in scan order wins).
 __device__ __forceinline__ void consider_ranked(const Axis &ax, Scan &s, uint32_t q, uint32_t p,
-                                                uint64_t c, uint64_t L) {
+                                                const Query &qy) {
   const uint8_t sj = load_state(&ax.state[q]);
   if (sj >= ST_HIT_PENDING) return;
-  const double d = deviation(c, L, ax.cen[q], ax.len[q], ax.len_ratio, ax.pos_ratio);
-  if (!(d > 0)) return;
+  const uint64_t oc = ax.cen[q], oL = ax.len[q];
+  if (!matches(qy, oc, oL)) return;
   if (sj == ST_ACTIVE) {
     s.any_active = true;
+    const double d = deviation(qy.c, qy.L, oc, oL, ax.len_ratio, ax.pos_ratio);
     if (d > s.best || (d == s.best && p < s.pos)) {
       s.best = d;
       s.win = q;
@@ -317,7 +418,7 @@ __device__ __forceinline__ void wave_combine(Scan &s) {
 
 __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big, uint32_t nbig,
                                                     uint8_t *rpend, uint32_t *counters) {
-  // big = starts of the runs of >= WAVE_MIN entries
+  // big = starts of the runs of more than LONG_RUN entries
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nbig;
        w += (gridDim.x * blockDim.x) >> 6) {
@@ -334,10 +435,11 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big
       if (st == ST_ACTIVE || st == ST_HIT) continue;
       const uint64_t c = ax.cen[t], L = ax.len[t];
       const uint32_t i = ax.ent[t];
+      const Query qy = make_query(c, L, ax.len_ratio, ax.pos_ratio);
       Scan s{0.0, NONE, 0xFFFFFFFFu, false, false};
       for (uint32_t q0 = beg; q0 < t; q0 += 64) {  // own run, newest first: rank t-1-q
         const uint32_t q = q0 + lane;
-        if (q < t) consider_ranked(ax, s, q, t - 1 - q, c, L);
+        if (q < t) consider_ranked(ax, s, q, t - 1 - q, qy);
       }
       const int dir = neighbour_dir(c, ax.max_index);
       if ((dir < 0 && has_lo) || (dir > 0 && has_hi)) {
@@ -345,7 +447,7 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big
         const uint32_t own = t - beg;
         for (uint32_t q0 = nb; q0 < ne; q0 += 64) {
           const uint32_t q = q0 + lane;
-          if (q < ne && ax.ent[q] < i) consider_ranked(ax, s, q, own + (ne - 1 - q), c, L);
+          if (q < ne && ax.ent[q] < i) consider_ranked(ax, s, q, own + (ne - 1 - q), qy);
         }
       }
       wave_combine(s);
@@ -363,89 +465,102 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big
   }
 }
 
-__global__ void k_run_flags(Axis ax, uint32_t *flag) {
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < ax.m; p += gridDim.x * blockDim.x)
-    flag[p] = run_start(ax, p);
+// Run bounds of every bucket run, one wavefront per 64 positions: rlen_at at
+// each run start, rbeg_at at each run end, and the starts of the runs longer
+// than LONG_RUN appended to `big` (one atomic per wave).  A run crossing the
+// window is finished by a wave-wide search 64 keys at a time; each wave
+// searches at most once in each direction, so the kernel is O(m).
+__device__ __forceinline__ bool is_start(const Axis &ax, uint32_t p) {
+  return p == 0 || p >= ax.m || ax.key[p] != ax.key[p - 1];
 }
-
-// run r starts at p (rank from the scan); its length key is filled next
-__global__ void k_run_emit(Axis ax, const uint32_t *flag, const uint32_t *rank, uint32_t *beg) {
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < ax.m; p += gridDim.x * blockDim.x)
-    if (flag[p]) beg[rank[p]] = p;
-}
-
-// length CLASS key (1, 2, 3-4, 5-8, ..., 33-47, >= WAVE_MIN): a stable sort by
-// class keeps runs in position order inside a class, so the lanes of a wave
-// walk runs of similar length that also sit close together in memory (a sort
-// by exact length scatters them and every lane drags in its own cache lines).
-// Counts runs shorter than WAVE_MIN (one atomic per block).
-__global__ void __launch_bounds__(256) k_run_len(const uint32_t *beg, uint32_t nruns, uint32_t m,
-                                                 uint32_t *lenkey, uint32_t *nshort) {
-  uint32_t mine = 0;
-  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nruns;
-       r += gridDim.x * blockDim.x) {
-    const uint32_t len = (r + 1 < nruns ? beg[r + 1] : m) - beg[r];
-    lenkey[r] = len >= WAVE_MIN ? 7u : (uint32_t)(32 - __clz((int)(len - 1)));  // ceil(log2)
-    mine += len < WAVE_MIN;
+__global__ void __launch_bounds__(256) k_run_bounds(Axis ax, uint32_t nwin, uint32_t *big,
+                                                    uint32_t *nbig) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (w >= nwin) return;
+  const uint32_t base = w * 64, p = base + lane, m = ax.m;
+  const bool in = p < m;
+  const bool st = in && is_start(ax, p);
+  const bool en = in && is_start(ax, p + 1);  // p + 1 == m counts as a start
+  const uint64_t S = __ballot(st), E = __ballot(en);
+  const uint64_t le = (2ull << lane) - 1ull;  // bits <= lane
+  // the run that started before the window and ends inside it (an end comes
+  // before the window's first start)
+  uint32_t first_beg = base;
+  const int fs = S ? __builtin_ctzll(S) : 64, fe = E ? __builtin_ctzll(E) : 64;
+  if (fe < fs) {  // base > 0 here: position 0 is always a start
+    uint32_t b = base;
+    for (;;) {  // wave-wide backward search
+      const uint32_t q0 = b - 64;
+      const uint64_t s2 = __ballot(is_start(ax, q0 + lane));
+      if (s2) {
+        first_beg = q0 + 63 - __clzll(s2);
+        break;
+      }
+      b = q0;
+    }
   }
-  __shared__ uint32_t part[4];
-  for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mine;
-  __syncthreads();
-  if (threadIdx.x == 0 && part[0] + part[1] + part[2] + part[3])
-    atomicAdd(nshort, part[0] + part[1] + part[2] + part[3]);
-}
-
-// per-position run tables: length at each run start, start at each run end
-__global__ void k_run_tables(Axis ax, const uint32_t *beg, uint32_t nruns, uint32_t *rlen_at,
-                             uint32_t *rbeg_at) {
-  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nruns;
-       r += gridDim.x * blockDim.x) {
-    const uint32_t b = beg[r], e = r + 1 < nruns ? beg[r + 1] : ax.m;
-    rlen_at[b] = e - b;
-    rbeg_at[e - 1] = b;
+  // the run that starts inside the window and ends after it
+  uint32_t last_end = 0;  // exclusive
+  {
+    const int hi_start = S ? 63 - __clzll(S) : 0;
+    const bool open = S && (E >> hi_start) == 0;
+    if (open) {
+      uint32_t b = base + 64;
+      for (;;) {  // wave-wide forward search
+        const uint32_t q = b + lane;
+        const uint64_t e2 = __ballot(q < m && is_start(ax, q + 1));
+        if (e2) {
+          last_end = b + __builtin_ctzll(e2) + 1;
+          break;
+        }
+        b += 64;
+      }
+    }
   }
+  bool isbig = false;
+  if (st) {
+    const uint64_t e_after = E & ~((1ull << lane) - 1ull);
+    const uint32_t end = e_after ? base + __builtin_ctzll(e_after) + 1 : last_end;
+    ax.rlen_at[p] = end - p;
+    isbig = end - p > LONG_RUN;
+  }
+  if (en) {
+    const uint64_t s_before = S & le;
+    ax.rbeg_at[p] = s_before ? base + 63 - __clzll(s_before) : first_beg;
+  }
+  const uint64_t bb = __ballot(isbig);
+  uint32_t at = 0;
+  if (lane == 0 && bb) at = atomicAdd(nbig, (uint32_t)__popcll(bb));
+  at = __shfl(at, 0);
+  if (isbig) big[at + __popcll(bb & ((1ull << lane) - 1ull))] = p;
 }
 
 }  // namespace
 
-size_t runs_scratch_words(uint32_t m) { return 4 * ((size_t)m + 1) + 64; }
+size_t runs_scratch_words(uint32_t m) { return (size_t)m / (LONG_RUN + 1) + 64; }
 
-void build_runs(const Axis &ax, RunList &rl, uint32_t *scratch, uint32_t *radix_k_tmp,
-                uint32_t *radix_v_tmp, uint32_t *radix_scratch, size_t radix_words,
-                ScanScratch ss, uint32_t *dev_words, uint32_t *host_words, hipStream_t st) {
-  rl.nruns = rl.nshort = 0;
+void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host_words,
+                hipStream_t st) {
+  rl.nbig = 0;
+  rl.nwin = (ax.m + 63) / 64;
   if (!ax.m) return;
-  const size_t m1 = (size_t)ax.m + 1;
-  uint32_t *flag = scratch, *rank = scratch + m1, *beg = rank + m1, *lenkey = beg + m1;
-  k_run_flags<<<grid_for(ax.m, 256), 256, 0, st>>>(ax, flag);
-  (void)hipMemsetAsync(flag + ax.m, 0, 4, st);
-  exclusive_scan_u32(flag, rank, m1, ss, st);
-  k_run_emit<<<grid_for(ax.m, 256), 256, 0, st>>>(ax, flag, rank, beg);
-  (void)hipMemcpyAsync(host_words, rank + ax.m, 4, hipMemcpyDeviceToHost, st);
+  (void)hipMemsetAsync(dev_count, 0, 4, st);
+  k_run_bounds<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.nwin, rl.big, dev_count);
+  (void)hipMemsetAsync(rl.wpend, 1, rl.nwin, st);
+  (void)hipMemcpyAsync(host_words, dev_count, 4, hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
-  rl.nruns = host_words[0];
-  (void)hipMemsetAsync(dev_words, 0, 4, st);
-  k_run_len<<<grid_for(rl.nruns, 256, 2048), 256, 0, st>>>(beg, rl.nruns, ax.m, lenkey, dev_words);
-  k_run_tables<<<grid_for(rl.nruns, 256), 256, 0, st>>>(ax, beg, rl.nruns, ax.rlen_at, ax.rbeg_at);
-  // ascending class: short runs first, long runs (class 7) last
-  radix_sort_pairs(lenkey, beg, rl.len, rl.beg, radix_k_tmp, radix_v_tmp, rl.nruns, 3,
-                   radix_scratch, radix_words, st);
-  (void)hipMemcpyAsync(host_words, dev_words, 4, hipMemcpyDeviceToHost, st);
-  (void)hipStreamSynchronize(st);
-  rl.nshort = host_words[0];
+  rl.nbig = host_words[0];
 }
 
 void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
                      hipStream_t st) {
   (void)hipMemsetAsync(counters, 0, PEND_SLOTS * sizeof(uint32_t), st);
-  if (rl.nshort)
-    k_sweep_lane<<<(rl.nshort + 255) / 256, 256, 0, st>>>(ax, rl.beg, rl.nshort, rpend,
-                                                          counters);
-  const uint32_t nbig = rl.nruns - rl.nshort;
-  if (nbig)
-    k_sweep_wave<<<grid_for(nbig, 4, 2048), 256, 0, st>>>(ax, rl.beg + rl.nshort, nbig, rpend,
-                                                          counters);
+  if (rl.nwin)
+    k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
+  if (rl.nbig)
+    k_sweep_wave<<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
+                                                             counters);
 }
 
 }  // namespace rk

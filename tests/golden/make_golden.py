@@ -15,6 +15,9 @@ Outputs
   corpus10k.in.csv.gz / corpus10k.out.csv.gz  cfg1 synthetic set and reference output
   hashes.json                                 SHA-256 of generator input and reference
                                               output for 1M-fragment sets (cfg2, repeat-rich)
+  boundary_hashes.json                        same for tests/boundary_cases.py (deviation
+                                              boundaries, NaN/inf/extreme ratios); only
+                                              this file with --boundary
 """
 from __future__ import annotations
 
@@ -223,5 +226,29 @@ def main():
         shutil.rmtree(tmp)
 
 
+def boundary():
+    sys.path.insert(0, os.path.dirname(HERE))
+    import boundary_cases as bc
+    tmp = tempfile.mkdtemp()
+    try:
+        fr = bc.short_dense(rk)
+        inp = os.path.join(tmp, "in.csv")
+        rk.write_input_csv(inp, fr, bc.GENOME, bc.GENOME)
+        out = {"input_sha256": sha256_file(inp), "outputs": {}}
+        for lr, pr in bc.RATIOS:
+            o = os.path.join(tmp, "out.csv")
+            p = subprocess.run([ro.REF_DRIVER, inp, o, lr, pr], capture_output=True, text=True)
+            assert p.returncode == 0, p.stderr
+            out["outputs"][f"{lr},{pr}"] = sha256_file(o)
+            print(lr, pr, out["outputs"][f"{lr},{pr}"])
+        with open(os.path.join(HERE, "boundary_hashes.json"), "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+    finally:
+        shutil.rmtree(tmp)
+
+
 if __name__ == "__main__":
-    main()
+    if "--boundary" in sys.argv:
+        boundary()
+    else:
+        main()

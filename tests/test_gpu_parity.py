@@ -17,6 +17,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import boundary_cases as bc
 from conftest import EDGE, GOLDEN, ROOT, edge_cases
 from oracle import rk_oracle as ro
 
@@ -87,6 +88,23 @@ def test_cfg1_vs_oracle(gpu_ctx, seed, lr, pr):
 def test_synthetic_vs_oracle(gpu_ctx, n, L, kw):
     f = rk.synth(n, L, seed=21, **kw)
     gpu_vs_oracle(gpu_ctx, f, L, L)
+
+
+with open(os.path.join(GOLDEN, "boundary_hashes.json")) as _f:
+    BOUNDARY = json.load(_f)
+
+
+@pytest.mark.parametrize("lr,pr", bc.RATIOS)
+def test_deviation_boundaries(gpu_ctx, tmp_path, lr, pr):
+    """sl == 0 / sp == 0 boundaries and NaN/inf/extreme ratios: bit-exact with
+    the reference's own output (hash) and with the oracle."""
+    f = bc.short_dense(rk)
+    inp = str(tmp_path / "in.csv")
+    rk.write_input_csv(inp, f, bc.GENOME, bc.GENOME)
+    db = rk.FragmentsDatabase(inp)
+    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, float(lr), float(pr))
+    assert sha256_csv(db, res, str(tmp_path / "out.csv")) == BOUNDARY["outputs"][f"{lr},{pr}"]
+    gpu_vs_oracle(gpu_ctx, f, bc.GENOME, bc.GENOME, float(lr), float(pr))
 
 
 def test_empty_and_tiny(gpu_ctx):

@@ -40,6 +40,27 @@ def test_oracle_corpus10k(tmp_path):
         assert out.read_bytes() == f.read()
 
 
+def test_oracle_boundary_hashes(tmp_path):
+    """The restatement agrees with the reference's own outputs on the deviation
+    boundary set (tests/boundary_cases.py, hashes from make_golden.py --boundary)."""
+    import hashlib
+    import json
+
+    import boundary_cases as bc
+    import repkiller_amd as rk
+    with open(os.path.join(GOLDEN, "boundary_hashes.json")) as f:
+        want = json.load(f)
+    inp = str(tmp_path / "in.csv")
+    rk.write_input_csv(inp, bc.short_dense(rk), bc.GENOME, bc.GENOME)
+    with open(inp, "rb") as f:
+        assert hashlib.sha256(f.read()).hexdigest() == want["input_sha256"]
+    for lr, pr in bc.RATIOS:
+        out = tmp_path / "out.csv"
+        p = subprocess.run([ro.CLI, inp, str(out), lr, pr], capture_output=True, text=True)
+        assert p.returncode == 0, p.stderr
+        assert hashlib.sha256(out.read_bytes()).hexdigest() == want["outputs"][f"{lr},{pr}"], (lr, pr)
+
+
 HARNESS = r"""
 #include <algorithm>
 #include <cstdint>
