@@ -12,9 +12,10 @@ each classifying its OWN independent 50M-fragment set (weak scaling, no data-pat
 collective -- DESIGN.md "Multi-GPU"); a gloo barrier brackets the timed region and
 the max time over ranks is reported.
 
-Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the dominant streaming
-kernel (the stable radix scatter: algorithmic bytes per launch / HIP-event launch
-time measured inside the timed steps; PMC HBM traffic from profiles/traffic.json),
+Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the kernel with the
+most device time per step (algorithmic bytes per launch / HIP-event launch time
+measured inside the timed steps; PMC HBM traffic from profiles/traffic.json),
+`kernels` (the same per kernel),
 `cpu_baseline` (the reference built from its sources, oracle/_ref/ref_driver, on
 a bounded sample, 1 core), `phases_ms` (per-step device time per phase).
 """
@@ -195,20 +196,28 @@ def main():
     if rank != 0:
         return
     per_step = {k: v[0] / max(1, v[1]) for k, v in phases.items()}
-    # roofline of the dominant streaming kernel (the stable radix scatter: 17
-    # launches per step at cfg3), HIP events around each launch on the
-    # library's stream, inside the timed steps
+    # per-kernel HIP-event timing inside the timed steps (on the library's
+    # stream); the roofline is reported for the kernel with the most device
+    # time per step, whatever it is
     kt = ctx.kernel_timing()
-    launch_ms = kt["total_ms"] / max(1, kt["launches"])
-    bytes_per_launch = kt["algo_bytes"] / max(1, kt["launches"])
+    kernels = {}
+    for name, k in kt.items():
+        gbps = k["algo_bytes"] / (k["total_ms"] * 1e-3) / 1e9 if k["total_ms"] and k["algo_bytes"] else None
+        kernels[name] = {"ms_per_step": round(k["total_ms"] / args.steps, 3),
+                         "launches_per_step": round(k["launches"] / args.steps, 2),
+                         "algo_GBps": round(gbps, 1) if gbps else None}
+    dom = max(kt, key=lambda n: kt[n]["total_ms"])
+    d = kt[dom]
+    launch_ms = d["total_ms"] / max(1, d["launches"])
+    bytes_per_launch = d["algo_bytes"] / max(1, d["launches"])
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms else 0.0
-    traffic = load_traffic(kt["kernel"])
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic, "kernel": kt["kernel"],
+                "traffic": load_traffic(dom), "kernel": dom,
                 "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                "launch_ms": round(launch_ms, 4), "launches_per_step": kt["launches"] // args.steps,
-                "kernel_ms_per_step": round(kt["total_ms"] / args.steps, 3)}
+                "launch_ms": round(launch_ms, 4),
+                "launches_per_step": round(d["launches"] / args.steps, 2),
+                "kernel_ms_per_step": round(d["total_ms"] / args.steps, 3)}
     value = frags_total * args.steps / dt_max
     line = {
         "metric": METRIC,
@@ -229,6 +238,7 @@ def main():
         "hbm_algorithmic_GBps": round(50 * value / 1e9, 3),  # 50 B/fragment
         "roofline": roofline,
         "phases_ms": {k: round(v, 3) for k, v in per_step.items()},
+        "kernels": kernels,
         "device_ms_per_step": round(st["device_ms"], 3),
         "groups": n_groups, "grouped_fragments": n_out,
         "sweeps": {"x": st["x_sweeps"], "y": st["y_sweeps"], "jump_rounds": st["jump_rounds"]},

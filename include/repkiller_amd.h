@@ -131,12 +131,15 @@ int rk_set_profiling(rk_ctx *ctx, int enable);
 int rk_get_phase_ms(const rk_ctx *ctx, double *ms /* [RK_N_PHASES] */,
                     uint32_t *calls /* nullable */);
 int rk_reset_phases(rk_ctx *ctx);
-/* Launch-level timing of the dominant streaming kernel (the stable radix
- * scatter, k_digit_scatter) while profiling: summed HIP-event milliseconds,
- * algorithmic bytes (16 B per element: key and value read once and written
- * once) and number of launches since the last rk_reset_phases. */
-int rk_get_kernel_timing(const rk_ctx *ctx, double *total_ms, double *algo_bytes,
+/* Launch-level timing of the pipeline's kernels while profiling: for kernel
+ * index `kernel` (0 .. rk_kernel_count()-1, named by rk_kernel_name), the
+ * summed HIP-event milliseconds of its launches, their summed ALGORITHMIC
+ * bytes (the minimum HBM traffic each launch's job needs) and the
+ * number of launches since the last rk_reset_phases. */
+int rk_get_kernel_timing(const rk_ctx *ctx, int kernel, double *total_ms, double *algo_bytes,
                          uint64_t *launches);
+int rk_kernel_count(void);
+const char *rk_kernel_name(int kernel);
 const char *rk_phase_name(int phase);
 
 /* ---- host ingress: FragmentsDatabase (FragmentsDatabase.cpp:17-101) ---- */

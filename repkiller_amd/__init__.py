@@ -42,7 +42,7 @@ STATUS = {
 EXPORTS = (
     "rk_create", "rk_destroy", "rk_last_error", "rk_classify", "rk_classify_device",
     "rk_get_stats", "rk_std_sort_segments", "rk_set_profiling", "rk_get_phase_ms", "rk_reset_phases", "rk_phase_name",
-    "rk_get_kernel_timing",
+    "rk_get_kernel_timing", "rk_kernel_count", "rk_kernel_name",
     "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
     "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
     "rk_synth_write_csv",
@@ -124,8 +124,10 @@ def load_library() -> ctypes.CDLL:
                                                 vp]),
         "rk_get_phase_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), _u32p]),
         "rk_reset_phases": (ctypes.c_int, [vp]),
-        "rk_get_kernel_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+        "rk_get_kernel_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_double), _u64p]),
+        "rk_kernel_count": (ctypes.c_int, []),
+        "rk_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
         "rk_phase_name": (ctypes.c_char_p, [ctypes.c_int]),
         "rk_db_load_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(vp)]),
         "rk_db_free": (None, [vp]),
@@ -342,12 +344,18 @@ class Context:
         return perm
 
     def kernel_timing(self) -> dict:
-        """HIP-event timing of the radix scatter launches while profiling."""
-        ms, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
-        _check(load_library().rk_get_kernel_timing(self._h, ctypes.byref(ms), ctypes.byref(by),
-                                                   ctypes.byref(n)))
-        return {"kernel": "k_digit_scatter", "total_ms": ms.value, "algo_bytes": by.value,
-                "launches": n.value}
+        """Per-kernel HIP-event timing while profiling:
+        {name: {"total_ms", "algo_bytes", "launches"}} for kernels that ran."""
+        lib = load_library()
+        out = {}
+        for k in range(lib.rk_kernel_count()):
+            ms, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+            _check(lib.rk_get_kernel_timing(self._h, k, ctypes.byref(ms), ctypes.byref(by),
+                                            ctypes.byref(n)))
+            if n.value:
+                out[lib.rk_kernel_name(k).decode()] = {"total_ms": ms.value, "algo_bytes": by.value,
+                                                       "launches": n.value}
+        return out
 
     def classify(self, f: Frags, len_x_hdr: int, len_y_hdr: int, len_ratio: float = 0.3,
                  pos_ratio: float = 0.3) -> ClassifyResult:

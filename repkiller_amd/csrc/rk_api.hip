@@ -43,10 +43,20 @@ struct rk_ctx {
   bool pev_used[RK_N_PHASES + 1] = {};
   double phase_ms[RK_N_PHASES] = {};
   uint32_t phase_calls[RK_N_PHASES] = {};
-  rk::KernelTimer kt{};   // radix scatter launches of the current call
-  double kt_ms = 0, kt_bytes = 0;
-  uint64_t kt_launches = 0;
+  rk::KernelTimer kt{};   // timed launches of the current call
+  double kt_ms[rk::KID_COUNT] = {}, kt_bytes[rk::KID_COUNT] = {};
+  uint64_t kt_launches[rk::KID_COUNT] = {};
 };
+
+namespace rk {
+const char *const kKernelNames[KID_COUNT] = {
+    "k_prep_keys",     "k_digit_hist",      "k_digit_scatter", "k_gather_proc",
+    "k_sort_keys",     "k_csr_fill_x",      "k_run_bounds",    "k_sweep_tile",
+    "k_sweep_wave",    "k_x_results",       "k_csr_fill_y",    "k_y_parents",
+    "k_jump",          "k_assign_gid",      "k_group_offsets", "k_build_records",
+    "k_sort_small",    "k_sort_groups_lds", "k_sort_groups_global", "k_emit",
+};
+}  // namespace rk
 
 static const char *kPhaseNames[RK_N_PHASES] = {
     "prep_keys",      "order_csr",  "gather_proc", "occupancy_csr", "sweep_x", "sweep_y",
@@ -186,9 +196,10 @@ void collect_phases(rk_ctx *ctx) {
   for (int i = 0; i < ctx->kt.n; ++i) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, ctx->kt.ev[2 * i], ctx->kt.ev[2 * i + 1]) == hipSuccess) {
-      ctx->kt_ms += ms;
-      ctx->kt_bytes += 16.0 * (double)ctx->kt.elems[i];  // key+value read once, written once
-      ctx->kt_launches++;
+      const int k = ctx->kt.kid[i];
+      ctx->kt_ms[k] += ms;
+      ctx->kt_bytes[k] += ctx->kt.bytes[i];
+      ctx->kt_launches[k]++;
     }
   }
   ctx->kt.n = 0;
@@ -247,7 +258,7 @@ int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss,
       ctx->err = "occupancy sweeps did not converge";
       return RK_E_INTERNAL;
     }
-    rk::occupancy_sweep(ax, rl, rpend, counters, ctx->stream);
+    rk::occupancy_sweep(ax, rl, rpend, counters, *sweeps == 0, ctx->stream);
     HIPCHK(ctx, hipGetLastError());
     ++*sweeps;
     int rc = readback(ctx, counters, rk::PEND_WORDS);
@@ -459,19 +470,25 @@ extern "C" int rk_get_phase_ms(const rk_ctx *ctx, double *ms, uint32_t *calls) {
   return RK_OK;
 }
 
-extern "C" int rk_get_kernel_timing(const rk_ctx *ctx, double *total_ms, double *algo_bytes,
-                                    uint64_t *launches) {
-  if (!ctx) return RK_E_ARG;
-  if (total_ms) *total_ms = ctx->kt_ms;
-  if (algo_bytes) *algo_bytes = ctx->kt_bytes;
-  if (launches) *launches = ctx->kt_launches;
+extern "C" int rk_get_kernel_timing(const rk_ctx *ctx, int kernel, double *total_ms,
+                                    double *algo_bytes, uint64_t *launches) {
+  if (!ctx || kernel < 0 || kernel >= rk::KID_COUNT) return RK_E_ARG;
+  if (total_ms) *total_ms = ctx->kt_ms[kernel];
+  if (algo_bytes) *algo_bytes = ctx->kt_bytes[kernel];
+  if (launches) *launches = ctx->kt_launches[kernel];
   return RK_OK;
+}
+
+extern "C" int rk_kernel_count(void) { return rk::KID_COUNT; }
+
+extern "C" const char *rk_kernel_name(int kernel) {
+  return kernel >= 0 && kernel < rk::KID_COUNT ? rk::kKernelNames[kernel] : "";
 }
 
 extern "C" int rk_reset_phases(rk_ctx *ctx) {
   if (!ctx) return RK_E_ARG;
-  ctx->kt_ms = ctx->kt_bytes = 0;
-  ctx->kt_launches = 0;
+  for (int k = 0; k < rk::KID_COUNT; ++k)
+    ctx->kt_ms[k] = ctx->kt_bytes[k] = 0, ctx->kt_launches[k] = 0;
   for (int i = 0; i < RK_N_PHASES; ++i) ctx->phase_ms[i] = 0, ctx->phase_calls[i] = 0;
   return RK_OK;
 }
@@ -497,7 +514,7 @@ extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const
     ctx->err = "unexpected C++ exception";
     rc = RK_E_INTERNAL;
   }
-  rk::g_ktimer = nullptr;  // never leave the radix timer pointing at this context
+  rk::g_ktimer = nullptr;  // never leave the kernel timer pointing at this context
   return rc;
 }
 

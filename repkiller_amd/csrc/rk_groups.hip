@@ -213,49 +213,82 @@ __global__ void k_emit(const uint32_t *tag, const uint32_t *gid_proc, const uint
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
                ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st) {
   if (f.n)
+  {
+    kt_begin(st);
     k_prep_keys<<<grid_for(f.n, 256, 2048), 256, 0, st>>>(f, vsize, max_x, max_y, pkey, rec, kept,
                                                            err);
+    kt_end(st, KID_PREP, 61.0 * f.n);  // x, y, len, strand in; key + 32-B record out
+  }
 }
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st) {
   if (!m) return;
   (void)f;
+  kt_begin(st);
   k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(p, m, nbx, nby);
+  kt_end(st, KID_GATHER, 84.0 * m);  // row + record in; ys, xrec, yrec, keyx, keyy out
+  kt_begin(st);
   k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m);
+  kt_end(st, KID_SORT_KEYS, 20.0 * m);  // key + yStart in, sort key out
 }
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, hipStream_t st) {
-  if (m) k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m);
+  if (!m) return;
+  kt_begin(st);
+  k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m);
+  kt_end(st, KID_CSR_FILL_X, 37.0 * m);  // id + record in; centre, length, state out
 }
 void x_results(Csr c, uint32_t *xres_proc, uint32_t m, uint32_t *err, hipStream_t st) {
-  if (m) k_x_results<<<grid_for(m, 256), 256, 0, st>>>(c, xres_proc, m, err);
+  if (!m) return;
+  kt_begin(st);
+  k_x_results<<<grid_for(m, 256), 256, 0, st>>>(c, xres_proc, m, err);
+  kt_end(st, KID_X_RESULTS, 13.0 * m);  // state, winner, id in; result out
 }
 void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *xres_proc, uint32_t *xres,
                 uint32_t m, hipStream_t st) {
-  if (m) k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, xres_proc, xres, m);
+  if (!m) return;
+  kt_begin(st);
+  k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, xres_proc, xres, m);
+  kt_end(st, KID_CSR_FILL_Y, 45.0 * m);  // id, record, X result in; centre, length, state, X result out
 }
 void y_parents(Csr c, const uint32_t *xres, uint32_t *par, uint32_t m, uint32_t *err,
                hipStream_t st) {
-  if (m) k_y_parents<<<grid_for(m, 256), 256, 0, st>>>(c, xres, par, m, err);
+  if (!m) return;
+  kt_begin(st);
+  k_y_parents<<<grid_for(m, 256), 256, 0, st>>>(c, xres, par, m, err);
+  kt_end(st, KID_Y_PARENTS, 17.0 * m);  // id, X result, state, winner in; parent out
 }
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st) {
+  kt_begin(st);
   k_group_offsets<<<grid_for(m, 256), 256, 0, st>>>(sgid, m, ngroups, goff);
+  kt_end(st, KID_GROUP_OFFSETS, 4.0 * m + 4.0 * ngroups);
 }
 void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, hipStream_t st) {
-  if (m) k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed, isnew);
+  if (!m) return;
+  kt_begin(st);
+  k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed, isnew);
+  kt_end(st, KID_JUMP, (isnew ? 12.0 : 8.0) * m);  // parent, grandparent (+ new flag)
 }
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {
-  if (m) k_assign_gid<<<grid_for(m, 256), 256, 0, st>>>(p, m, newrank);
+  if (!m) return;
+  kt_begin(st);
+  k_assign_gid<<<grid_for(m, 256), 256, 0, st>>>(p, m, newrank);
+  kt_end(st, KID_ASSIGN_GID, 12.0 * m);  // root, root's rank in; gid out
 }
 void build_records(const uint32_t *gmem, const uint64_t *ha, uint32_t m, uint64_t *key,
                    uint32_t *tag, hipStream_t st) {
-  if (m) k_build_records<<<grid_for(m, 256), 256, 0, st>>>(gmem, ha, m, key, tag);
+  if (!m) return;
+  kt_begin(st);
+  k_build_records<<<grid_for(m, 256), 256, 0, st>>>(gmem, ha, m, key, tag);
+  kt_end(st, KID_BUILD_RECORDS, 24.0 * m);  // member, sort key in; (key, tag) out
 }
 void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
                  const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st) {
-  if (m)
-    k_emit<<<grid_for(m, 256), 256, 0, st>>>(tag, gid_proc, goff, row, m, out_gid, out_rep,
-                                             out_order);
+  if (!m) return;
+  kt_begin(st);
+  k_emit<<<grid_for(m, 256), 256, 0, st>>>(tag, gid_proc, goff, row, m, out_gid, out_rep,
+                                           out_order);
+  kt_end(st, KID_EMIT, 29.0 * m);  // tag, gid, group bounds, row in; gid, flag, order out
 }
 
 }  // namespace rk

@@ -355,14 +355,33 @@ __global__ void k_sort_small(const uint32_t *gid_sorted, const uint32_t *goff, u
 }
 
 // flags for the tier lists: 1 = LDS tier, 2 = global tier
-__global__ void k_tier_flags(const uint32_t *goff, uint32_t ngroups, uint32_t cap, uint32_t cap2,
-                             uint32_t *f1, uint32_t *f2, uint32_t *f3) {
+// (members per tier -> tcount[0..3] for the timing accounts; one atomic per
+// block and tier, grid <= 1024 blocks)
+__global__ void __launch_bounds__(256) k_tier_flags(const uint32_t *goff, uint32_t ngroups,
+                                                    uint32_t cap, uint32_t cap2, uint32_t *f1,
+                                                    uint32_t *f2, uint32_t *f3, uint32_t *tcount) {
+  uint32_t c[4] = {0, 0, 0, 0};
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
        g += gridDim.x * blockDim.x) {
     const uint32_t n = goff[g + 1] - goff[g];
-    f1[g] = n > (uint32_t)THRESH && n <= cap;
-    f2[g] = n > cap && n <= cap2;
-    f3[g] = n > cap2;
+    const int t = n <= (uint32_t)THRESH ? 0 : n <= cap ? 1 : n <= cap2 ? 2 : 3;
+    f1[g] = t == 1;
+    f2[g] = t == 2;
+    f3[g] = t == 3;
+    c[t] += n;
+  }
+  __shared__ uint32_t part[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    uint32_t v = c[t];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) part[t][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const uint32_t v = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] +
+                       part[threadIdx.x][3];
+    if (v) atomicAdd(&tcount[threadIdx.x], v);
   }
 }
 
@@ -384,7 +403,7 @@ constexpr uint32_t LDS_CAP2 = 2048;  // up to this size: large LDS tier (3 waves
 size_t groupsort_scratch_bytes(uint32_t n) {
   const size_t g1 = (size_t)n + 1;
   const size_t frames = (size_t)n / 8 + 80 * ((size_t)n / (LDS_CAP2 + 1) + 1) + 80;
-  return (size_t)n * 4 * 2 + g1 * 4 * 9 + (size_t)n + 64 + frames * sizeof(Frame) + 256;
+  return (size_t)n * 4 * 2 + g1 * 4 * 9 + (size_t)n + 64 + 64 + frames * sizeof(Frame) + 256;
 }
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
@@ -397,11 +416,17 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   uint32_t *f1 = pr + m, *f2 = f1 + g1, *f3 = f2 + g1, *p1 = f3 + g1, *p2 = p1 + g1,
            *p3 = p2 + g1, *l1 = p3 + g1, *l2 = l1 + g1, *l3 = l2 + g1;
   uint8_t *bnd = reinterpret_cast<uint8_t *>(l3 + g1);
-  Frame *frames = reinterpret_cast<Frame *>(
+  uint32_t *tcount = reinterpret_cast<uint32_t *>(
       (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
+  Frame *frames = reinterpret_cast<Frame *>(tcount + 16);
+  uint32_t *members = host_words + 4;  // device counters live after the tier flags
+  kt_begin(st);
   k_sort_small<<<grid_for(m, 256), 256, 0, st>>>(gid_sorted, goff, m, key, tag, otag);
-  k_tier_flags<<<grid_for(ngroups, 256), 256, 0, st>>>(goff, ngroups, LDS_CAP, LDS_CAP2, f1, f2,
-                                                       f3);
+  kt_end(st, KID_SORT_SMALL, 0.0);  // bytes filled in below from the tier sizes
+  const int small_slot = g_ktimer ? g_ktimer->n - 1 : -1;
+  (void)hipMemsetAsync(tcount, 0, 4 * sizeof(uint32_t), st);
+  k_tier_flags<<<grid_for(ngroups, 256, 1024), 256, 0, st>>>(goff, ngroups, LDS_CAP, LDS_CAP2, f1,
+                                                             f2, f3, tcount);
   uint32_t *fl[3] = {f1, f2, f3}, *ps[3] = {p1, p2, p3}, *ls[3] = {l1, l2, l3};
   for (int t = 0; t < 3; ++t) {
     (void)hipMemsetAsync(fl[t] + ngroups, 0, 4, st);
@@ -409,17 +434,30 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     k_compact<<<grid_for(ngroups, 256), 256, 0, st>>>(fl[t], ps[t], ngroups, ls[t]);
     (void)hipMemcpyAsync(host_words + t, ps[t] + ngroups, 4, hipMemcpyDeviceToHost, st);
   }
+  (void)hipMemcpyAsync(members, tcount, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
   const uint32_t n1 = host_words[0], n2 = host_words[1], n3 = host_words[2];
-  if (n1)
+  // algorithmic bytes of every tier: each member's (key, tag) read, its tag
+  // written once at its final slot
+  if (small_slot >= 0) g_ktimer->bytes[small_slot] = 16.0 * members[0];
+  if (n1) {
+    kt_begin(st);
     k_sort_groups_lds<<<n1 < 16384 ? n1 : 16384, 64, lds_bytes(LDS_CAP), st>>>(
         l1, n1, goff, key, tag, otag, LDS_CAP);
-  if (n2)
+    kt_end(st, KID_SORT_LDS, 16.0 * members[1]);
+  }
+  if (n2) {
+    kt_begin(st);
     k_sort_groups_lds<<<n2 < 2048 ? n2 : 2048, 64, lds_bytes(LDS_CAP2), st>>>(
         l2, n2, goff, key, tag, otag, LDS_CAP2);
-  if (n3)
+    kt_end(st, KID_SORT_LDS, 16.0 * members[2]);
+  }
+  if (n3) {
+    kt_begin(st);
     k_sort_groups_global<<<n3 < 1024 ? n3 : 1024, 64, 0, st>>>(l3, n3, goff, key, tag, otag, pl,
                                                                pr, bnd, frames);
+    kt_end(st, KID_SORT_GLOBAL, 16.0 * members[3]);
+  }
 }
 
 }  // namespace rk

@@ -44,16 +44,40 @@ size_t scan_blocks(size_t n);
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
                         hipStream_t st);
 
-// Launch-level HIP-event timer for the radix scatter kernel (the pipeline's
-// dominant streaming kernel), active only while a context profiles
-// (rk_set_profiling); set per thread by rk_classify_device.
+// Launch-level HIP-event timing of the pipeline's kernels, active only while a
+// context profiles (rk_set_profiling): rk_classify_device points g_ktimer at
+// its context's timer for the duration of the call.  Every timed launch is
+// bracketed by kt_begin / kt_end on the launch stream and carries the
+// ALGORITHMIC bytes of that launch (the minimum HBM traffic its job needs,
+// DESIGN.md "Kernels and their rooflines").
+enum KernelId : int {
+  KID_PREP, KID_HIST, KID_SCATTER, KID_GATHER, KID_SORT_KEYS, KID_CSR_FILL_X, KID_RUN_BOUNDS,
+  KID_SWEEP_TILE, KID_SWEEP_WAVE, KID_X_RESULTS, KID_CSR_FILL_Y, KID_Y_PARENTS, KID_JUMP,
+  KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_LDS,
+  KID_SORT_GLOBAL, KID_EMIT, KID_COUNT
+};
+extern const char *const kKernelNames[KID_COUNT];
 struct KernelTimer {
-  static constexpr int MAX = 96;
+  static constexpr int MAX = 256;
   hipEvent_t ev[2 * MAX];
-  uint64_t elems[MAX];
+  int kid[MAX];
+  double bytes[MAX];
   int n;
 };
 extern thread_local KernelTimer *g_ktimer;
+inline void kt_begin(hipStream_t st) {
+  KernelTimer *t = g_ktimer;
+  if (t && t->n < KernelTimer::MAX) (void)hipEventRecord(t->ev[2 * t->n], st);
+}
+inline void kt_end(hipStream_t st, int kid, double bytes) {
+  KernelTimer *t = g_ktimer;
+  if (t && t->n < KernelTimer::MAX) {
+    (void)hipEventRecord(t->ev[2 * t->n + 1], st);
+    t->kid[t->n] = kid;
+    t->bytes[t->n] = bytes;
+    t->n++;
+  }
+}
 
 // ----------------------------------------------------------- rk_radix.hip --
 size_t radix_scratch_words(uint32_t n);
@@ -93,7 +117,7 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
 // sum is the number of waves/runs still pending after the sweep.
 constexpr uint32_t PEND_WORDS = 64;
 void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
-                     hipStream_t st);
+                     bool first, hipStream_t st);
 
 // ---------------------------------------------------------- rk_groups.hip --
 struct Frags {  // file-order inputs

@@ -546,7 +546,9 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
   rl.nwin = (ax.m + 63) / 64;
   if (!ax.m) return;
   (void)hipMemsetAsync(dev_count, 0, 4, st);
+  kt_begin(st);
   k_run_bounds<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.nwin, rl.big, dev_count);
+  kt_end(st, KID_RUN_BOUNDS, 4.0 * ax.m);  // keys read once (boundary writes not counted)
   (void)hipMemsetAsync(rl.wpend, 1, rl.nwin, st);
   (void)hipMemcpyAsync(host_words, dev_count, 4, hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
@@ -554,13 +556,22 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
 }
 
 void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
-                     hipStream_t st) {
+                     bool first, hipStream_t st) {
   (void)hipMemsetAsync(counters, 0, PEND_SLOTS * sizeof(uint32_t), st);
-  if (rl.nwin)
+  // algorithmic bytes: the first sweep reads every entry's key, centre, length,
+  // id and state and writes state (+ winner): 30 B; later sweeps only need the
+  // window flags (their real work is what the first one left open)
+  if (rl.nwin) {
+    kt_begin(st);
     k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
-  if (rl.nbig)
+    kt_end(st, KID_SWEEP_TILE, first ? 30.0 * ax.m : (double)rl.nwin);
+  }
+  if (rl.nbig) {
+    kt_begin(st);
     k_sweep_wave<<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
                                                              counters);
+    kt_end(st, KID_SWEEP_WAVE, 0.0);
+  }
 }
 
 }  // namespace rk

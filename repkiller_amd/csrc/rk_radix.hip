@@ -173,16 +173,13 @@ constexpr uint32_t RTILE = RT * RITEMS;
 template <int T, int I>
 void launch_pass(const uint32_t *ki, const uint32_t *vi, uint32_t n, int shift, uint32_t tiles,
                  uint32_t *counts, ScanScratch ss, uint32_t *ko, uint32_t *vo, hipStream_t st) {
+  kt_begin(st);
   k_digit_hist<T, I><<<tiles, T, 0, st>>>(ki, n, shift, tiles, counts);
+  kt_end(st, KID_HIST, 4.0 * n);  // keys read once
   exclusive_scan_u32(counts, counts, (size_t)tiles * RADIX, ss, st);
-  KernelTimer *kt = g_ktimer;
-  const bool timed = kt && kt->n < KernelTimer::MAX;
-  if (timed) (void)hipEventRecord(kt->ev[2 * kt->n], st);
+  kt_begin(st);
   k_digit_scatter<T, I><<<tiles, T, 0, st>>>(ki, vi, n, shift, tiles, counts, ko, vo);
-  if (timed) {
-    (void)hipEventRecord(kt->ev[2 * kt->n + 1], st);
-    kt->elems[kt->n++] = n;
-  }
+  kt_end(st, KID_SCATTER, (vi ? 16.0 : 12.0) * n);  // key (+value) read, key+value written
 }
 
 }  // namespace
