@@ -85,6 +85,16 @@ def allsum(world, v: float) -> float:
     return float(t.item())
 
 
+def rank_seed(rank: int) -> int:
+    """Each rank classifies its own independent fragment set (weak scaling)."""
+    return 3 + rank
+
+
+def aggregate(world: int, n_local: int, dt_local: float) -> tuple[float, float]:
+    """Whole-job fragments and the slowest rank's time (the contract's max over ranks)."""
+    return allsum(world, float(n_local)), allmax(world, dt_local)
+
+
 def cpu_baseline(cfg: dict, seconds_hint: float) -> dict | None:
     """The reference (oracle/_ref/ref_driver, built from /root/reference/src by
     oracle/ref.mk) on a bounded sample of the same workload: the cfg3 density
@@ -150,7 +160,7 @@ def main():
     torch.cuda.set_device(dev)
     ctx = rk.Context(local)
 
-    f = rk.synth(n, L, seed=3 + rank)  # independent fragment set per rank
+    f = rk.synth(n, L, seed=rank_seed(rank))  # independent fragment set per rank
     x = torch.from_numpy(f.x_start.view(np.int64)).to(dev)
     y = torch.from_numpy(f.y_start.view(np.int64)).to(dev)
     ln = torch.from_numpy(f.length.view(np.int64)).to(dev)
@@ -178,8 +188,7 @@ def main():
     barrier(world)
     dt = time.perf_counter() - t0
     ctx.set_profiling(False)
-    dt_max = allmax(world, dt)
-    frags_total = allsum(world, float(n))
+    frags_total, dt_max = aggregate(world, n, dt)
     phases = ctx.phases()
     st = ctx.stats()
 

@@ -1,0 +1,62 @@
+"""World-size-2 gloo run of bench.py's multi-rank plumbing on CPU.
+
+bench.py --gpus N runs one process per GPU, each classifying its own
+independent fragment set: the only cross-rank traffic is
+the barrier around the timed region and the reductions of fragment counts
+(sum) and times (max).  This covers that path without a GPU.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    import repkiller_amd as rk
+    r, w, local = bench.dist_setup()
+    assert (r, w, local) == (rank, world, rank)
+    f = rk.synth(1000, 100_000, seed=bench.rank_seed(r))
+    bench.barrier(w)
+    total, dt = bench.aggregate(w, f.n + r, 0.5 + r)  # ranks differ in size and time
+    q.put((r, total, dt, int(f.x_start[:16].sum())))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_two_rank_aggregation():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    # every rank sees the whole-job count (1000 + 1001) and the slowest time
+    assert [r[1] for r in res] == [2001.0, 2001.0]
+    assert [r[2] for r in res] == [1.5, 1.5]
+    # independent fragment sets per rank
+    assert res[0][3] != res[1][3]
+
+
+def test_single_rank_is_local():
+    import bench
+    assert bench.aggregate(1, 7, 0.25) == (7.0, 0.25)
+    assert bench.rank_seed(0) != bench.rank_seed(1)
