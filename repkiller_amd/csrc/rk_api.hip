@@ -244,11 +244,11 @@ int err_status(rk_ctx *ctx, uint32_t bits) {
 }
 
 // run sweeps on one axis until no bucket has undecided entries
-int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss,
+int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss, bool fast32,
                  uint32_t *sweeps) {
   uint32_t *counters = w.ctrl + 64;
   uint8_t *rpend = reinterpret_cast<uint8_t *>(w.rpend);
-  rk::RunList rl{w.runs, w.wpend, 0, 0};
+  rk::RunList rl{w.runs, w.wpend, 0, 0, fast32};
   rk::build_runs(ax, rl, w.ctrl + 2, ctx->host + 128, ctx->stream);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));
@@ -317,6 +317,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   HIPCHK(ctx, hipGetLastError());
   if ((rc = readback(ctx, w.ctrl, 2))) return rc;
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
+  const bool fast32 = !(ctx->host[0] & rk::ERRB_WIDE_LENGTH);
   const uint32_t m = ctx->host[1];
   ctx->stats.n_proc = m;
   out->n_out = m;
@@ -346,13 +347,13 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   mark(ctx, RK_PH_SWEEP_X);
   rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, w.rlen_at,
               w.rbeg_at, m, pl.max_x, prm->len_ratio, prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ax, w, ss, &ctx->stats.x_sweeps))) return rc;
+  if ((rc = resolve_axis(ctx, ax, w, ss, fast32, &ctx->stats.x_sweeps))) return rc;
   rk::x_results(w.cx, w.p.xres, m, w.ctrl, st);
   mark(ctx, RK_PH_SWEEP_Y);
   rk::csr_fill_y(w.cy, w.p.yrec, w.p.xres, w.xres, m, st);
   rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.rlen_at,
               w.rbeg_at, m, pl.max_y, prm->len_ratio, prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ay, w, ss, &ctx->stats.y_sweeps))) return rc;
+  if ((rc = resolve_axis(ctx, ay, w, ss, fast32, &ctx->stats.y_sweeps))) return rc;
 
   // 6: group roots and ids
   mark(ctx, RK_PH_ROOTS);

@@ -38,8 +38,10 @@ __device__ __forceinline__ uint64_t probe_max_bucket(uint64_t c, uint64_t max_in
 __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t max_y,
                             uint32_t *pkey, ulonglong2 *rec, uint32_t *kept, uint32_t *err) {
   uint32_t mine = 0;
+  bool wide = false;  // a length >= 2^31 (disables the 32-bit sweep)
   GRID_STRIDE(i, f.n) {
     const uint64_t x = f.x[i];
+    wide |= f.len[i] >= 0x80000000ull;
     const uint64_t pk = x / 10;
     // pack the row once, coalesced, so the processing-order gather is one
     // 32-B read per row instead of four scattered reads
@@ -66,6 +68,7 @@ __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t ma
     const uint32_t t = part[0] + part[1] + part[2] + part[3];
     if (t) atomicAdd(kept, t);
   }
+  if ((threadIdx.x & 63) == 0 && __ballot(wide)) atomicOr(err, ERRB_WIDE_LENGTH);
 }
 
 // Processing-order SoA and bucket keys (one 32-B record gather per row).

@@ -22,6 +22,7 @@ enum : uint32_t {
   ERRB_UB_BUCKET = 1u,
   ERRB_UB_CENTER = 2u,
   ERRB_INTERNAL = 4u,
+  ERRB_WIDE_LENGTH = 8u,  // not an error: some length >= 2^31 (generic sweep kernel)
 };
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -108,6 +109,7 @@ struct RunList {
   uint32_t *big;
   uint8_t *wpend;
   uint32_t nbig, nwin;
+  bool fast32;  // every length < 2^31: the 32-bit window kernel applies
 };
 size_t runs_scratch_words(uint32_t m);
 void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host_words,

@@ -376,6 +376,227 @@ __global__ void __launch_bounds__(256) k_sweep_tile(Axis ax, uint8_t *wpend, uin
   count_pending(counters, pending);
 }
 
+// 64 bits of a 128-bit window mask starting at bit a (0 <= a < 128)
+__device__ __forceinline__ uint64_t bits_from(uint64_t lo, uint64_t hi, int a) {
+  if (a >= 64) return hi >> (a - 64);
+  return a ? (lo >> a) | (hi << (64 - a)) : lo;
+}
+
+// ---- 32-bit fast path of the window sweep --------------------------------
+// When every length is below 2^31 (checked once per call in k_prep_keys), the
+// length difference of two entries fits 31 bits and the centre difference of
+// two entries in the same or adjacent 100-bp buckets is below 200, so the
+// candidate test and the deviation run on 32-bit operands (the values, and
+// therefore every f64 result, are identical).  Thresholds saturate at 2^32-1,
+// which no 31-bit difference reaches.
+struct Q32 {
+  uint32_t c, L, tl, tc;
+  bool ok, eq;
+};
+__device__ __forceinline__ Q32 make_q32(uint64_t c, uint32_t L, double lr, double pr) {
+  Q32 q;
+  const double bl = (double)L * lr, bc = (double)L * pr;
+  q.c = (uint32_t)c;
+  q.L = L;
+  q.ok = L != 0 && bl == bl && bc == bc;
+  q.tl = bl >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)bl;
+  q.tc = bc >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)bc;
+  q.eq = (double)q.tl == bl && (double)q.tc == bc;
+  return q;
+}
+__device__ __forceinline__ void diffs32(const Q32 &q, uint2 o, uint32_t &dl, uint32_t &dc) {
+  dl = q.L > o.y ? q.L - o.y : o.y - q.L;
+  const int32_t d = (int32_t)(q.c - o.x);
+  dc = (uint32_t)(d < 0 ? -d : d);
+}
+__device__ __forceinline__ bool m32(const Q32 &q, uint2 o) {
+  uint32_t dl, dc;
+  diffs32(q, o, dl, dc);
+  return q.ok && dl <= q.tl && dc <= q.tc && !(q.eq && dl == q.tl && dc == q.tc);
+}
+// deviation (SequenceOcupationList.cpp:20-31) from the same integer operands
+__device__ __forceinline__ double dev32(const Q32 &q, uint2 o, double lr, double pr) {
+  uint32_t dl, dc;
+  diffs32(q, o, dl, dc);
+  const double sl = -fabs((double)dl / ((double)q.L * lr)) + 1.0;
+  if (sl < 0) return 0.0;
+  const double sp = -fabs((double)dc / ((double)q.L * pr)) + 1.0;
+  if (sp < 0) return 0.0;
+  return sl * 0.4 + sp * 0.6;
+}
+
+__global__ void __launch_bounds__(256) k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin,
+                                                    uint32_t *counters) {
+  __shared__ uint2 s_pk[4][128];  // {centre low 32 bits, length}
+  __shared__ uint32_t s_ent[4][128], s_key[4][128];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.x * 4 + wv;
+  bool pending = false;
+  if (w < nwin && wpend[w]) {
+    uint2 *pk = s_pk[wv];
+    uint32_t *ent = s_ent[wv], *key = s_key[wv];
+    const uint32_t base = w * 64, m = ax.m;
+    uint64_t S0, S1;
+    {
+      const uint32_t p0 = base + lane, p1 = base + 64 + lane;
+      const uint32_t k0 = p0 < m ? ax.key[p0] : NONE, k1 = p1 < m ? ax.key[p1] : NONE;
+      const uint32_t q0 = p0 < m && p0 > 0 ? ax.key[p0 - 1] : NONE;
+      const uint32_t q1 = p1 < m ? ax.key[p1 - 1] : NONE;
+      key[lane] = k0;
+      key[64 + lane] = k1;
+      S0 = __ballot(p0 >= m || p0 == 0 || q0 != k0);
+      S1 = __ballot(p1 >= m || q1 != k1);
+    }
+    bool own[2];
+    int rs[2];
+    uint8_t st[2], st0[2];
+    uint64_t cfull[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int P = 64 * s + lane;
+      rs[s] = hs_le(S0, S1, P);
+      const int re = ls_gt(S0, S1, P);
+      own[s] = base + P < m && rs[s] >= 0 && rs[s] < 64 && re - rs[s] <= (int)LONG_RUN;
+      st[s] = ST_HIT;
+      cfull[s] = 0;
+      if (own[s]) {
+        const uint32_t p = base + P;
+        cfull[s] = ax.cen[p];
+        pk[P] = make_uint2((uint32_t)cfull[s], (uint32_t)ax.len[p]);
+        ent[P] = ax.ent[p];
+        st[s] = ax.state[p];
+      }
+      st0[s] = st[s];
+    }
+    wave_sync_lds();
+    // matching candidates: own run (bit j = entry rs + j), owned neighbour run
+    // (bit j = entry nbs + j); a foreign neighbour run is summarised in fs
+    uint64_t rown[2], rnb[2];
+    int nbs[2];
+    Scan fs[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      rown[s] = rnb[s] = 0;
+      nbs[s] = 0;
+      fs[s] = Scan{0.0, NONE, 0, false, false};
+      if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
+      const int P = 64 * s + lane;
+      const uint2 me = pk[P];
+      const Q32 q = make_q32(cfull[s], me.y, ax.len_ratio, ax.pos_ratio);
+      const int n = P - rs[s];
+      for (int j = 0; j < n; ++j) rown[s] |= (uint64_t)m32(q, pk[rs[s] + j]) << j;
+      const int dir = neighbour_dir(cfull[s], ax.max_index);
+      if (!dir) continue;
+      const uint32_t i = ent[P], k = key[P];
+      uint32_t gb = 0, ge = 0;
+      bool foreign = false;
+      int nb = -1, ne = -1;
+      if (dir < 0) {
+        const int q2 = rs[s] - 1;
+        if (q2 >= 0) {
+          if (key[q2] == k - 1) {
+            const int b2 = hs_le(S0, S1, q2);
+            if (b2 >= 0) nb = b2, ne = rs[s];
+            else foreign = true, ge = base + rs[s], gb = ax.rbeg_at[ge - 1];
+          }
+        } else if (base > 0 && ax.key[base - 1] == k - 1) {
+          foreign = true, ge = base, gb = ax.rbeg_at[base - 1];
+        }
+      } else {
+        const int q2 = ls_gt(S0, S1, P);
+        const uint32_t gq = base + q2;
+        if (gq < m) {
+          const uint32_t kq = q2 < 128 ? key[q2] : ax.key[gq];
+          if (kq == k + 1) {
+            const int e2 = q2 < 127 ? ls_gt(S0, S1, q2) : 128;
+            if (q2 < 64 && e2 - q2 <= (int)LONG_RUN && e2 < 128) nb = q2, ne = e2;
+            else foreign = true, gb = gq, ge = gq + ax.rlen_at[gq];
+          }
+        }
+      }
+      if (nb >= 0) {
+        nbs[s] = nb;
+        for (int u = nb; u < ne && ent[u] < i; ++u) rnb[s] |= (uint64_t)m32(q, pk[u]) << (u - nb);
+      } else if (foreign) {
+        const Query qy = make_query(cfull[s], me.y, ax.len_ratio, ax.pos_ratio);
+        for (uint32_t g = ge; g-- > gb;)  // newest first, only entries inserted before i
+          if (ax.ent[g] < i) consider(ax, fs[s], g, qy);
+        if (fs[s].win != NONE) fs[s].win = ax.ent[fs[s].win];
+      }
+    }
+    // rounds of ballots: a matching ACTIVE candidate means a hit; a matching
+    // UNKNOWN one blocks the final decision (it may still become ACTIVE and win)
+    uint64_t A0, A1;
+    for (;;) {
+      A0 = __ballot(own[0] && st[0] == ST_ACTIVE);
+      A1 = __ballot(own[1] && st[1] == ST_ACTIVE);
+      const uint64_t U0 = __ballot(own[0] && st[0] == ST_UNKNOWN);
+      const uint64_t U1 = __ballot(own[1] && st[1] == ST_UNKNOWN);
+      bool changed = false;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
+        const bool has_act = (bits_from(A0, A1, rs[s]) & rown[s]) != 0 ||
+                             (rnb[s] && (bits_from(A0, A1, nbs[s]) & rnb[s]) != 0) ||
+                             fs[s].any_active;
+        const bool has_unk = (bits_from(U0, U1, rs[s]) & rown[s]) != 0 ||
+                             (rnb[s] && (bits_from(U0, U1, nbs[s]) & rnb[s]) != 0) ||
+                             fs[s].any_unknown;
+        if (st[s] == ST_UNKNOWN) {
+          if (has_act) st[s] = ST_HIT_PENDING, changed = true;
+          else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
+        }
+        if (st[s] == ST_HIT_PENDING && !has_unk) st[s] = ST_HIT, changed = true;
+      }
+      if (!__ballot(changed)) break;
+    }
+    // winners: the first strict maximum in scan order among the matching
+    // ACTIVE candidates (own run newest first, then the neighbour run); a
+    // single candidate needs no deviation
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (!own[s]) continue;
+      pending |= st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING;
+      if (st[s] == st0[s]) continue;
+      const uint32_t p = base + 64 * s + lane;
+      if (st[s] == ST_HIT) {
+        const uint64_t ao = bits_from(A0, A1, rs[s]) & rown[s];
+        const uint64_t an = rnb[s] ? bits_from(A0, A1, nbs[s]) & rnb[s] : 0;
+        uint32_t win;
+        if (__popcll(ao) + __popcll(an) + (fs[s].any_active ? 1 : 0) == 1) {
+          win = ao ? ent[rs[s] + 63 - __clzll(ao)]
+                   : an ? ent[nbs[s] + 63 - __clzll(an)] : fs[s].win;
+        } else {
+          const int P = 64 * s + lane;
+          const Q32 q = make_q32(cfull[s], pk[P].y, ax.len_ratio, ax.pos_ratio);
+          double best = 0.0;
+          win = NONE;
+          uint64_t b = ao;
+          while (b) {
+            const int v = 63 - __clzll(b);
+            b &= ~(1ull << v);
+            const double d = dev32(q, pk[rs[s] + v], ax.len_ratio, ax.pos_ratio);
+            if (d > best) best = d, win = ent[rs[s] + v];
+          }
+          b = an;
+          while (b) {
+            const int v = 63 - __clzll(b);
+            b &= ~(1ull << v);
+            const double d = dev32(q, pk[nbs[s] + v], ax.len_ratio, ax.pos_ratio);
+            if (d > best) best = d, win = ent[nbs[s] + v];
+          }
+          if (fs[s].any_active && fs[s].best > best) win = fs[s].win;
+        }
+        ax.win[p] = win;
+      }
+      store_state(&ax.state[p], st[s]);
+    }
+    const bool wp = __ballot(pending) != 0;
+    if (lane == 0) wpend[w] = wp;
+  }
+  count_pending(counters, pending);
+}
+
 // ---- one wavefront walks one long run --------------------------------------
 // Entries are decided one after another (the walk is inherently ordered); the
 // 64 lanes split each entry's candidate scan and combine with a wave argmax
@@ -563,7 +784,10 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   // window flags (their real work is what the first one left open)
   if (rl.nwin) {
     kt_begin(st);
-    k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
+    if (rl.fast32)
+      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
+    else
+      k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
     kt_end(st, KID_SWEEP_TILE, first ? 30.0 * ax.m : (double)rl.nwin);
   }
   if (rl.nbig) {

@@ -107,6 +107,20 @@ def test_deviation_boundaries(gpu_ctx, tmp_path, lr, pr):
     gpu_vs_oracle(gpu_ctx, f, bc.GENOME, bc.GENOME, float(lr), float(pr))
 
 
+def test_wide_lengths_generic_sweep(gpu_ctx):
+    """Lengths >= 2^31 switch the occupancy sweep to its 64-bit kernel."""
+    f = rk.synth(20_000, 1_000_000, seed=41)
+    rng = np.random.default_rng(41)
+    k = 40
+    wide = rk.Frags(rng.integers(1, 1_000_000, k).astype(np.uint64),
+                    rng.integers(1, 1_000_000, k).astype(np.uint64),
+                    (np.uint64(2**31) + rng.integers(0, 3, k).astype(np.uint64) * np.uint64(7)),
+                    np.full(k, ord('f'), np.uint8))
+    g = rk.Frags(np.concatenate([f.x_start, wide.x_start]), np.concatenate([f.y_start, wide.y_start]),
+                 np.concatenate([f.length, wide.length]), np.concatenate([f.strand, wide.strand]))
+    gpu_vs_oracle(gpu_ctx, g, 5_000_000_000, 5_000_000_000)
+
+
 def test_empty_and_tiny(gpu_ctx):
     f = rk.Frags(np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint64),
                  np.zeros(0, np.uint8))
