@@ -132,45 +132,112 @@ __device__ void heap_sort_segment(const View &v, uint32_t f, uint32_t l) {
   for (uint32_t x = f; x < l; ++x) v.B[x] = 2;
 }
 
-// Sequential __introsort_loop on a small segment (one lane).  Frames pushed
-// are > 16 and disjoint, so a segment of <= 64 never holds more than 3.
-__device__ void seq_introsort(const View &v, uint32_t f0, uint32_t l0, int d0) {
-  uint32_t sf[8], sl[8];
-  int sd[8];
-  int sp = 0;
-  sf[0] = f0, sl[0] = l0, sd[0] = d0, sp = 1;
-  while (sp) {
-    --sp;
-    uint32_t f = sf[sp], l = sl[sp];
-    int d = sd[sp];
-    bool heap = false;
-    while (l - f > THRESH) {
-      if (d == 0) {
-        heap_sort_segment(v, f, l);
-        heap = true;
-        break;
-      }
-      --d;
-      median_to_first(v, f, l);
-      const uint64_t p = v.K[f];
-      uint32_t i = f + 1, j = l;
-      for (;;) {  // __unguarded_partition
-        while (v.K[i] < p) ++i;
-        --j;
-        while (p < v.K[j]) --j;
-        if (!(i < j)) break;
-        vswap(v, i, j);
-        ++i;
-      }
-      if (l - i > THRESH) {
-        sf[sp] = i, sl[sp] = l, sd[sp] = d, ++sp;
-      } else {
-        v.B[i] = 1;  // right part is a leaf
-      }
-      l = i;
+// position of the r-th (0-based, from bit 0) set bit of m; m has more than r bits
+__device__ __forceinline__ int select_bit(uint64_t m, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ull << w) - 1ull));
+    if (r >= c) {
+      r -= c;
+      m >>= w;
+      pos += w;
     }
-    if (!heap) v.B[f] = 1;
   }
+  return pos;
+}
+
+// __introsort_loop on a segment [f0, f0+n) of at most 64 elements, in
+// registers: lane x holds element f0+x.  Partitions of disjoint sub-segments
+// are independent, so every sub-segment of one recursion level is partitioned
+// at once (each keeps its own depth budget, as in the sequential recursion);
+// each Hoare partition is the stopper matching of wave_partition done with
+// ballots and shuffles.  Leaves (<= 16) get B = 1 at their first element; a
+// depth-exhausted sub-segment is heap-sorted in memory by its first lane.
+template <bool GLOBAL>
+__device__ void reg_introsort(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane) {
+  const int x = (int)lane;
+  const bool in = x < (int)n;
+  uint64_t k = in ? v.K[f0 + x] : ~0ull;
+  uint32_t t = in ? v.T[f0 + x] : 0u;
+  int sf = 0, sl = (int)n, sd = d0;
+  bool heaped = false;
+  const uint64_t below = (1ull << x) - 1ull, above = ~below & ~(1ull << x);
+  for (;;) {
+    bool active = in && !heaped && sl - sf > THRESH;
+    const bool need_heap = active && sd == 0;
+    if (__ballot(need_heap)) {  // rare: heap fallback in memory
+      if (in) v.K[f0 + x] = k, v.T[f0 + x] = t;
+      sync_mem<GLOBAL>();
+      if (need_heap && x == sf) heap_sort_segment(v, f0 + sf, f0 + sl);
+      sync_mem<GLOBAL>();
+      if (in) k = v.K[f0 + x], t = v.T[f0 + x];
+      heaped |= need_heap;
+      active &= !need_heap;
+    }
+    if (!__ballot(active)) break;
+    const int len = sl - sf;
+    // __move_median_to_first(f, f+1, mid, l-1)
+    const int a = active ? sf + 1 : x, b = active ? sf + len / 2 : x, c = active ? sl - 1 : x;
+    const uint64_t ka = __shfl(k, a), kb = __shfl(k, b), kc = __shfl(k, c);
+    int med;
+    if (ka < kb) med = kb < kc ? b : (ka < kc ? c : a);
+    else med = ka < kc ? a : (kb < kc ? c : b);
+    int src = x;
+    if (active) src = x == sf ? med : (x == med ? sf : x);
+    k = __shfl(k, src);
+    t = __shfl(t, src);
+    const uint64_t p = __shfl(k, active ? sf : x);
+    // stoppers of __unguarded_partition(f+1, l, f)
+    const uint64_t segm = (sl >= 64 ? ~0ull : (1ull << sl) - 1ull) & ~((1ull << sf) - 1ull);
+    const bool lf = active && x > sf && !(k < p);
+    const bool rf = active && !(p < k);
+    const uint64_t Ls = __ballot(lf) & segm, Rs = __ballot(rf) & segm;
+    const int nL = __popcll(Ls), nR = __popcll(Rs);
+    int rl = 0, partner = 0;
+    bool stop = false;
+    if (lf) {
+      rl = __popcll(Ls & below);
+      if (rl < nR) {
+        partner = select_bit(Rs, nR - 1 - rl);
+        stop = x >= partner;
+      } else {
+        stop = true;
+      }
+    }
+    const uint64_t stopm = __ballot(stop) & segm;
+    const int lim = nL < nR ? nL : nR;
+    const int K = stopm ? __popcll(Ls & ((1ull << __builtin_ctzll(stopm)) - 1ull)) : lim;
+    int s2 = x;
+    if (lf && rl < K) s2 = partner;
+    if (rf) {
+      const int rr = __popcll(Rs & above);  // rank from the right
+      if (rr < K) s2 = select_bit(Ls, rr);
+    }
+    k = __shfl(k, s2);
+    t = __shfl(t, s2);
+    if (active) {
+      int cut;
+      if (K == 0) {
+        cut = select_bit(Ls, 0);
+      } else {
+        cut = select_bit(Rs, nR - K);
+        if (K < nL) {
+          const int lk = select_bit(Ls, K);
+          if (lk < cut) cut = lk;
+        }
+      }
+      if (x < cut) sl = cut;
+      else sf = cut;
+      --sd;
+    }
+  }
+  if (in) {
+    v.K[f0 + x] = k;
+    v.T[f0 + x] = t;
+    if (!heaped && x == sf) v.B[f0 + x] = 1;
+  }
+  sync_mem<GLOBAL>();
 }
 
 // wavefront-parallel __unguarded_partition_pivot on [f, l); returns the cut
@@ -248,7 +315,7 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
         final_leaf = false;
         break;
       }
-      if (l - f <= 64) {  // small: a single lane finishes this subtree
+      if (l - f <= 64) {  // small: finished in registers (reg_introsort)
         if (lane == 0) smallq[nsmall] = {f, l, d};
         ++nsmall;
         final_leaf = false;
@@ -263,7 +330,10 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
     if (final_leaf && lane == 0) v.B[f] = 1;
     sync_mem<GLOBAL>();
   }
-  for (int q = (int)lane; q < nsmall; q += 64) seq_introsort(v, smallq[q].f, smallq[q].l, smallq[q].d);
+  for (int q = 0; q < nsmall; ++q) {
+    const Frame fr = smallq[q];
+    reg_introsort<GLOBAL>(v, fr.f, fr.l - fr.f, fr.d, lane);
+  }
   for (int q = (int)lane; q < nheap; q += 64) heap_sort_segment(v, heapq[q].f, heapq[q].l);
   sync_mem<GLOBAL>();
   // __final_insertion_sort == stable sort inside every leaf

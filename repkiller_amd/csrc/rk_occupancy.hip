@@ -427,7 +427,7 @@ __device__ __forceinline__ double dev32(const Q32 &q, uint2 o, double lr, double
 
 __global__ void __launch_bounds__(256) k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin,
                                                     uint32_t *counters) {
-  __shared__ uint2 s_pk[4][128];  // {centre low 32 bits, length}
+  __shared__ uint2 s_pk[4][132];  // {centre low 32 bits, length}; 4 entries of read padding
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t w = blockIdx.x * 4 + wv;
@@ -484,7 +484,15 @@ __global__ void __launch_bounds__(256) k_sweep_fast(Axis ax, uint8_t *wpend, uin
       const uint2 me = pk[P];
       const Q32 q = make_q32(cfull[s], me.y, ax.len_ratio, ax.pos_ratio);
       const int n = P - rs[s];
-      for (int j = 0; j < n; ++j) rown[s] |= (uint64_t)m32(q, pk[rs[s] + j]) << j;
+      // four independent LDS reads per step (pk is padded past position 127)
+      for (int j = 0; j < n; j += 4) {
+        const uint2 o0 = pk[rs[s] + j], o1 = pk[rs[s] + j + 1], o2 = pk[rs[s] + j + 2],
+                    o3 = pk[rs[s] + j + 3];
+        uint64_t b4 = (uint64_t)m32(q, o0) | (uint64_t)m32(q, o1) << 1 |
+                      (uint64_t)m32(q, o2) << 2 | (uint64_t)m32(q, o3) << 3;
+        if (n - j < 4) b4 &= (1ull << (n - j)) - 1ull;
+        rown[s] |= b4 << j;
+      }
       const int dir = neighbour_dir(cfull[s], ax.max_index);
       if (!dir) continue;
       const uint32_t i = ent[P], k = key[P];
