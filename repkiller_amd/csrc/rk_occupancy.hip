@@ -382,6 +382,32 @@ __device__ __forceinline__ uint64_t bits_from(uint64_t lo, uint64_t hi, int a) {
   return a ? (lo >> a) | (hi << (64 - a)) : lo;
 }
 
+// A neighbour run owned elsewhere, scanned from global memory from g0 in
+// direction `step` while the key is `want` (no run-table lookup; the key,
+// id, state, centre and length of an entry are loaded together); only
+// entries inserted before i count.  Ties go to the higher position (newest
+// first, the reference's scan order).  fs.win receives the winner's id.
+__device__ __forceinline__ void foreign_scan(const Axis &ax, uint32_t g0, int step, uint32_t want,
+                                             uint32_t i, const Query &qy, Scan &fs) {
+  uint32_t bestpos = 0;
+  for (uint32_t q = g0;; q += step) {
+    if (step < 0 ? q == NONE : q >= ax.m) return;
+    const uint32_t kq = ax.key[q], eq = ax.ent[q];
+    const uint8_t sq = load_state(&ax.state[q]);
+    const uint64_t cq = ax.cen[q], lq = ax.len[q];
+    if (kq != want) return;
+    if (eq >= i || sq >= ST_HIT_PENDING || !matches(qy, cq, lq)) continue;
+    if (sq != ST_ACTIVE) {
+      fs.any_unknown = true;
+      continue;
+    }
+    const double d = deviation(qy.c, qy.L, cq, lq, ax.len_ratio, ax.pos_ratio);
+    if (!fs.any_active || d > fs.best || (d == fs.best && q > bestpos))
+      fs.best = d, fs.win = eq, bestpos = q;
+    fs.any_active = true;
+  }
+}
+
 // ---- 32-bit fast path of the window sweep --------------------------------
 // When every length is below 2^31 (checked once per call in k_prep_keys), the
 // length difference of two entries fits 31 bits and the centre difference of
@@ -425,8 +451,8 @@ __device__ __forceinline__ double dev32(const Q32 &q, uint2 o, double lr, double
   return sl * 0.4 + sp * 0.6;
 }
 
-__global__ void __launch_bounds__(256) k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin,
-                                                    uint32_t *counters) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
   __shared__ uint2 s_pk[4][132];  // {centre low 32 bits, length}; 4 entries of read padding
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -496,7 +522,7 @@ __global__ void __launch_bounds__(256) k_sweep_fast(Axis ax, uint8_t *wpend, uin
       const int dir = neighbour_dir(cfull[s], ax.max_index);
       if (!dir) continue;
       const uint32_t i = ent[P], k = key[P];
-      uint32_t gb = 0, ge = 0;
+      uint32_t g0 = 0;  // first position of a foreign neighbour scan
       bool foreign = false;
       int nb = -1, ne = -1;
       if (dir < 0) {
@@ -505,20 +531,20 @@ __global__ void __launch_bounds__(256) k_sweep_fast(Axis ax, uint8_t *wpend, uin
           if (key[q2] == k - 1) {
             const int b2 = hs_le(S0, S1, q2);
             if (b2 >= 0) nb = b2, ne = rs[s];
-            else foreign = true, ge = base + rs[s], gb = ax.rbeg_at[ge - 1];
+            else foreign = true, g0 = base + q2;
           }
-        } else if (base > 0 && ax.key[base - 1] == k - 1) {
-          foreign = true, ge = base, gb = ax.rbeg_at[base - 1];
+        } else if (base > 0) {
+          foreign = true, g0 = base - 1;  // the key test happens in the scan
         }
       } else {
         const int q2 = ls_gt(S0, S1, P);
         const uint32_t gq = base + q2;
         if (gq < m) {
-          const uint32_t kq = q2 < 128 ? key[q2] : ax.key[gq];
+          const uint32_t kq = q2 < 128 ? key[q2] : k + 1;  // q2 == 128: tested in the scan
           if (kq == k + 1) {
             const int e2 = q2 < 127 ? ls_gt(S0, S1, q2) : 128;
             if (q2 < 64 && e2 - q2 <= (int)LONG_RUN && e2 < 128) nb = q2, ne = e2;
-            else foreign = true, gb = gq, ge = gq + ax.rlen_at[gq];
+            else foreign = true, g0 = gq;
           }
         }
       }
@@ -527,9 +553,7 @@ __global__ void __launch_bounds__(256) k_sweep_fast(Axis ax, uint8_t *wpend, uin
         for (int u = nb; u < ne && ent[u] < i; ++u) rnb[s] |= (uint64_t)m32(q, pk[u]) << (u - nb);
       } else if (foreign) {
         const Query qy = make_query(cfull[s], me.y, ax.len_ratio, ax.pos_ratio);
-        for (uint32_t g = ge; g-- > gb;)  // newest first, only entries inserted before i
-          if (ax.ent[g] < i) consider(ax, fs[s], g, qy);
-        if (fs[s].win != NONE) fs[s].win = ax.ent[fs[s].win];
+        foreign_scan(ax, g0, dir, k + dir, i, qy, fs[s]);
       }
     }
     // rounds of ballots: a matching ACTIVE candidate means a hit; a matching
