@@ -8,8 +8,9 @@
 //   2 counting_sort    -> processing order (stable bucket order of FragmentsDatabase)
 //   3 gather_proc      processing-order SoA + 100-bp bucket keys + sort key
 //   4 counting_sort x2 -> X and Y occupancy CSRs (SequenceOcupationList buckets)
-//   5 sweeps on X, then Y (rk_occupancy.hip) until every fragment is decided
-//   6 parents -> pointer jumping -> new-group rank (DPP scan) -> gid
+//   5 sweeps on X, then Y (rk_occupancy.hip) until every fragment is decided;
+//     X hits get their parent from k_x_results, X misses from the Y sweeps
+//   6 pointer jumping -> new-group rank (DPP scan) -> gid
 //   7 counting_sort    -> group member lists in processing order
 //   8 sort_groups      libstdc++ introsort per group; 9 emit flags / order
 //
@@ -52,8 +53,8 @@ namespace rk {
 const char *const kKernelNames[KID_COUNT] = {
     "k_prep_keys",     "k_digit_hist",      "k_digit_scatter", "k_gather_proc",
     "k_sort_keys",     "k_csr_fill_x",      "k_run_bounds",    "k_sweep_tile",
-    "k_sweep_wave",    "k_x_results",       "k_csr_fill_y",    "k_y_parents",
-    "k_jump",          "k_assign_gid",      "k_group_offsets", "k_build_records",
+    "k_sweep_wave",    "k_x_results",       "k_merge_xres",    "k_csr_fill_y",    "k_jump",
+    "k_assign_gid",    "k_group_offsets",   "k_build_records",
     "k_sort_small",    "k_sort_groups_lds", "k_sort_groups_global", "k_emit",
 };
 }  // namespace rk
@@ -101,7 +102,7 @@ struct Work {
   size_t radix_words;
   rk::Proc p;
   rk::Csr cx, cy;
-  uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag, *otag, *xres;
+  uint32_t *isnew, *newrank, *sgid, *gmem, *goff, *tag, *otag;
   void *gsort;
   uint64_t *reckey;
   uint32_t *rpend, *runs, *rlen_at, *rbeg_at;
@@ -124,11 +125,11 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.p.row = c.take<uint32_t>(n);
   w.p.xrec = c.take<ulonglong2>(n);
   w.p.yrec = c.take<ulonglong2>(n);
+  w.p.ylenhi = c.take<uint32_t>(n);
   w.p.xres = c.take<uint32_t>(n);
   w.p.ha = c.take<uint64_t>(n);
   w.p.keyx = c.take<uint32_t>(n);
   w.p.keyy = c.take<uint32_t>(n);
-  w.xres = c.take<uint32_t>(n);
   w.p.par = c.take<uint32_t>(n);
   w.p.gid = c.take<uint32_t>(n);
   for (rk::Csr *cs : {&w.cx, &w.cy}) {
@@ -332,6 +333,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
 
   // 3: processing-order SoA, bucket keys, in-group sort keys
   mark(ctx, RK_PH_GATHER);
+  if (fast32) w.p.ylenhi = nullptr;  // every length fits the Y record's 32-bit field
   rk::gather_proc(f, w.p, m, pl.nbx, pl.nby, st);
 
   // 4: the two occupancy axes as bucket runs (stable: processing order inside)
@@ -345,23 +347,25 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
 
   // 5: X, then Y (X hits join the Y lists; X misses query Y)
   mark(ctx, RK_PH_SWEEP_X);
-  rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, w.rlen_at,
-              w.rbeg_at, m, pl.max_x, prm->len_ratio, prm->pos_ratio};
+  rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, nullptr,
+              w.rlen_at, w.rbeg_at, m, pl.max_x, prm->len_ratio, prm->pos_ratio};
   if ((rc = resolve_axis(ctx, ax, w, ss, fast32, &ctx->stats.x_sweeps))) return rc;
-  rk::x_results(w.cx, w.p.xres, m, w.ctrl, st);
+  // X hits: parent = X winner; X results into the Y records
+  rk::x_results(w.cx, w.p.xres, w.p.yrec, w.p.par, m, w.ctrl, st);
   mark(ctx, RK_PH_SWEEP_Y);
-  rk::csr_fill_y(w.cy, w.p.yrec, w.p.xres, w.xres, m, st);
-  rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.rlen_at,
-              w.rbeg_at, m, pl.max_y, prm->len_ratio, prm->pos_ratio};
+  rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, st);
+  // X misses: the Y sweeps write parent = Y winner, or itself (new group)
+  rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.p.par,
+              w.rlen_at, w.rbeg_at, m, pl.max_y, prm->len_ratio, prm->pos_ratio};
   if ((rc = resolve_axis(ctx, ay, w, ss, fast32, &ctx->stats.y_sweeps))) return rc;
 
   // 6: group roots and ids
   mark(ctx, RK_PH_ROOTS);
-  rk::y_parents(w.cy, w.xres, w.p.par, m, w.ctrl, st);
   HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
   for (;;) {
     HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
-    rk::jump_round(w.p, m, w.ctrl + 5, ctx->stats.jump_rounds == 0 ? w.isnew : nullptr, st);
+    rk::jump_round(w.p, m, w.ctrl + 5, ctx->stats.jump_rounds == 0 ? w.isnew : nullptr, w.ctrl,
+                   st);
     if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
     ctx->stats.jump_rounds++;
     if (!ctx->host[0]) break;

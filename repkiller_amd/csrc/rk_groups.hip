@@ -77,13 +77,14 @@ __global__ void k_gather_proc(Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
     const uint32_t r = p.row[k];
     const ulonglong2 a = p.rec[2 * (size_t)r], b = p.rec[2 * (size_t)r + 1];
     const uint64_t x = a.x, y = a.y, L = b.x;
-    const uint64_t xc = x + L / 2, yc = y + L / 2;
+    const uint64_t xc = x + L / 2;
     const uint32_t s = b.y == 'f' ? 0u : 1u;
     p.ys[k] = y;
     p.xrec[k] = make_ulonglong2(xc, L);
-    p.yrec[k] = make_ulonglong2(yc, L);
+    p.yrec[k] = make_ulonglong2(y + L / 2, L & 0xFFFFFFFFull);  // X result merged later
+    if (p.ylenhi) p.ylenhi[k] = (uint32_t)(L >> 32);
     p.keyx[k] = s * nbx + (uint32_t)(xc / 100);
-    p.keyy[k] = s * nby + (uint32_t)(yc / 100);
+    p.keyy[k] = s * nby + (uint32_t)((y + L / 2) / 100);
   }
 }
 
@@ -121,44 +122,46 @@ __global__ void k_csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m) {
   }
 }
 
-// X-CSR order is nearly processing order, so these writes stay local
-__global__ void k_x_results(Csr c, uint32_t *xres_proc, uint32_t m, uint32_t *err) {
+// X-CSR order is nearly processing order, so these 4-B writes stay local:
+// the X result of every entry, and an X hit's parent (its X winner), which is
+// final (commonFunctions.cpp:55-61)
+__global__ void k_x_results(Csr c, uint32_t *xres, uint32_t *par, uint32_t m, uint32_t *err) {
   GRID_STRIDE(q, m) {
     const uint8_t st = c.state[q];
     if (st != ST_HIT && st != ST_ACTIVE) atomicOr(err, ERRB_INTERNAL);
-    xres_proc[c.ent[q]] = st == ST_HIT ? c.win[q] : NONE;
+    const uint32_t k = c.ent[q];
+    uint32_t xr = NONE;
+    if (st == ST_HIT) {
+      xr = c.win[q];
+      if (xr >= k) {  // winners are always earlier; never let a bad id reach the gathers
+        atomicOr(err, ERRB_INTERNAL);
+        xr = NONE;
+      } else {
+        par[k] = xr;
+      }
+    }
+    xres[k] = xr;
   }
 }
 
-__global__ void k_csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *xres_proc,
-                             uint32_t *xres, uint32_t m) {
+// the X result joins the Y record (processing order, full-record rewrite), so
+// the Y-ordered gather of k_csr_fill_y is one 16-B read per entry
+__global__ void k_merge_xres(ulonglong2 *yrec, const uint32_t *xres, uint32_t m) {
+  GRID_STRIDE(k, m) {
+    ulonglong2 r = yrec[k];
+    r.y = (r.y & 0xFFFFFFFFull) | (uint64_t)xres[k] << 32;
+    yrec[k] = r;
+  }
+}
+
+// X hits sit in the Y list (commonFunctions.cpp:59); X misses query Y
+__global__ void k_csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m) {
   GRID_STRIDE(q, m) {
     const size_t k = c.ent[q];
     const ulonglong2 a = yrec[k];
-    const uint32_t xr = xres_proc[k];
     c.cen[q] = a.x;
-    c.len[q] = a.y;
-    c.state[q] = xr != NONE ? ST_ACTIVE : ST_UNKNOWN;  // X hits are inserted into Y
-    xres[q] = xr;
-  }
-}
-
-// generate_fragment_groups (commonFunctions.cpp:55-76): X hit -> X winner's
-// group; else Y hit -> Y winner's group; else a new group
-__global__ void k_y_parents(Csr c, const uint32_t *xres, uint32_t *par, uint32_t m,
-                            uint32_t *err) {
-  GRID_STRIDE(q, m) {
-    const uint32_t k = c.ent[q], xr = xres[q];
-    const uint8_t st = c.state[q];
-    uint32_t pa = k;
-    if (xr != NONE) pa = xr;
-    else if (st == ST_HIT) pa = c.win[q];
-    else if (st != ST_ACTIVE) atomicOr(err, ERRB_INTERNAL);
-    if (pa > k) {  // winners are always earlier; never let a bad id reach the gathers
-      atomicOr(err, ERRB_INTERNAL);
-      pa = k;
-    }
-    par[k] = pa;
+    c.len[q] = (a.y & 0xFFFFFFFFull) | (ylenhi ? (uint64_t)ylenhi[k] << 32 : 0ull);
+    c.state[q] = (uint32_t)(a.y >> 32) != NONE ? ST_ACTIVE : ST_UNKNOWN;
   }
 }
 
@@ -170,10 +173,15 @@ __global__ void k_group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngrou
   if (blockIdx.x == 0 && threadIdx.x == 0) goff[ngroups] = m;
 }
 
-__global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew) {
+__global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err) {
   bool ch = false;
   GRID_STRIDE(k, m) {
-    const uint32_t a = p.par[k];
+    uint32_t a = p.par[k];
+    if (isnew && a > k) {  // first round: parents are always earlier
+      atomicOr(err, ERRB_INTERNAL);
+      a = k;
+      p.par[k] = k;
+    }
     if (isnew) isnew[k] = a == k;
     const uint32_t b = p.par[a];
     if (a != b) {
@@ -239,25 +247,21 @@ void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, hipStream_t st) {
   k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m);
   kt_end(st, KID_CSR_FILL_X, 37.0 * m);  // id + record in; centre, length, state out
 }
-void x_results(Csr c, uint32_t *xres_proc, uint32_t m, uint32_t *err, hipStream_t st) {
+void x_results(Csr c, uint32_t *xres, ulonglong2 *yrec, uint32_t *par, uint32_t m,
+               uint32_t *err, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_x_results<<<grid_for(m, 256), 256, 0, st>>>(c, xres_proc, m, err);
-  kt_end(st, KID_X_RESULTS, 13.0 * m);  // state, winner, id in; result out
+  k_x_results<<<grid_for(m, 256), 256, 0, st>>>(c, xres, par, m, err);
+  kt_end(st, KID_X_RESULTS, 17.0 * m);  // state, winner, id in; X result (+ parent) out
+  kt_begin(st);
+  k_merge_xres<<<grid_for(m, 256), 256, 0, st>>>(yrec, xres, m);
+  kt_end(st, KID_MERGE_XRES, 36.0 * m);  // Y record + X result in, Y record out
 }
-void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *xres_proc, uint32_t *xres,
-                uint32_t m, hipStream_t st) {
+void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, xres_proc, xres, m);
-  kt_end(st, KID_CSR_FILL_Y, 45.0 * m);  // id, record, X result in; centre, length, state, X result out
-}
-void y_parents(Csr c, const uint32_t *xres, uint32_t *par, uint32_t m, uint32_t *err,
-               hipStream_t st) {
-  if (!m) return;
-  kt_begin(st);
-  k_y_parents<<<grid_for(m, 256), 256, 0, st>>>(c, xres, par, m, err);
-  kt_end(st, KID_Y_PARENTS, 17.0 * m);  // id, X result, state, winner in; parent out
+  k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, ylenhi, m);
+  kt_end(st, KID_CSR_FILL_Y, 37.0 * m);  // id, Y record in; centre, length, state out
 }
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st) {
@@ -265,10 +269,11 @@ void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t 
   k_group_offsets<<<grid_for(m, 256), 256, 0, st>>>(sgid, m, ngroups, goff);
   kt_end(st, KID_GROUP_OFFSETS, 4.0 * m + 4.0 * ngroups);
 }
-void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, hipStream_t st) {
+void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
+                hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed, isnew);
+  k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed, isnew, err);
   kt_end(st, KID_JUMP, (isnew ? 12.0 : 8.0) * m);  // parent, grandparent (+ new flag)
 }
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {

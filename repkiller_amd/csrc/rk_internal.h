@@ -53,7 +53,7 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch
 // DESIGN.md "Kernels and their rooflines").
 enum KernelId : int {
   KID_PREP, KID_HIST, KID_SCATTER, KID_GATHER, KID_SORT_KEYS, KID_CSR_FILL_X, KID_RUN_BOUNDS,
-  KID_SWEEP_TILE, KID_SWEEP_WAVE, KID_X_RESULTS, KID_CSR_FILL_Y, KID_Y_PARENTS, KID_JUMP,
+  KID_SWEEP_TILE, KID_SWEEP_WAVE, KID_X_RESULTS, KID_MERGE_XRES, KID_CSR_FILL_Y, KID_JUMP,
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_COUNT
 };
@@ -95,7 +95,9 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   const uint64_t *cen; // centre
   const uint64_t *len; // length
   uint8_t *state;      // ST_*
-  uint32_t *win;       // winner's processing index (valid when ST_HIT)
+  uint32_t *win;       // winner's processing index (valid when ST_HIT; X axis)
+  uint32_t *par;       // Y axis: parent of every entry decided here (X misses), by
+                       // processing index -- Y winner, or itself for a new group
   uint32_t *rlen_at;   // run length, stored at each run's first position
   uint32_t *rbeg_at;   // run start, stored at each run's last position
   uint32_t m;          // entries
@@ -133,8 +135,10 @@ struct Proc {  // processing-order working set
   uint32_t *pkey;  // sorted xStart/10 key
   uint32_t *row;   // proc -> file row
   ulonglong2 *xrec;  // {x centre, length}
-  ulonglong2 *yrec;  // {y centre, length}
-  uint32_t *xres;    // X result per fragment: X winner (X hit) or NONE (X miss)
+  ulonglong2 *yrec;  // {y centre, length low 32 | X result << 32} (X result: X winner or
+                     // NONE, merged in by x_results)
+  uint32_t *xres;    // X result per fragment
+  uint32_t *ylenhi;  // length high 32 bits, only when some length >= 2^31 (else null)
   uint64_t *ha;
   uint32_t *keyx, *keyy;
   uint32_t *par, *gid;
@@ -152,17 +156,17 @@ void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, u
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
 // X axis in CSR order: centre/length, state UNKNOWN
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, hipStream_t st);
-// X results (X-CSR order, i.e. nearly processing order) -> p.xres
-void x_results(Csr c, uint32_t *xres_proc, uint32_t m, uint32_t *err, hipStream_t st);
+// X results (X-CSR order, i.e. nearly processing order): into the Y records,
+// and the parent of every X hit (its X winner); X misses get theirs from the
+// Y sweeps (Axis::par)
+void x_results(Csr c, uint32_t *xres, ulonglong2 *yrec, uint32_t *par, uint32_t m,
+               uint32_t *err, hipStream_t st);
 // Y axis in CSR order: centre/length, state ACTIVE for X hits (they sit in the
-// Y list) else UNKNOWN; xres[q] = the entry's X result
-void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *xres_proc, uint32_t *xres,
-                uint32_t m, hipStream_t st);
-// parent of every fragment: X winner, else Y winner, else itself (new group)
-void y_parents(Csr c, const uint32_t *xres, uint32_t *par, uint32_t m, uint32_t *err,
-               hipStream_t st);
+// Y list) else UNKNOWN
+void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m, hipStream_t st);
 // one pointer-jumping round; the first also writes isnew[k] = (par[k] == k)
-void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, hipStream_t st);
+void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
+                hipStream_t st);
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st);
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st);

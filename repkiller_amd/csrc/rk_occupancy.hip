@@ -366,7 +366,10 @@ __global__ void __launch_bounds__(256) k_sweep_tile(Axis ax, uint8_t *wpend, uin
           }
         }
         if (fs[s].any_active && fs[s].best > best) best = fs[s].best, win = fwin_ent[s];
-        ax.win[p] = win;
+        if (ax.par) ax.par[ent[P]] = win;
+        else ax.win[p] = win;
+      } else if (st[s] == ST_ACTIVE && ax.par) {
+        ax.par[ent[P]] = ent[P];  // a Y miss opens a new group
       }
       store_state(&ax.state[p], st[s]);
     }
@@ -619,7 +622,10 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
           }
           if (fs[s].any_active && fs[s].best > best) win = fs[s].win;
         }
-        ax.win[p] = win;
+        if (ax.par) ax.par[ent[64 * s + lane]] = win;
+        else ax.win[p] = win;
+      } else if (st[s] == ST_ACTIVE && ax.par) {
+        ax.par[ent[64 * s + lane]] = ent[64 * s + lane];  // a Y miss opens a new group
       }
       store_state(&ax.state[p], st[s]);
     }
@@ -706,7 +712,12 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big
       wave_combine(s);
       const uint8_t ns = decide(s);
       if (lane == 0) {
-        if (ns == ST_HIT) ax.win[t] = ax.ent[s.win];
+        if (ns != st && ax.par) {  // Y axis: final decisions give the parent
+          if (ns == ST_HIT) ax.par[i] = ax.ent[s.win];
+          else if (ns == ST_ACTIVE) ax.par[i] = i;
+        } else if (ns == ST_HIT) {
+          ax.win[t] = ax.ent[s.win];
+        }
         if (ns != st) store_state(&ax.state[t], ns);
       }
       pending |= ns == ST_UNKNOWN || ns == ST_HIT_PENDING;
