@@ -139,6 +139,8 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
     cs->len = c.take<uint64_t>(n);
     cs->state = c.take<uint8_t>(n);
     cs->win = c.take<uint32_t>(n);
+    cs->pk = c.take<uint2>(n);
+    cs->nbd = c.take<uint8_t>(n);
   }
   w.isnew = c.take<uint32_t>(n);
   w.newrank = c.take<uint32_t>(n);
@@ -333,7 +335,10 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
 
   // 3: processing-order SoA, bucket keys, in-group sort keys
   mark(ctx, RK_PH_GATHER);
-  if (fast32) w.p.ylenhi = nullptr;  // every length fits the Y record's 32-bit field
+  if (fast32) {  // every length fits 32 bits: the 64-bit centre/length copies are unused
+    w.p.ylenhi = nullptr;
+    w.cx.cen = w.cx.len = w.cy.cen = w.cy.len = nullptr;
+  }
   rk::gather_proc(f, w.p, m, pl.nbx, pl.nby, st);
 
   // 4: the two occupancy axes as bucket runs (stable: processing order inside)
@@ -342,21 +347,23 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
                        rk::bit_length(2ull * pl.nbx - 1), w.radix, w.radix_words, st);
   rk::radix_sort_pairs(w.p.keyy, nullptr, w.cy.key, w.cy.ent, w.tk, w.tv, m,
                        rk::bit_length(2ull * pl.nby - 1), w.radix, w.radix_words, st);
-  rk::csr_fill_x(w.cx, w.p.xrec, m, st);
+  rk::csr_fill_x(w.cx, w.p.xrec, m, pl.max_x, st);
   HIPCHK(ctx, hipGetLastError());
 
   // 5: X, then Y (X hits join the Y lists; X misses query Y)
   mark(ctx, RK_PH_SWEEP_X);
   rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, nullptr,
-              w.rlen_at, w.rbeg_at, m, pl.max_x, prm->len_ratio, prm->pos_ratio};
+              w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, prm->len_ratio,
+              prm->pos_ratio};
   if ((rc = resolve_axis(ctx, ax, w, ss, fast32, &ctx->stats.x_sweeps))) return rc;
   // X hits: parent = X winner; X results into the Y records
   rk::x_results(w.cx, w.p.xres, w.p.yrec, w.p.par, m, w.ctrl, st);
   mark(ctx, RK_PH_SWEEP_Y);
-  rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, st);
+  rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, pl.max_y, st);
   // X misses: the Y sweeps write parent = Y winner, or itself (new group)
   rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.p.par,
-              w.rlen_at, w.rbeg_at, m, pl.max_y, prm->len_ratio, prm->pos_ratio};
+              w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, prm->len_ratio,
+              prm->pos_ratio};
   if ((rc = resolve_axis(ctx, ay, w, ss, fast32, &ctx->stats.y_sweeps))) return rc;
 
   // 6: group roots and ids

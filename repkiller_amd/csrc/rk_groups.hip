@@ -113,11 +113,17 @@ __global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m) {
   }
 }
 
-__global__ void k_csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m) {
+__device__ __forceinline__ uint8_t nbd_code(uint64_t c, uint64_t max_index) {
+  const int d = neighbour_dir(c, max_index);
+  return d < 0 ? 1 : d > 0 ? 2 : 0;
+}
+
+__global__ void k_csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index) {
   GRID_STRIDE(q, m) {
     const ulonglong2 r = xrec[c.ent[q]];
-    c.cen[q] = r.x;
-    c.len[q] = r.y;
+    if (c.cen) c.cen[q] = r.x, c.len[q] = r.y;  // the 64-bit kernels only
+    c.pk[q] = make_uint2((uint32_t)r.x, (uint32_t)r.y);
+    c.nbd[q] = nbd_code(r.x, max_index);
     c.state[q] = ST_UNKNOWN;
   }
 }
@@ -155,12 +161,17 @@ __global__ void k_merge_xres(ulonglong2 *yrec, const uint32_t *xres, uint32_t m)
 }
 
 // X hits sit in the Y list (commonFunctions.cpp:59); X misses query Y
-__global__ void k_csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m) {
+__global__ void k_csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
+                             uint64_t max_index) {
   GRID_STRIDE(q, m) {
     const size_t k = c.ent[q];
     const ulonglong2 a = yrec[k];
-    c.cen[q] = a.x;
-    c.len[q] = (a.y & 0xFFFFFFFFull) | (ylenhi ? (uint64_t)ylenhi[k] << 32 : 0ull);
+    if (c.cen) {  // the 64-bit kernels only
+      c.cen[q] = a.x;
+      c.len[q] = (a.y & 0xFFFFFFFFull) | (ylenhi ? (uint64_t)ylenhi[k] << 32 : 0ull);
+    }
+    c.pk[q] = make_uint2((uint32_t)a.x, (uint32_t)a.y);
+    c.nbd[q] = nbd_code(a.x, max_index);
     c.state[q] = (uint32_t)(a.y >> 32) != NONE ? ST_ACTIVE : ST_UNKNOWN;
   }
 }
@@ -241,11 +252,12 @@ void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby,
   k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m);
   kt_end(st, KID_SORT_KEYS, 20.0 * m);  // key + yStart in, sort key out
 }
-void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, hipStream_t st) {
+void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m);
-  kt_end(st, KID_CSR_FILL_X, 37.0 * m);  // id + record in; centre, length, state out
+  k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m, max_index);
+  // id + record in; (centre, length,) packed record, neighbour code, state out
+  kt_end(st, KID_CSR_FILL_X, (c.cen ? 46.0 : 30.0) * m);
 }
 void x_results(Csr c, uint32_t *xres, ulonglong2 *yrec, uint32_t *par, uint32_t m,
                uint32_t *err, hipStream_t st) {
@@ -257,11 +269,13 @@ void x_results(Csr c, uint32_t *xres, ulonglong2 *yrec, uint32_t *par, uint32_t 
   k_merge_xres<<<grid_for(m, 256), 256, 0, st>>>(yrec, xres, m);
   kt_end(st, KID_MERGE_XRES, 36.0 * m);  // Y record + X result in, Y record out
 }
-void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m, hipStream_t st) {
+void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
+                uint64_t max_index, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, ylenhi, m);
-  kt_end(st, KID_CSR_FILL_Y, 37.0 * m);  // id, Y record in; centre, length, state out
+  k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, ylenhi, m, max_index);
+  // id, Y record in; (centre, length,) packed record, neighbour code, state out
+  kt_end(st, KID_CSR_FILL_Y, (c.cen ? 46.0 : 30.0) * m);
 }
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st) {

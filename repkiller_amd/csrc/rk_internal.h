@@ -98,6 +98,8 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   uint32_t *win;       // winner's processing index (valid when ST_HIT; X axis)
   uint32_t *par;       // Y axis: parent of every entry decided here (X misses), by
                        // processing index -- Y winner, or itself for a new group
+  const uint2 *pk;     // {centre low 32, length low 32}: the 32-bit sweep's record
+  const uint8_t *nbd;  // neighbour_dir code per entry (0, 1 = -1, 2 = +1)
   uint32_t *rlen_at;   // run length, stored at each run's first position
   uint32_t *rbeg_at;   // run start, stored at each run's last position
   uint32_t m;          // entries
@@ -148,14 +150,28 @@ struct Csr {  // one axis in CSR order (see Axis)
   uint64_t *cen, *len;
   uint8_t *state;
   uint32_t *win;
+  uint2 *pk;     // {centre low 32 bits, length low 32 bits} (the 32-bit sweep)
+  uint8_t *nbd;  // neighbour bucket probed: 0 none, 1 = B-1, 2 = B+1
 };
+
+// The neighbour bucket get_associated_group effectively probes
+// (SequenceOcupationList.cpp:47-89): rescanning a bucket under the strict `>`
+// is a no-op, so only B-1 (c % 100 in {0, 1}, c >= 100) or B+1 (c % 100 == 99
+// and c < max_index, or c % 100 == 98 and c < max_index - 1) can add
+// candidates.  -1 / +1 / 0.
+__device__ __forceinline__ int neighbour_dir(uint64_t c, uint64_t max_index) {
+  const uint64_t r = c % 100;
+  if (r <= 1 && c >= 100) return -1;
+  if ((r == 99 && c < max_index) || (r == 98 && c < max_index - 1)) return 1;
+  return 0;
+}
 // processing key per file row (dropped last bucket -> vsize-1, sorts last);
 // counts kept rows into *kept; flags UB into *err
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
                ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st);
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
-// X axis in CSR order: centre/length, state UNKNOWN
-void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, hipStream_t st);
+// X axis in CSR order: centre/length (+ packed record, neighbour code), state UNKNOWN
+void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st);
 // X results (X-CSR order, i.e. nearly processing order): into the Y records,
 // and the parent of every X hit (its X winner); X misses get theirs from the
 // Y sweeps (Axis::par)
@@ -163,7 +179,8 @@ void x_results(Csr c, uint32_t *xres, ulonglong2 *yrec, uint32_t *par, uint32_t 
                uint32_t *err, hipStream_t st);
 // Y axis in CSR order: centre/length, state ACTIVE for X hits (they sit in the
 // Y list) else UNKNOWN
-void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m, hipStream_t st);
+void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
+                uint64_t max_index, hipStream_t st);
 // one pointer-jumping round; the first also writes isnew[k] = (par[k] == k)
 void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
                 hipStream_t st);

@@ -93,13 +93,6 @@ __device__ __forceinline__ bool matches(const Query &q, uint64_t oc, uint64_t oL
   return q.ok && al <= q.bl && ac <= q.bc && !(al == q.bl && ac == q.bc);
 }
 
-// -1: bucket B-1, +1: bucket B+1, 0: none
-__device__ __forceinline__ int neighbour_dir(uint64_t c, uint64_t max_index) {
-  const uint64_t r = c % 100;
-  if (r <= 1 && c >= 100) return -1;
-  if ((r == 99 && c < max_index) || (r == 98 && c < max_index - 1)) return 1;
-  return 0;
-}
 
 // States only move UNKNOWN -> decided (and HIT_PENDING -> HIT), so a stale
 // read of another run's state is always conservative: it can only postpone a
@@ -385,32 +378,6 @@ __device__ __forceinline__ uint64_t bits_from(uint64_t lo, uint64_t hi, int a) {
   return a ? (lo >> a) | (hi << (64 - a)) : lo;
 }
 
-// A neighbour run owned elsewhere, scanned from global memory from g0 in
-// direction `step` while the key is `want` (no run-table lookup; the key,
-// id, state, centre and length of an entry are loaded together); only
-// entries inserted before i count.  Ties go to the higher position (newest
-// first, the reference's scan order).  fs.win receives the winner's id.
-__device__ __forceinline__ void foreign_scan(const Axis &ax, uint32_t g0, int step, uint32_t want,
-                                             uint32_t i, const Query &qy, Scan &fs) {
-  uint32_t bestpos = 0;
-  for (uint32_t q = g0;; q += step) {
-    if (step < 0 ? q == NONE : q >= ax.m) return;
-    const uint32_t kq = ax.key[q], eq = ax.ent[q];
-    const uint8_t sq = load_state(&ax.state[q]);
-    const uint64_t cq = ax.cen[q], lq = ax.len[q];
-    if (kq != want) return;
-    if (eq >= i || sq >= ST_HIT_PENDING || !matches(qy, cq, lq)) continue;
-    if (sq != ST_ACTIVE) {
-      fs.any_unknown = true;
-      continue;
-    }
-    const double d = deviation(qy.c, qy.L, cq, lq, ax.len_ratio, ax.pos_ratio);
-    if (!fs.any_active || d > fs.best || (d == fs.best && q > bestpos))
-      fs.best = d, fs.win = eq, bestpos = q;
-    fs.any_active = true;
-  }
-}
-
 // ---- 32-bit fast path of the window sweep --------------------------------
 // When every length is below 2^31 (checked once per call in k_prep_keys), the
 // length difference of two entries fits 31 bits and the centre difference of
@@ -422,10 +389,10 @@ struct Q32 {
   uint32_t c, L, tl, tc;
   bool ok, eq;
 };
-__device__ __forceinline__ Q32 make_q32(uint64_t c, uint32_t L, double lr, double pr) {
+__device__ __forceinline__ Q32 make_q32(uint32_t c, uint32_t L, double lr, double pr) {
   Q32 q;
   const double bl = (double)L * lr, bc = (double)L * pr;
-  q.c = (uint32_t)c;
+  q.c = c;
   q.L = L;
   q.ok = L != 0 && bl == bl && bc == bc;
   q.tl = bl >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)bl;
@@ -454,6 +421,34 @@ __device__ __forceinline__ double dev32(const Q32 &q, uint2 o, double lr, double
   return sl * 0.4 + sp * 0.6;
 }
 
+// A neighbour run owned elsewhere, scanned from global memory from g0 in
+// direction `step` while the key is `want` (no run-table lookup; key, id,
+// state and packed record of an entry are loaded together); only entries
+// inserted before i count.  Ties go to the higher position (newest first, the
+// reference's scan order).  fs.win receives the winner's id.  The packed
+// 32-bit records suffice: lengths are < 2^31 and a centre in an adjacent
+// bucket differs by less than 200.
+__device__ __forceinline__ void foreign_scan32(const Axis &ax, uint32_t g0, int step,
+                                               uint32_t want, uint32_t i, const Q32 &q, Scan &fs) {
+  uint32_t bestpos = 0;
+  for (uint32_t g = g0;; g += step) {
+    if (step < 0 ? g == NONE : g >= ax.m) return;
+    const uint32_t kg = ax.key[g], eg = ax.ent[g];
+    const uint8_t sg = load_state(&ax.state[g]);
+    const uint2 o = ax.pk[g];
+    if (kg != want) return;
+    if (eg >= i || sg >= ST_HIT_PENDING || !m32(q, o)) continue;
+    if (sg != ST_ACTIVE) {
+      fs.any_unknown = true;
+      continue;
+    }
+    const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
+    if (!fs.any_active || d > fs.best || (d == fs.best && g > bestpos))
+      fs.best = d, fs.win = eg, bestpos = g;
+    fs.any_active = true;
+  }
+}
+
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
 k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
   __shared__ uint2 s_pk[4][132];  // {centre low 32 bits, length}; 4 entries of read padding
@@ -478,8 +473,7 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
     }
     bool own[2];
     int rs[2];
-    uint8_t st[2], st0[2];
-    uint64_t cfull[2];
+    uint8_t st[2], st0[2], nd[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int P = 64 * s + lane;
@@ -487,13 +481,13 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
       const int re = ls_gt(S0, S1, P);
       own[s] = base + P < m && rs[s] >= 0 && rs[s] < 64 && re - rs[s] <= (int)LONG_RUN;
       st[s] = ST_HIT;
-      cfull[s] = 0;
+      nd[s] = 0;
       if (own[s]) {
         const uint32_t p = base + P;
-        cfull[s] = ax.cen[p];
-        pk[P] = make_uint2((uint32_t)cfull[s], (uint32_t)ax.len[p]);
+        pk[P] = ax.pk[p];
         ent[P] = ax.ent[p];
         st[s] = ax.state[p];
+        nd[s] = ax.nbd[p];
       }
       st0[s] = st[s];
     }
@@ -511,7 +505,7 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
       if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
       const int P = 64 * s + lane;
       const uint2 me = pk[P];
-      const Q32 q = make_q32(cfull[s], me.y, ax.len_ratio, ax.pos_ratio);
+      const Q32 q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
       const int n = P - rs[s];
       // four independent LDS reads per step (pk is padded past position 127)
       for (int j = 0; j < n; j += 4) {
@@ -522,8 +516,8 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
         if (n - j < 4) b4 &= (1ull << (n - j)) - 1ull;
         rown[s] |= b4 << j;
       }
-      const int dir = neighbour_dir(cfull[s], ax.max_index);
-      if (!dir) continue;
+      if (!nd[s]) continue;
+      const int dir = nd[s] == 1 ? -1 : 1;
       const uint32_t i = ent[P], k = key[P];
       uint32_t g0 = 0;  // first position of a foreign neighbour scan
       bool foreign = false;
@@ -555,8 +549,7 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
         nbs[s] = nb;
         for (int u = nb; u < ne && ent[u] < i; ++u) rnb[s] |= (uint64_t)m32(q, pk[u]) << (u - nb);
       } else if (foreign) {
-        const Query qy = make_query(cfull[s], me.y, ax.len_ratio, ax.pos_ratio);
-        foreign_scan(ax, g0, dir, k + dir, i, qy, fs[s]);
+        foreign_scan32(ax, g0, dir, k + dir, i, q, fs[s]);
       }
     }
     // rounds of ballots: a matching ACTIVE candidate means a hit; a matching
@@ -603,7 +596,7 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
                    : an ? ent[nbs[s] + 63 - __clzll(an)] : fs[s].win;
         } else {
           const int P = 64 * s + lane;
-          const Q32 q = make_q32(cfull[s], pk[P].y, ax.len_ratio, ax.pos_ratio);
+          const Q32 q = make_q32(pk[P].x, pk[P].y, ax.len_ratio, ax.pos_ratio);
           double best = 0.0;
           win = NONE;
           uint64_t b = ao;
@@ -658,6 +651,26 @@ __device__ __forceinline__ void consider_ranked(const Axis &ax, Scan &s, uint32_
   }
 }
 
+// the same on the packed 32-bit records (RunList::fast32)
+__device__ __forceinline__ void consider_ranked32(const Axis &ax, Scan &s, uint32_t q, uint32_t p,
+                                                  const Q32 &qy) {
+  const uint8_t sj = load_state(&ax.state[q]);
+  if (sj >= ST_HIT_PENDING) return;
+  const uint2 o = ax.pk[q];
+  if (!m32(qy, o)) return;
+  if (sj == ST_ACTIVE) {
+    s.any_active = true;
+    const double d = dev32(qy, o, ax.len_ratio, ax.pos_ratio);
+    if (d > s.best || (d == s.best && p < s.pos)) {
+      s.best = d;
+      s.win = q;
+      s.pos = p;
+    }
+  } else {
+    s.any_unknown = true;
+  }
+}
+
 __device__ __forceinline__ void wave_combine(Scan &s) {
   for (int off = 32; off > 0; off >>= 1) {
     const double ob = __shfl_xor(s.best, off);
@@ -675,6 +688,7 @@ __device__ __forceinline__ void wave_combine(Scan &s) {
   }
 }
 
+template <bool FAST>
 __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big, uint32_t nbig,
                                                     uint8_t *rpend, uint32_t *counters) {
   // big = starts of the runs of more than LONG_RUN entries
@@ -692,21 +706,36 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big
     for (uint32_t t = beg; t < end; ++t) {
       const uint8_t st = load_state(&ax.state[t]);
       if (st == ST_ACTIVE || st == ST_HIT) continue;
-      const uint64_t c = ax.cen[t], L = ax.len[t];
       const uint32_t i = ax.ent[t];
-      const Query qy = make_query(c, L, ax.len_ratio, ax.pos_ratio);
+      Query qy;
+      Q32 q32;
+      int dir;
+      if (FAST) {
+        const uint2 me = ax.pk[t];
+        q32 = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
+        dir = ax.nbd[t] == 1 ? -1 : ax.nbd[t] == 2 ? 1 : 0;
+      } else {
+        const uint64_t c = ax.cen[t];
+        qy = make_query(c, ax.len[t], ax.len_ratio, ax.pos_ratio);
+        dir = neighbour_dir(c, ax.max_index);
+      }
       Scan s{0.0, NONE, 0xFFFFFFFFu, false, false};
       for (uint32_t q0 = beg; q0 < t; q0 += 64) {  // own run, newest first: rank t-1-q
         const uint32_t q = q0 + lane;
-        if (q < t) consider_ranked(ax, s, q, t - 1 - q, qy);
+        if (q < t) {
+          if (FAST) consider_ranked32(ax, s, q, t - 1 - q, q32);
+          else consider_ranked(ax, s, q, t - 1 - q, qy);
+        }
       }
-      const int dir = neighbour_dir(c, ax.max_index);
       if ((dir < 0 && has_lo) || (dir > 0 && has_hi)) {
         const uint32_t nb = dir < 0 ? lo_b : hi_b, ne = dir < 0 ? lo_e : hi_e;
         const uint32_t own = t - beg;
         for (uint32_t q0 = nb; q0 < ne; q0 += 64) {
           const uint32_t q = q0 + lane;
-          if (q < ne && ax.ent[q] < i) consider_ranked(ax, s, q, own + (ne - 1 - q), qy);
+          if (q < ne && ax.ent[q] < i) {
+            if (FAST) consider_ranked32(ax, s, q, own + (ne - 1 - q), q32);
+            else consider_ranked(ax, s, q, own + (ne - 1 - q), qy);
+          }
         }
       }
       wave_combine(s);
@@ -835,8 +864,12 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   }
   if (rl.nbig) {
     kt_begin(st);
-    k_sweep_wave<<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
-                                                             counters);
+    if (rl.fast32)
+      k_sweep_wave<true><<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
+                                                                     counters);
+    else
+      k_sweep_wave<false><<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
+                                                                      counters);
     kt_end(st, KID_SWEEP_WAVE, 0.0);
   }
 }
