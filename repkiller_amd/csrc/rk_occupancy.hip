@@ -852,15 +852,17 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
                      bool first, hipStream_t st) {
   (void)hipMemsetAsync(counters, 0, PEND_SLOTS * sizeof(uint32_t), st);
   // algorithmic bytes: the first sweep reads every entry's key, centre, length,
-  // id and state and writes state (+ winner): 30 B; later sweeps only need the
-  // window flags (their real work is what the first one left open)
+  // id and state and writes state (+ winner): 30 B (26 B with the packed 8-B
+  // record and neighbour code of the 32-bit kernel); later sweeps only need
+  // the window flags (their real work is what the first one left open)
   if (rl.nwin) {
     kt_begin(st);
     if (rl.fast32)
       k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
     else
       k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
-    kt_end(st, KID_SWEEP_TILE, first ? 30.0 * ax.m : (double)rl.nwin);
+    kt_end(st, rl.fast32 ? KID_SWEEP_FAST : KID_SWEEP_TILE,
+           first ? (rl.fast32 ? 26.0 : 30.0) * ax.m : (double)rl.nwin);
   }
   if (rl.nbig) {
     kt_begin(st);
