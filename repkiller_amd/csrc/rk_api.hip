@@ -251,7 +251,7 @@ int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss, b
                  uint32_t *sweeps) {
   uint32_t *counters = w.ctrl + 64;
   uint8_t *rpend = reinterpret_cast<uint8_t *>(w.rpend);
-  rk::RunList rl{w.runs, w.wpend, 0, 0, fast32};
+  rk::RunList rl{w.runs, w.wpend, 0, 0, fast32, nullptr};
   rk::build_runs(ax, rl, w.ctrl + 2, ctx->host + 128, ctx->stream);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));

@@ -184,21 +184,29 @@ __global__ void k_group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngrou
   if (blockIdx.x == 0 && threadIdx.x == 0) goff[ngroups] = m;
 }
 
+// Every thread follows its parent chain towards the root (up to 32 links per
+// round) and stores what it reached; other threads compress the same chains
+// concurrently, which only ever replaces a parent by one of its ancestors.
+// Winner chains are short, so one round usually finishes; a chain longer than
+// the step budget reports `changed` and the host runs another round.
 __global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err) {
   bool ch = false;
   GRID_STRIDE(k, m) {
-    uint32_t a = p.par[k];
+    const uint32_t a0 = p.par[k];
+    uint32_t a = a0;
     if (isnew && a > k) {  // first round: parents are always earlier
       atomicOr(err, ERRB_INTERNAL);
       a = k;
       p.par[k] = k;
     }
     if (isnew) isnew[k] = a == k;
-    const uint32_t b = p.par[a];
-    if (a != b) {
-      p.par[k] = b;
-      ch = true;
+    for (int step = 0; step < 32; ++step) {
+      const uint32_t b = p.par[a];
+      if (b == a) break;
+      a = b;
     }
+    if (a != a0) p.par[k] = a;
+    if (p.par[a] != a) ch = true;
   }
   if (ch) *changed = 1u;
 }
@@ -288,7 +296,7 @@ void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t
   if (!m) return;
   kt_begin(st);
   k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed, isnew, err);
-  kt_end(st, KID_JUMP, (isnew ? 12.0 : 8.0) * m);  // parent, grandparent (+ new flag)
+  kt_end(st, KID_JUMP, (isnew ? 16.0 : 12.0) * m);  // parent, root, parent written (+ new flag)
 }
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {
   if (!m) return;

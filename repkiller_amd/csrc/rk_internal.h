@@ -113,7 +113,8 @@ struct RunList {
   uint32_t *big;
   uint8_t *wpend;
   uint32_t nbig, nwin;
-  bool fast32;  // every length < 2^31: the 32-bit window kernel applies
+  bool fast32;          // every length < 2^31: the 32-bit window kernel applies
+  uint32_t *nbig_dev;   // fast32: the long-run count, found by the first sweep
 };
 size_t runs_scratch_words(uint32_t m);
 void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host_words,

@@ -450,7 +450,8 @@ __device__ __forceinline__ void foreign_scan32(const Axis &ax, uint32_t g0, int 
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
+k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_t *big,
+             uint32_t *nbig) {
   __shared__ uint2 s_pk[4][132];  // {centre low 32 bits, length}; 4 entries of read padding
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -480,6 +481,14 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
       rs[s] = hs_le(S0, S1, P);
       const int re = ls_gt(S0, S1, P);
       own[s] = base + P < m && rs[s] >= 0 && rs[s] < 64 && re - rs[s] <= (int)LONG_RUN;
+      if (s == 0 && big) {  // first sweep: list the long runs that start here
+        const bool lng = base + P < m && rs[0] == P && re - P > (int)LONG_RUN;
+        const uint64_t bb = __ballot(lng);
+        uint32_t at = 0;
+        if (lane == 0 && bb) at = atomicAdd(nbig, (uint32_t)__popcll(bb));
+        at = __shfl(at, 0);
+        if (lng) big[at + __popcll(bb & ((1ull << lane) - 1ull))] = base + P;
+      }
       st[s] = ST_HIT;
       nd[s] = 0;
       if (own[s]) {
@@ -688,20 +697,54 @@ __device__ __forceinline__ void wave_combine(Scan &s) {
   }
 }
 
+// first position >= from whose key is not `key` (or m), 64 keys per step
+__device__ __forceinline__ uint32_t wave_scan_end(const Axis &ax, uint32_t from, uint32_t key,
+                                                  uint32_t lane) {
+  for (uint32_t b = from;; b += 64) {
+    const uint32_t q = b + lane;
+    const uint64_t e = __ballot(q >= ax.m || ax.key[q] != key);
+    if (e) return b + __builtin_ctzll(e);
+  }
+}
+// smallest p with key `key` on all of [p, before), 64 keys per step
+__device__ __forceinline__ uint32_t wave_scan_begin(const Axis &ax, uint32_t before, uint32_t key,
+                                                    uint32_t lane) {
+  for (uint32_t b = before;;) {
+    const uint32_t q0 = b >= 64 ? b - 64 : 0;
+    const uint32_t q = q0 + lane;
+    const uint64_t e = __ballot(q < b && ax.key[q] != key);
+    if (e) return q0 + 64 - __clzll(e);
+    if (q0 == 0) return 0;
+    b = q0;
+  }
+}
+
 template <bool FAST>
 __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big, uint32_t nbig,
-                                                    uint8_t *rpend, uint32_t *counters) {
-  // big = starts of the runs of more than LONG_RUN entries
+                                                    const uint32_t *nbig_dev, uint8_t *rpend,
+                                                    uint32_t *counters) {
+  // big = starts of the runs of more than LONG_RUN entries; FAST: the run
+  // table is not built, runs and their neighbours are found by their keys
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nbig;
+  const uint32_t count = FAST ? *nbig_dev : nbig;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < count;
        w += (gridDim.x * blockDim.x) >> 6) {
     const uint32_t beg = big[w];
     if (!rpend[beg]) continue;
     const uint32_t key = ax.key[beg];
-    const uint32_t end = beg + ax.rlen_at[beg];
-    uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
-    const bool has_lo = neighbour_run(ax, beg, end, key, -1, lo_b, lo_e);
-    const bool has_hi = neighbour_run(ax, beg, end, key, 1, hi_b, hi_e);
+    uint32_t end, lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
+    bool has_lo, has_hi;
+    if (FAST) {
+      end = wave_scan_end(ax, beg + LONG_RUN, key, lane);
+      has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
+      if (has_lo) lo_e = beg, lo_b = wave_scan_begin(ax, beg, key - 1, lane);
+      has_hi = end < ax.m && ax.key[end] == key + 1;
+      if (has_hi) hi_b = end, hi_e = wave_scan_end(ax, end + 1, key + 1, lane);
+    } else {
+      end = beg + ax.rlen_at[beg];
+      has_lo = neighbour_run(ax, beg, end, key, -1, lo_b, lo_e);
+      has_hi = neighbour_run(ax, beg, end, key, 1, hi_b, hi_e);
+    }
     bool pending = false;
     for (uint32_t t = beg; t < end; ++t) {
       const uint8_t st = load_state(&ax.state[t]);
@@ -837,12 +880,14 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
                 hipStream_t st) {
   rl.nbig = 0;
   rl.nwin = (ax.m + 63) / 64;
+  rl.nbig_dev = dev_count;
   if (!ax.m) return;
   (void)hipMemsetAsync(dev_count, 0, 4, st);
+  (void)hipMemsetAsync(rl.wpend, 1, rl.nwin, st);
+  if (rl.fast32) return;  // the first sweep lists the long runs itself
   kt_begin(st);
   k_run_bounds<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.nwin, rl.big, dev_count);
   kt_end(st, KID_RUN_BOUNDS, 4.0 * ax.m);  // keys read once (boundary writes not counted)
-  (void)hipMemsetAsync(rl.wpend, 1, rl.nwin, st);
   (void)hipMemcpyAsync(host_words, dev_count, 4, hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
   rl.nbig = host_words[0];
@@ -858,20 +903,21 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   if (rl.nwin) {
     kt_begin(st);
     if (rl.fast32)
-      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
+      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters,
+                                                      first ? rl.big : nullptr, rl.nbig_dev);
     else
       k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
     kt_end(st, rl.fast32 ? KID_SWEEP_FAST : KID_SWEEP_TILE,
            first ? (rl.fast32 ? 26.0 : 30.0) * ax.m : (double)rl.nwin);
   }
-  if (rl.nbig) {
+  if (rl.fast32) {  // the long-run count lives on the device: a fixed grid reads it
     kt_begin(st);
-    if (rl.fast32)
-      k_sweep_wave<true><<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
-                                                                     counters);
-    else
-      k_sweep_wave<false><<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
-                                                                      counters);
+    k_sweep_wave<true><<<256, 256, 0, st>>>(ax, rl.big, 0, rl.nbig_dev, rpend, counters);
+    kt_end(st, KID_SWEEP_WAVE, 0.0);
+  } else if (rl.nbig) {
+    kt_begin(st);
+    k_sweep_wave<false><<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, nullptr,
+                                                                    rpend, counters);
     kt_end(st, KID_SWEEP_WAVE, 0.0);
   }
 }
