@@ -462,8 +462,15 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_
     uint32_t *ent = s_ent[wv], *key = s_key[wv];
     const uint32_t base = w * 64, m = ax.m;
     uint64_t S0, S1;
+    // slot-0 records are loaded with the keys (one memory round trip for
+    // nearly everything; slot 1 only holds the tail of the last run)
+    const uint32_t p0 = base + lane;
+    uint2 pk0 = make_uint2(0, 0);
+    uint32_t ent0 = 0;
+    uint8_t st00 = ST_HIT, nd00 = 0;
+    if (p0 < m) pk0 = ax.pk[p0], ent0 = ax.ent[p0], st00 = ax.state[p0], nd00 = ax.nbd[p0];
     {
-      const uint32_t p0 = base + lane, p1 = base + 64 + lane;
+      const uint32_t p1 = base + 64 + lane;
       const uint32_t k0 = p0 < m ? ax.key[p0] : NONE, k1 = p1 < m ? ax.key[p1] : NONE;
       const uint32_t q0 = p0 < m && p0 > 0 ? ax.key[p0 - 1] : NONE;
       const uint32_t q1 = p1 < m ? ax.key[p1 - 1] : NONE;
@@ -493,10 +500,11 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_
       nd[s] = 0;
       if (own[s]) {
         const uint32_t p = base + P;
-        pk[P] = ax.pk[p];
-        ent[P] = ax.ent[p];
-        st[s] = ax.state[p];
-        nd[s] = ax.nbd[p];
+        if (s == 0) {
+          pk[P] = pk0, ent[P] = ent0, st[s] = st00, nd[s] = nd00;
+        } else {
+          pk[P] = ax.pk[p], ent[P] = ax.ent[p], st[s] = ax.state[p], nd[s] = ax.nbd[p];
+        }
       }
       st0[s] = st[s];
     }
