@@ -9,8 +9,9 @@
 //
 // One pass per 8-bit digit, three kernels:
 //   k_digit_hist   256-bin histogram of each 4096-key tile in LDS (LDS atomics),
-//                  written digit-major: counts[digit * tiles + tile]
-//   exclusive scan over counts (rk_sort.hip, DPP wave scan)
+//                  written tile-major: counts[tile * 256 + digit] (one 1-KB row)
+//   column scan    offset of (tile, digit) = all keys of smaller digits + the
+//                  same digit in earlier tiles, in place, three small kernels
 //   k_digit_scatter  re-reads the tile in index order, ranks every key among
 //                  equal digits (8 wave ballots -> peer mask -> popcount against
 //                  a wave-private counter), places it at its tile-local sorted
@@ -45,7 +46,70 @@ __global__ void __launch_bounds__(T) k_digit_hist(const uint32_t *__restrict__ k
   for (int r = 0; r < ITEMS; ++r)
     if (base + r * T + threadIdx.x < n) atomicAdd(&hist[(kk[r] >> shift) & (RADIX - 1)], 1u);
   __syncthreads();
-  if (threadIdx.x < RADIX) counts[threadIdx.x * tiles + blockIdx.x] = hist[threadIdx.x];
+  if (threadIdx.x < RADIX) counts[(size_t)blockIdx.x * RADIX + threadIdx.x] = hist[threadIdx.x];
+}
+
+// Column scan of the [tiles][256] digit counts: thread d of block b sums
+// digit d over the rows [b*ROWS, (b+1)*ROWS) (each row read coalesced)...
+constexpr uint32_t ROWS = 16;
+__global__ void __launch_bounds__(RADIX) k_col_partial(const uint32_t *__restrict__ counts,
+                                                       uint32_t tiles,
+                                                       uint32_t *__restrict__ part) {
+  const uint32_t t0 = blockIdx.x * ROWS, t1 = min(t0 + ROWS, tiles);
+  uint32_t s = 0;
+  for (uint32_t t = t0; t < t1; ++t) s += counts[(size_t)t * RADIX + threadIdx.x];
+  part[blockIdx.x * RADIX + threadIdx.x] = s;
+}
+// ...block d scans digit d's partial sums over the row blocks (exclusive) and
+// stores the digit total...
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *tot) {
+  __shared__ uint32_t wsum[RADIX / 64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(inc, off);
+    if ((int)lane >= off) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, all = 0;
+  for (uint32_t k = 0; k < RADIX / 64; ++k) {
+    pre += k < w ? wsum[k] : 0u;
+    all += wsum[k];
+  }
+  __syncthreads();
+  *tot = all;
+  return pre + inc - v;
+}
+__global__ void __launch_bounds__(RADIX) k_col_digit(uint32_t *__restrict__ part, uint32_t nb,
+                                                     uint32_t *__restrict__ dtot) {
+  const uint32_t d = blockIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += RADIX) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t v = b < nb ? part[(size_t)b * RADIX + d] : 0u;
+    uint32_t tot;
+    const uint32_t e = block_excl_scan256(v, &tot);
+    if (b < nb) part[(size_t)b * RADIX + d] = carry + e;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) dtot[d] = carry;
+}
+// ...and every block rewrites its rows with running offsets (in place).
+// (the digit base -- keys of all smaller digits -- is re-derived per block
+// from the 256 digit totals)
+__global__ void __launch_bounds__(RADIX) k_col_final(uint32_t *__restrict__ counts, uint32_t tiles,
+                                                     const uint32_t *__restrict__ part,
+                                                     const uint32_t *__restrict__ dtot) {
+  const uint32_t t0 = blockIdx.x * ROWS, t1 = min(t0 + ROWS, tiles);
+  uint32_t all;
+  const uint32_t base = block_excl_scan256(dtot[threadIdx.x], &all);
+  uint32_t run = base + part[blockIdx.x * RADIX + threadIdx.x];
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t c = counts[(size_t)t * RADIX + threadIdx.x];
+    counts[(size_t)t * RADIX + threadIdx.x] = run;
+    run += c;
+  }
 }
 
 // Workgroups are dispatched round-robin over the 8 XCDs: block b takes the
@@ -158,7 +222,7 @@ __global__ void __launch_bounds__(T) k_digit_scatter(const uint32_t *__restrict_
   for (uint32_t j = threadIdx.x; j < cnt; j += T) {
     const uint32_t k = sk[j];
     const uint32_t d = (k >> shift) & (RADIX - 1);
-    const uint32_t gpos = offs[d * tiles + tile] + (j - lbase[d]);
+    const uint32_t gpos = offs[(size_t)tile * RADIX + d] + (j - lbase[d]);
     key_out[gpos] = k;
     val_out[gpos] = sv[j];
   }
@@ -176,7 +240,12 @@ void launch_pass(const uint32_t *ki, const uint32_t *vi, uint32_t n, int shift, 
   kt_begin(st);
   k_digit_hist<T, I><<<tiles, T, 0, st>>>(ki, n, shift, tiles, counts);
   kt_end(st, KID_HIST, 4.0 * n);  // keys read once
-  exclusive_scan_u32(counts, counts, (size_t)tiles * RADIX, ss, st);
+  const uint32_t nb = (tiles + ROWS - 1) / ROWS;
+  uint32_t *part = ss.block_sums;  // nb * 256 words
+  uint32_t *dtot = part + (size_t)nb * RADIX;
+  k_col_partial<<<nb, RADIX, 0, st>>>(counts, tiles, part);
+  k_col_digit<<<RADIX, RADIX, 0, st>>>(part, nb, dtot);
+  k_col_final<<<nb, RADIX, 0, st>>>(counts, tiles, part, dtot);
   kt_begin(st);
   k_digit_scatter<T, I><<<tiles, T, 0, st>>>(ki, vi, n, shift, tiles, counts, ko, vo);
   kt_end(st, KID_SCATTER, (vi ? 16.0 : 12.0) * n);  // key (+value) read, key+value written
@@ -189,7 +258,8 @@ thread_local KernelTimer *g_ktimer = nullptr;
 size_t radix_scratch_words(uint32_t n) {
   const size_t tiles = (n + RTILE - 1) / RTILE;
   const size_t cnt = tiles * RADIX + 1;
-  return ((cnt + 3) & ~(size_t)3) + scan_blocks(cnt) + 64;
+  const size_t part = ((tiles + ROWS - 1) / ROWS + 1) * RADIX;  // column-scan partials, totals
+  return ((cnt + 3) & ~(size_t)3) + part + 64;
 }
 
 // Sorts by the low `bits` bits of key.  key_in/val_in are not modified unless
