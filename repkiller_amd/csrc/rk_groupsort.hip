@@ -25,9 +25,11 @@
 //     every element's final slot is its stable rank inside its leaf.
 //
 // Tiers (chosen per group by size): 1..16 members -> one thread per member
-// (insertion sort == stable rank); 17..512 and 513..2048 -> one wavefront per
-// group with the group staged in LDS (12 KB / 45 KB per wave); larger -> the
-// same wavefront code on global memory.
+// (insertion sort == stable rank); 17..64 -> one wavefront per group entirely
+// in registers; 65..512 and 513..2048 -> one wavefront per group with the
+// group staged in LDS (12 KB / 45 KB per wave); larger -> the same wavefront
+// code on global memory.  Segments of <= 64 inside the larger tiers are
+// finished in registers as well.
 // In every tier the result goes to `otag` (member order, group-major).
 #include "rk_internal.h"
 
@@ -129,7 +131,8 @@ __device__ void heap_sort_segment(const View &v, uint32_t f, uint32_t l) {
     v.T[f + last] = v.T[f];
     adjust_heap(v, f, 0, last, vk, vt);
   }
-  for (uint32_t x = f; x < l; ++x) v.B[x] = 2;
+  if (v.B)
+    for (uint32_t x = f; x < l; ++x) v.B[x] = 2;
 }
 
 // position of the r-th (0-based, from bit 0) set bit of m; m has more than r bits
@@ -154,14 +157,17 @@ __device__ __forceinline__ int select_bit(uint64_t m, int r) {
 // each Hoare partition is the stopper matching of wave_partition done with
 // ballots and shuffles.  Leaves (<= 16) get B = 1 at their first element; a
 // depth-exhausted sub-segment is heap-sorted in memory by its first lane.
+// Core on registers (k, t of lane x = element x); returns each lane's final
+// segment [sf, sl) -- a leaf, or a heap-sorted range when `heaped`.  The heap
+// fallback writes the registers to v[f0 ..) and reads them back.
 template <bool GLOBAL>
-__device__ void reg_introsort(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane) {
+__device__ void reg_sort_core(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane,
+                              uint64_t &k, uint32_t &t, int &sf, int &sl, bool &heaped) {
   const int x = (int)lane;
   const bool in = x < (int)n;
-  uint64_t k = in ? v.K[f0 + x] : ~0ull;
-  uint32_t t = in ? v.T[f0 + x] : 0u;
-  int sf = 0, sl = (int)n, sd = d0;
-  bool heaped = false;
+  sf = 0, sl = (int)n;
+  int sd = d0;
+  heaped = false;
   const uint64_t below = (1ull << x) - 1ull, above = ~below & ~(1ull << x);
   for (;;) {
     bool active = in && !heaped && sl - sf > THRESH;
@@ -232,6 +238,17 @@ __device__ void reg_introsort(const View &v, uint32_t f0, uint32_t n, int d0, ui
       --sd;
     }
   }
+}
+
+template <bool GLOBAL>
+__device__ void reg_introsort(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane) {
+  const int x = (int)lane;
+  const bool in = x < (int)n;
+  uint64_t k = in ? v.K[f0 + x] : ~0ull;
+  uint32_t t = in ? v.T[f0 + x] : 0u;
+  int sf, sl;
+  bool heaped;
+  reg_sort_core<GLOBAL>(v, f0, n, d0, lane, k, t, sf, sl, heaped);
   if (in) {
     v.K[f0 + x] = k;
     v.T[f0 + x] = t;
@@ -356,6 +373,36 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
   }
 }
 
+// Register tier: one wavefront per group of 17..64 members, no LDS.  The
+// group lives in registers (lane x = member x), the introsort runs there and
+// __final_insertion_sort is the stable rank inside each leaf (<= 16 lanes,
+// by shuffles); heap-sorted ranges are already in order.
+__global__ void __launch_bounds__(256) k_sort_groups_reg(const uint32_t *list, uint32_t nlist,
+                                                         const uint32_t *goff, uint64_t *key,
+                                                         uint32_t *tag, uint32_t *otag) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nlist;
+       w += (gridDim.x * blockDim.x) >> 6) {
+    const uint32_t g = list[w];
+    const uint32_t b = goff[g], n = goff[g + 1] - b;
+    const bool in = lane < n;
+    uint64_t k = in ? key[b + lane] : ~0ull;
+    uint32_t t = in ? tag[b + lane] : 0u;
+    const View v{key + b, tag + b, nullptr, nullptr, nullptr};
+    int sf, sl;
+    bool heaped;
+    reg_sort_core<true>(v, 0, n, 2 * (31 - __clz((int)n)), lane, k, t, sf, sl, heaped);
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < THRESH; ++j) {
+      const int y = sf + j;
+      const uint64_t ky = __shfl(k, y < 64 ? y : 63);
+      r += (y < sl) && (ky < k || (ky == k && y < (int)lane));
+    }
+    if (in) otag[b + (heaped ? lane : sf + r)] = t;
+  }
+}
+
 // LDS tier: one wavefront (block of 64) per group of 17..cap members
 __global__ void __launch_bounds__(64) k_sort_groups_lds(const uint32_t *list, uint32_t nlist,
                                                         const uint32_t *goff, const uint64_t *key,
@@ -424,31 +471,32 @@ __global__ void k_sort_small(const uint32_t *gid_sorted, const uint32_t *goff, u
   }
 }
 
-// flags for the tier lists: 1 = LDS tier, 2 = global tier
-// (members per tier -> tcount[0..3] for the timing accounts; one atomic per
+// tier flags per group: 0 = 1..16 members (k_sort_small), 1 = 17..64
+// (registers), 2 = ..cap (LDS), 3 = ..cap2 (LDS), 4 = larger (global memory);
+// members per tier -> tcount[0..4] for the timing accounts (one atomic per
 // block and tier, grid <= 1024 blocks)
+constexpr int NTIER = 5;
 __global__ void __launch_bounds__(256) k_tier_flags(const uint32_t *goff, uint32_t ngroups,
-                                                    uint32_t cap, uint32_t cap2, uint32_t *f1,
-                                                    uint32_t *f2, uint32_t *f3, uint32_t *tcount) {
-  uint32_t c[4] = {0, 0, 0, 0};
+                                                    uint32_t cap, uint32_t cap2, uint32_t *f,
+                                                    size_t fstride, uint32_t *tcount) {
+  uint32_t c[NTIER] = {0, 0, 0, 0, 0};
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
        g += gridDim.x * blockDim.x) {
     const uint32_t n = goff[g + 1] - goff[g];
-    const int t = n <= (uint32_t)THRESH ? 0 : n <= cap ? 1 : n <= cap2 ? 2 : 3;
-    f1[g] = t == 1;
-    f2[g] = t == 2;
-    f3[g] = t == 3;
+    const int t = n <= (uint32_t)THRESH ? 0 : n <= 64 ? 1 : n <= cap ? 2 : n <= cap2 ? 3 : 4;
+#pragma unroll
+    for (int u = 1; u < NTIER; ++u) f[(u - 1) * fstride + g] = t == u;
     c[t] += n;
   }
-  __shared__ uint32_t part[4][4];
+  __shared__ uint32_t part[NTIER][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < NTIER; ++t) {
     uint32_t v = c[t];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((threadIdx.x & 63) == 0) part[t][threadIdx.x >> 6] = v;
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
+  if (threadIdx.x < NTIER) {
     const uint32_t v = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] +
                        part[threadIdx.x][3];
     if (v) atomicAdd(&tcount[threadIdx.x], v);
@@ -473,7 +521,10 @@ constexpr uint32_t LDS_CAP2 = 2048;  // up to this size: large LDS tier (3 waves
 size_t groupsort_scratch_bytes(uint32_t n) {
   const size_t g1 = (size_t)n + 1;
   const size_t frames = (size_t)n / 8 + 80 * ((size_t)n / (LDS_CAP2 + 1) + 1) + 80;
-  return (size_t)n * 4 * 2 + g1 * 4 * 9 + (size_t)n + 64 + 64 + frames * sizeof(Frame) + 256;
+  // pl, pr; 3 x (NTIER-1) per-group arrays (flags, positions, lists); bounds;
+  // counters; frames
+  return (size_t)n * 4 * 2 + g1 * 4 * 3 * (NTIER - 1) + (size_t)n + 64 + 64 +
+         frames * sizeof(Frame) + 256;
 }
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
@@ -481,52 +532,58 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
                        ScanScratch ss, uint32_t *host_words, hipStream_t st) {
   if (!m) return;
   const size_t g1 = (size_t)ngroups + 1;
+  constexpr int NL = NTIER - 1;  // listed tiers 1..4
   uint32_t *pl = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *pr = pl + m;
-  uint32_t *f1 = pr + m, *f2 = f1 + g1, *f3 = f2 + g1, *p1 = f3 + g1, *p2 = p1 + g1,
-           *p3 = p2 + g1, *l1 = p3 + g1, *l2 = l1 + g1, *l3 = l2 + g1;
-  uint8_t *bnd = reinterpret_cast<uint8_t *>(l3 + g1);
+  uint32_t *fl = pr + m, *ps = fl + NL * g1, *ls = ps + NL * g1;
+  uint8_t *bnd = reinterpret_cast<uint8_t *>(ls + NL * g1);
   uint32_t *tcount = reinterpret_cast<uint32_t *>(
       (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
   Frame *frames = reinterpret_cast<Frame *>(tcount + 16);
-  uint32_t *members = host_words + 4;  // device counters live after the tier flags
+  uint32_t *members = host_words + 8;  // device counters live after the tier counts
   kt_begin(st);
   k_sort_small<<<grid_for(m, 256), 256, 0, st>>>(gid_sorted, goff, m, key, tag, otag);
   kt_end(st, KID_SORT_SMALL, 0.0);  // bytes filled in below from the tier sizes
   const int small_slot = g_ktimer ? g_ktimer->n - 1 : -1;
-  (void)hipMemsetAsync(tcount, 0, 4 * sizeof(uint32_t), st);
-  k_tier_flags<<<grid_for(ngroups, 256, 1024), 256, 0, st>>>(goff, ngroups, LDS_CAP, LDS_CAP2, f1,
-                                                             f2, f3, tcount);
-  uint32_t *fl[3] = {f1, f2, f3}, *ps[3] = {p1, p2, p3}, *ls[3] = {l1, l2, l3};
-  for (int t = 0; t < 3; ++t) {
-    (void)hipMemsetAsync(fl[t] + ngroups, 0, 4, st);
-    exclusive_scan_u32(fl[t], ps[t], g1, ss, st);
-    k_compact<<<grid_for(ngroups, 256), 256, 0, st>>>(fl[t], ps[t], ngroups, ls[t]);
-    (void)hipMemcpyAsync(host_words + t, ps[t] + ngroups, 4, hipMemcpyDeviceToHost, st);
+  (void)hipMemsetAsync(tcount, 0, NTIER * sizeof(uint32_t), st);
+  k_tier_flags<<<grid_for(ngroups, 256, 1024), 256, 0, st>>>(goff, ngroups, LDS_CAP, LDS_CAP2, fl,
+                                                             g1, tcount);
+  for (int t = 0; t < NL; ++t) {
+    uint32_t *f = fl + t * g1, *p = ps + t * g1, *l = ls + t * g1;
+    (void)hipMemsetAsync(f + ngroups, 0, 4, st);
+    exclusive_scan_u32(f, p, g1, ss, st);
+    k_compact<<<grid_for(ngroups, 256), 256, 0, st>>>(f, p, ngroups, l);
+    (void)hipMemcpyAsync(host_words + t, p + ngroups, 4, hipMemcpyDeviceToHost, st);
   }
-  (void)hipMemcpyAsync(members, tcount, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+  (void)hipMemcpyAsync(members, tcount, NTIER * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
-  const uint32_t n1 = host_words[0], n2 = host_words[1], n3 = host_words[2];
+  const uint32_t n1 = host_words[0], n2 = host_words[1], n3 = host_words[2], n4 = host_words[3];
+  uint32_t *l1 = ls, *l2 = ls + g1, *l3 = ls + 2 * g1, *l4 = ls + 3 * g1;
   // algorithmic bytes of every tier: each member's (key, tag) read, its tag
   // written once at its final slot
   if (small_slot >= 0) g_ktimer->bytes[small_slot] = 16.0 * members[0];
   if (n1) {
     kt_begin(st);
-    k_sort_groups_lds<<<n1 < 16384 ? n1 : 16384, 64, lds_bytes(LDS_CAP), st>>>(
-        l1, n1, goff, key, tag, otag, LDS_CAP);
-    kt_end(st, KID_SORT_LDS, 16.0 * members[1]);
+    k_sort_groups_reg<<<grid_for(n1, 4, 16384), 256, 0, st>>>(l1, n1, goff, key, tag, otag);
+    kt_end(st, KID_SORT_REG, 16.0 * members[1]);
   }
   if (n2) {
     kt_begin(st);
-    k_sort_groups_lds<<<n2 < 2048 ? n2 : 2048, 64, lds_bytes(LDS_CAP2), st>>>(
-        l2, n2, goff, key, tag, otag, LDS_CAP2);
+    k_sort_groups_lds<<<n2 < 16384 ? n2 : 16384, 64, lds_bytes(LDS_CAP), st>>>(
+        l2, n2, goff, key, tag, otag, LDS_CAP);
     kt_end(st, KID_SORT_LDS, 16.0 * members[2]);
   }
   if (n3) {
     kt_begin(st);
-    k_sort_groups_global<<<n3 < 1024 ? n3 : 1024, 64, 0, st>>>(l3, n3, goff, key, tag, otag, pl,
+    k_sort_groups_lds<<<n3 < 2048 ? n3 : 2048, 64, lds_bytes(LDS_CAP2), st>>>(
+        l3, n3, goff, key, tag, otag, LDS_CAP2);
+    kt_end(st, KID_SORT_LDS, 16.0 * members[3]);
+  }
+  if (n4) {
+    kt_begin(st);
+    k_sort_groups_global<<<n4 < 1024 ? n4 : 1024, 64, 0, st>>>(l4, n4, goff, key, tag, otag, pl,
                                                                pr, bnd, frames);
-    kt_end(st, KID_SORT_GLOBAL, 16.0 * members[3]);
+    kt_end(st, KID_SORT_GLOBAL, 16.0 * members[4]);
   }
 }
 

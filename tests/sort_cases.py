@@ -78,6 +78,6 @@ def sort_cases():
         cases.append(rng.integers(0, 1 << 40, n).astype(np.uint64))  # distinct
     cases.append(np.zeros(300, np.uint64))
     cases.append(np.arange(400, dtype=np.uint64)[::-1].copy())
-    for n in (100, 512, 1000, 3000):  # depth-limit heapsort fallback
+    for n in (40, 64, 100, 512, 1000, 3000):  # depth-limit heapsort fallback
         cases.append(mcilroy_killer(n))
     return cases
