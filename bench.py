@@ -46,6 +46,10 @@ CONFIGS = {
                  desc="cfg2: 1M fragments, 100 Mbp x 100 Mbp"),
     "cfg3": dict(n=50_000_000, genome_len=3_000_000_000,
                  desc="cfg3: 50M fragments, 3 Gbp human-scale self-comparison"),
+    # BASELINE.json configs[3] is quoted for 8 GPUs; its 200M fragments also fit
+    # one MI355X (~62 GB of HBM), so it runs here as a single-GPU stress case
+    "cfg4": dict(n=200_000_000, genome_len=3_000_000_000,
+                 desc="cfg4: 200M fragments, 3 Gbp x 3 Gbp"),
 }
 
 
