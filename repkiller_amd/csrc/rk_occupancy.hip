@@ -373,6 +373,11 @@ __global__ void __launch_bounds__(256) k_sweep_tile(Axis ax, uint8_t *wpend, uin
 }
 
 // 64 bits of a 128-bit window mask starting at bit a (0 <= a < 128)
+// m << a as a 128-bit window mask (0 <= a < 128)
+__device__ __forceinline__ M128 shl128(uint64_t m, int a) {
+  if (a >= 64) return M128{0, m << (a - 64)};
+  return M128{m << a, a ? m >> (64 - a) : 0};
+}
 __device__ __forceinline__ uint64_t bits_from(uint64_t lo, uint64_t hi, int a) {
   if (a >= 64) return hi >> (a - 64);
   return a ? (lo >> a) | (hi << (64 - a)) : lo;
@@ -569,6 +574,14 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_
         foreign_scan32(ax, g0, dir, k + dir, i, q, fs[s]);
       }
     }
+    // all candidates of a slot as one mask in window positions, so a round
+    // is two ANDs per ballot word
+    M128 cm[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const M128 o = shl128(rown[s], rs[s]), q = shl128(rnb[s], nbs[s]);
+      cm[s] = M128{o.lo | q.lo, o.hi | q.hi};
+    }
     // rounds of ballots: a matching ACTIVE candidate means a hit; a matching
     // UNKNOWN one blocks the final decision (it may still become ACTIVE and win)
     uint64_t A0, A1;
@@ -581,12 +594,8 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
-        const bool has_act = (bits_from(A0, A1, rs[s]) & rown[s]) != 0 ||
-                             (rnb[s] && (bits_from(A0, A1, nbs[s]) & rnb[s]) != 0) ||
-                             fs[s].any_active;
-        const bool has_unk = (bits_from(U0, U1, rs[s]) & rown[s]) != 0 ||
-                             (rnb[s] && (bits_from(U0, U1, nbs[s]) & rnb[s]) != 0) ||
-                             fs[s].any_unknown;
+        const bool has_act = ((A0 & cm[s].lo) | (A1 & cm[s].hi)) != 0 || fs[s].any_active;
+        const bool has_unk = ((U0 & cm[s].lo) | (U1 & cm[s].hi)) != 0 || fs[s].any_unknown;
         if (st[s] == ST_UNKNOWN) {
           if (has_act) st[s] = ST_HIT_PENDING, changed = true;
           else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
