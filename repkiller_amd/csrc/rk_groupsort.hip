@@ -257,6 +257,32 @@ __device__ void reg_introsort(const View &v, uint32_t f0, uint32_t n, int d0, ui
   sync_mem<GLOBAL>();
 }
 
+// reg_introsort plus __final_insertion_sort for the segment: the stable rank
+// inside every leaf (<= 16 lanes) by shuffles, tags written straight to
+// out[f0 ..) and the positions marked B = 3 (finished)
+template <bool GLOBAL>
+__device__ void reg_introsort_final(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane,
+                                    uint32_t *out) {
+  const int x = (int)lane;
+  const bool in = x < (int)n;
+  uint64_t k = in ? v.K[f0 + x] : ~0ull;
+  uint32_t t = in ? v.T[f0 + x] : 0u;
+  int sf, sl;
+  bool heaped;
+  reg_sort_core<GLOBAL>(v, f0, n, d0, lane, k, t, sf, sl, heaped);
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < THRESH; ++j) {
+    const int y = sf + j;
+    const uint64_t ky = __shfl(k, y < 64 ? y : 63);
+    r += (y < sl) && (ky < k || (ky == k && y < x));
+  }
+  if (in) {
+    out[f0 + (heaped ? x : sf + (int)r)] = t;
+    v.B[f0 + x] = 3;
+  }
+}
+
 // wavefront-parallel __unguarded_partition_pivot on [f, l); returns the cut
 template <bool GLOBAL>
 __device__ uint32_t wave_partition(const View &v, uint32_t f, uint32_t l, uint32_t lane) {
@@ -349,12 +375,14 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
   }
   for (int q = 0; q < nsmall; ++q) {
     const Frame fr = smallq[q];
-    reg_introsort<GLOBAL>(v, fr.f, fr.l - fr.f, fr.d, lane);
+    reg_introsort_final<GLOBAL>(v, fr.f, fr.l - fr.f, fr.d, lane, out);
   }
   for (int q = (int)lane; q < nheap; q += 64) heap_sort_segment(v, heapq[q].f, heapq[q].l);
   sync_mem<GLOBAL>();
-  // __final_insertion_sort == stable sort inside every leaf
+  // __final_insertion_sort == stable sort inside every leaf (segments
+  // finished in registers are already written, B == 3)
   for (uint32_t x = lane; x < n; x += 64) {
+    if (v.B[x] == 3) continue;
     if (v.B[x] == 2) {
       out[x] = v.T[x];
       continue;
