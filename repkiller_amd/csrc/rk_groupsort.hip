@@ -150,34 +150,30 @@ __device__ __forceinline__ int select_bit(uint64_t m, int r) {
   return pos;
 }
 
-// __introsort_loop on a segment [f0, f0+n) of at most 64 elements, in
-// registers: lane x holds element f0+x.  Partitions of disjoint sub-segments
-// are independent, so every sub-segment of one recursion level is partitioned
-// at once (each keeps its own depth budget, as in the sequential recursion);
-// each Hoare partition is the stopper matching of wave_partition done with
-// ballots and shuffles.  Leaves (<= 16) get B = 1 at their first element; a
-// depth-exhausted sub-segment is heap-sorted in memory by its first lane.
-// Core on registers (k, t of lane x = element x); returns each lane's final
-// segment [sf, sl) -- a leaf, or a heap-sorted range when `heaped`.  The heap
-// fallback writes the registers to v[f0 ..) and reads them back.
-template <bool GLOBAL>
-__device__ void reg_sort_core(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane,
-                              uint64_t &k, uint32_t &t, int &sf, int &sl, bool &heaped) {
+// __introsort_loop on segments of at most 64 elements, in registers (lane x
+// holds one element).  Partitions of disjoint sub-segments are independent,
+// so every sub-segment of one recursion level is partitioned at once (each
+// keeps its own depth budget, as in the sequential recursion); each Hoare
+// partition is the stopper matching of wave_partition done with ballots and
+// shuffles.  Each lane ends with its final segment [sf, sl) (lane indices) --
+// a leaf, or a heap-sorted range when `heaped`: a depth-exhausted sub-segment
+// is written to memory (lane x at mpos), heap-sorted there by its first lane
+// and read back.
+template <bool GLOBAL, class KT>
+__device__ void reg_sort_core(const View &v, bool in, uint32_t mpos, int &sf, int &sl, int sd,
+                              uint32_t lane, KT &k, uint32_t &t, bool &heaped) {
   const int x = (int)lane;
-  const bool in = x < (int)n;
-  sf = 0, sl = (int)n;
-  int sd = d0;
   heaped = false;
   const uint64_t below = (1ull << x) - 1ull, above = ~below & ~(1ull << x);
   for (;;) {
     bool active = in && !heaped && sl - sf > THRESH;
     const bool need_heap = active && sd == 0;
     if (__ballot(need_heap)) {  // rare: heap fallback in memory
-      if (in) v.K[f0 + x] = k, v.T[f0 + x] = t;
+      if (in) v.K[mpos] = k, v.T[mpos] = t;
       sync_mem<GLOBAL>();
-      if (need_heap && x == sf) heap_sort_segment(v, f0 + sf, f0 + sl);
+      if (need_heap && x == sf) heap_sort_segment(v, mpos, mpos + (sl - sf));
       sync_mem<GLOBAL>();
-      if (in) k = v.K[f0 + x], t = v.T[f0 + x];
+      if (in) k = (KT)v.K[mpos], t = v.T[mpos];
       heaped |= need_heap;
       active &= !need_heap;
     }
@@ -185,7 +181,7 @@ __device__ void reg_sort_core(const View &v, uint32_t f0, uint32_t n, int d0, ui
     const int len = sl - sf;
     // __move_median_to_first(f, f+1, mid, l-1)
     const int a = active ? sf + 1 : x, b = active ? sf + len / 2 : x, c = active ? sl - 1 : x;
-    const uint64_t ka = __shfl(k, a), kb = __shfl(k, b), kc = __shfl(k, c);
+    const KT ka = __shfl(k, a), kb = __shfl(k, b), kc = __shfl(k, c);
     int med;
     if (ka < kb) med = kb < kc ? b : (ka < kc ? c : a);
     else med = ka < kc ? a : (kb < kc ? c : b);
@@ -193,7 +189,7 @@ __device__ void reg_sort_core(const View &v, uint32_t f0, uint32_t n, int d0, ui
     if (active) src = x == sf ? med : (x == med ? sf : x);
     k = __shfl(k, src);
     t = __shfl(t, src);
-    const uint64_t p = __shfl(k, active ? sf : x);
+    const KT p = __shfl(k, active ? sf : x);
     // stoppers of __unguarded_partition(f+1, l, f)
     const uint64_t segm = (sl >= 64 ? ~0ull : (1ull << sl) - 1ull) & ~((1ull << sf) - 1ull);
     const bool lf = active && x > sf && !(k < p);
@@ -240,47 +236,44 @@ __device__ void reg_sort_core(const View &v, uint32_t f0, uint32_t n, int d0, ui
   }
 }
 
-template <bool GLOBAL>
-__device__ void reg_introsort(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane) {
+// Lane x of a batch holds one element of one of up to three small segments
+// packed side by side (segment j in lanes [bl, bl + len), memory [bm, bm +
+// len), depth budget d).  Keys below 2^32 in the whole batch run the core on
+// 32-bit registers (half the shuffle traffic).  The final order -- stable
+// leaf ranks, or heap-sorted ranges in place -- is written to out[] and the
+// positions are marked B = 3.
+template <bool GLOBAL, class KT>
+__device__ void reg_finish(const View &v, bool in, int bl, uint32_t bm, int len, int d,
+                           uint32_t lane, uint64_t k64, uint32_t t, uint32_t *out) {
   const int x = (int)lane;
-  const bool in = x < (int)n;
-  uint64_t k = in ? v.K[f0 + x] : ~0ull;
-  uint32_t t = in ? v.T[f0 + x] : 0u;
-  int sf, sl;
+  KT k = in ? (KT)k64 : (KT)~(KT)0;
+  int sf = in ? bl : x, sl = in ? bl + len : x + 1;
   bool heaped;
-  reg_sort_core<GLOBAL>(v, f0, n, d0, lane, k, t, sf, sl, heaped);
-  if (in) {
-    v.K[f0 + x] = k;
-    v.T[f0 + x] = t;
-    if (!heaped && x == sf) v.B[f0 + x] = 1;
-  }
-  sync_mem<GLOBAL>();
-}
-
-// reg_introsort plus __final_insertion_sort for the segment: the stable rank
-// inside every leaf (<= 16 lanes) by shuffles, tags written straight to
-// out[f0 ..) and the positions marked B = 3 (finished)
-template <bool GLOBAL>
-__device__ void reg_introsort_final(const View &v, uint32_t f0, uint32_t n, int d0, uint32_t lane,
-                                    uint32_t *out) {
-  const int x = (int)lane;
-  const bool in = x < (int)n;
-  uint64_t k = in ? v.K[f0 + x] : ~0ull;
-  uint32_t t = in ? v.T[f0 + x] : 0u;
-  int sf, sl;
-  bool heaped;
-  reg_sort_core<GLOBAL>(v, f0, n, d0, lane, k, t, sf, sl, heaped);
+  const uint32_t mpos = bm + (uint32_t)(x - bl);
+  reg_sort_core<GLOBAL, KT>(v, in, mpos, sf, sl, d, lane, k, t, heaped);
   uint32_t r = 0;
 #pragma unroll
   for (int j = 0; j < THRESH; ++j) {
     const int y = sf + j;
-    const uint64_t ky = __shfl(k, y < 64 ? y : 63);
+    const KT ky = __shfl(k, y < 64 ? y : 63);
     r += (y < sl) && (ky < k || (ky == k && y < x));
   }
   if (in) {
-    out[f0 + (heaped ? x : sf + (int)r)] = t;
-    v.B[f0 + x] = 3;
+    out[heaped ? mpos : bm + (uint32_t)(sf - bl) + r] = t;
+    if (v.B) v.B[mpos] = 3;
   }
+}
+
+template <bool GLOBAL>
+__device__ void reg_batch(const View &v, bool in, int bl, uint32_t bm, int len, int d,
+                          uint32_t lane, uint32_t *out) {
+  const uint32_t mpos = bm + (uint32_t)((int)lane - bl);
+  const uint64_t k = in ? v.K[mpos] : ~0ull;
+  const uint32_t t = in ? v.T[mpos] : 0u;
+  if (__ballot(in && (k >> 32) != 0))
+    reg_finish<GLOBAL, uint64_t>(v, in, bl, bm, len, d, lane, k, t, out);
+  else
+    reg_finish<GLOBAL, uint32_t>(v, in, bl, bm, len, d, lane, k, t, out);
 }
 
 // wavefront-parallel __unguarded_partition_pivot on [f, l); returns the cut
@@ -358,7 +351,7 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
         final_leaf = false;
         break;
       }
-      if (l - f <= 64) {  // small: finished in registers (reg_introsort)
+      if (l - f <= 64) {  // small: finished in registers (reg_batch)
         if (lane == 0) smallq[nsmall] = {f, l, d};
         ++nsmall;
         final_leaf = false;
@@ -373,10 +366,19 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
     if (final_leaf && lane == 0) v.B[f] = 1;
     sync_mem<GLOBAL>();
   }
-  for (int q = 0; q < nsmall; ++q) {
-    const Frame fr = smallq[q];
-    reg_introsort_final<GLOBAL>(v, fr.f, fr.l - fr.f, fr.d, lane, out);
+  // small segments, packed up to three per 64-lane batch
+  for (int q0 = 0; q0 < nsmall;) {
+    int tot = 0, q1 = q0;
+    while (q1 < nsmall && tot + (int)(smallq[q1].l - smallq[q1].f) <= 64)
+      tot += (int)(smallq[q1].l - smallq[q1].f), ++q1;
+    int bl = 0, j = q0;
+    while (j + 1 < q1 && (int)lane >= bl + (int)(smallq[j].l - smallq[j].f))
+      bl += (int)(smallq[j].l - smallq[j].f), ++j;
+    const Frame fr = smallq[j];
+    reg_batch<GLOBAL>(v, (int)lane < tot, bl, fr.f, (int)(fr.l - fr.f), fr.d, lane, out);
+    q0 = q1;
   }
+  sync_mem<GLOBAL>();
   for (int q = (int)lane; q < nheap; q += 64) heap_sort_segment(v, heapq[q].f, heapq[q].l);
   sync_mem<GLOBAL>();
   // __final_insertion_sort == stable sort inside every leaf (segments
@@ -413,21 +415,8 @@ __global__ void __launch_bounds__(256) k_sort_groups_reg(const uint32_t *list, u
        w += (gridDim.x * blockDim.x) >> 6) {
     const uint32_t g = list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
-    const bool in = lane < n;
-    uint64_t k = in ? key[b + lane] : ~0ull;
-    uint32_t t = in ? tag[b + lane] : 0u;
     const View v{key + b, tag + b, nullptr, nullptr, nullptr};
-    int sf, sl;
-    bool heaped;
-    reg_sort_core<true>(v, 0, n, 2 * (31 - __clz((int)n)), lane, k, t, sf, sl, heaped);
-    uint32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < THRESH; ++j) {
-      const int y = sf + j;
-      const uint64_t ky = __shfl(k, y < 64 ? y : 63);
-      r += (y < sl) && (ky < k || (ky == k && y < (int)lane));
-    }
-    if (in) otag[b + (heaped ? lane : sf + r)] = t;
+    reg_batch<true>(v, lane < n, 0, 0, (int)n, 2 * (31 - __clz((int)n)), lane, otag + b);
   }
 }
 
