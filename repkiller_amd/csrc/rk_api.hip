@@ -1,8 +1,10 @@
 // rk_api.hip -- C ABI (include/repkiller_amd.h) and the device pipeline driver.
 //
-// One rk_ctx = one device + one HIP stream + one grow-only workspace in HBM,
+// One rk_ctx = one device + two HIP streams + one grow-only workspace in HBM,
 // mirroring the reference's one-private-state-per-worker model
-// (repkiller.cpp:60-72).  rk_classify_device runs, all on the context stream:
+// (repkiller.cpp:60-72).  rk_classify_device runs, on the context stream
+// (the Y-axis sort and the in-group sort keys on the second stream, overlapped
+// with the X sweeps):
 //
 //   1 prep_keys        xStart/10 keys, last-bucket drop, probe validation
 //   2 counting_sort    -> processing order (stable bucket order of FragmentsDatabase)
@@ -28,7 +30,9 @@
 struct rk_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;             // Y-axis sort, overlapped with the X sweeps
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   void *ws = nullptr;  // device workspace
   size_t ws_cap = 0;
   uint32_t *host = nullptr;  // pinned readback words
@@ -98,8 +102,8 @@ struct Plan {
 
 struct Work {
   uint32_t *ctrl;  // [0] err bits, [1] kept rows, [2..7] counters
-  uint32_t *pkey_in, *tk, *tv;
-  uint32_t *radix;
+  uint32_t *pkey_in, *tk, *tv, *tk2, *tv2;
+  uint32_t *radix, *radix2;
   size_t radix_words;
   rk::Proc p;
   rk::Csr cx, cy;
@@ -118,8 +122,11 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.pkey_in = c.take<uint32_t>(n);
   w.tk = c.take<uint32_t>(n);
   w.tv = c.take<uint32_t>(n);
+  w.tk2 = c.take<uint32_t>(n);
+  w.tv2 = c.take<uint32_t>(n);
   w.radix_words = rk::radix_scratch_words((uint32_t)n);
   w.radix = c.take<uint32_t>(w.radix_words);
+  w.radix2 = c.take<uint32_t>(w.radix_words);
   w.p.rec = c.take<ulonglong2>(2 * n);
   w.p.ys = c.take<uint64_t>(n);
   w.p.pkey = c.take<uint32_t>(n);
@@ -342,12 +349,18 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   }
   rk::gather_proc(f, w.p, m, pl.nbx, pl.nby, st);
 
-  // 4: the two occupancy axes as bucket runs (stable: processing order inside)
+  // 4: the two occupancy axes as bucket runs (stable: processing order inside).
+  // The Y sort and the in-group sort keys run on the second stream, overlapped
+  // with the X sort and sweeps; the Y fill waits for them.
+  HIPCHK(ctx, hipEventRecord(ctx->fork, st));
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
+  rk::radix_sort_pairs(w.p.keyy, nullptr, w.cy.key, w.cy.ent, w.tk2, w.tv2, m,
+                       rk::bit_length(2ull * pl.nby - 1), w.radix2, w.radix_words, ctx->stream2);
+  rk::sort_keys(w.p, m, ctx->stream2);
+  HIPCHK(ctx, hipEventRecord(ctx->join, ctx->stream2));
   mark(ctx, RK_PH_OCC_CSR);
   rk::radix_sort_pairs(w.p.keyx, nullptr, w.cx.key, w.cx.ent, w.tk, w.tv, m,
                        rk::bit_length(2ull * pl.nbx - 1), w.radix, w.radix_words, st);
-  rk::radix_sort_pairs(w.p.keyy, nullptr, w.cy.key, w.cy.ent, w.tk, w.tv, m,
-                       rk::bit_length(2ull * pl.nby - 1), w.radix, w.radix_words, st);
   rk::csr_fill_x(w.cx, w.p.xrec, m, pl.max_x, st);
   HIPCHK(ctx, hipGetLastError());
 
@@ -360,6 +373,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   // X hits: parent = X winner; X results into the Y records
   rk::x_results(w.cx, w.p.xres, w.p.yrec, w.p.par, m, w.ctrl, st);
   mark(ctx, RK_PH_SWEEP_Y);
+  HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
   rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, pl.max_y, st);
   // X misses: the Y sweeps write parent = Y winner, or itself (new group)
   rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.p.par,
@@ -429,7 +443,10 @@ extern "C" int rk_create(rk_ctx **out, int device) {
   ctx->device = device;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void **)&ctx->host, 256 * sizeof(uint32_t), hipHostMallocDefault) !=
           hipSuccess) {
     rk_destroy(ctx);
@@ -453,6 +470,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (!ctx) return;
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->io) (void)hipFree(ctx->io);
   if (ctx->host) (void)hipHostFree(ctx->host);
@@ -462,6 +480,9 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto &e : ctx->kt.ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+  if (ctx->join) (void)hipEventDestroy(ctx->join);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -528,6 +549,8 @@ extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const
     rc = RK_E_INTERNAL;
   }
   rk::g_ktimer = nullptr;  // never leave the kernel timer pointing at this context
+  // an early error return may leave the second stream's work in flight
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   return rc;
 }
 

@@ -256,6 +256,9 @@ void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby,
   kt_begin(st);
   k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(p, m, nbx, nby);
   kt_end(st, KID_GATHER, 84.0 * m);  // row + record in; ys, xrec, yrec, keyx, keyy out
+}
+void sort_keys(Proc p, uint32_t m, hipStream_t st) {
+  if (!m) return;
   kt_begin(st);
   k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m);
   kt_end(st, KID_SORT_KEYS, 20.0 * m);  // key + yStart in, sort key out

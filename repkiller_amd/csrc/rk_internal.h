@@ -171,6 +171,8 @@ __device__ __forceinline__ int neighbour_dir(uint64_t c, uint64_t max_index) {
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
                ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st);
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
+// in-group sort key |yStart - diag_func[xStart/10]| per fragment (p.ha)
+void sort_keys(Proc p, uint32_t m, hipStream_t st);
 // X axis in CSR order: centre/length (+ packed record, neighbour code), state UNKNOWN
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st);
 // X results (X-CSR order, i.e. nearly processing order): into the Y records,
