@@ -57,7 +57,7 @@ namespace rk {
 const char *const kKernelNames[KID_COUNT] = {
     "k_prep_keys",     "k_digit_hist",      "k_digit_scatter", "k_gather_proc",
     "k_sort_keys",     "k_csr_fill_x",      "k_run_bounds",    "k_sweep_tile",
-    "k_sweep_fast",    "k_sweep_wave",    "k_x_results",       "k_merge_xres",    "k_csr_fill_y",    "k_jump",
+    "k_sweep_fast",    "k_sweep_fast_more", "k_sweep_wave",    "k_x_results",       "k_merge_xres",    "k_csr_fill_y",    "k_jump",
     "k_assign_gid",    "k_group_offsets",   "k_build_records",
     "k_sort_small",    "k_sort_groups_reg", "k_sort_groups_lds", "k_sort_groups_global",
     "k_emit",

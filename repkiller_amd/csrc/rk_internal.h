@@ -53,7 +53,7 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch
 // DESIGN.md "Kernels and their rooflines").
 enum KernelId : int {
   KID_PREP, KID_HIST, KID_SCATTER, KID_GATHER, KID_SORT_KEYS, KID_CSR_FILL_X, KID_RUN_BOUNDS,
-  KID_SWEEP_TILE, KID_SWEEP_FAST, KID_SWEEP_WAVE, KID_X_RESULTS, KID_MERGE_XRES, KID_CSR_FILL_Y, KID_JUMP,
+  KID_SWEEP_TILE, KID_SWEEP_FAST, KID_SWEEP_MORE, KID_SWEEP_WAVE, KID_X_RESULTS, KID_MERGE_XRES, KID_CSR_FILL_Y, KID_JUMP,
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_COUNT
 };

@@ -454,17 +454,14 @@ __device__ __forceinline__ void foreign_scan32(const Axis &ax, uint32_t g0, int 
   }
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_t *big,
-             uint32_t *nbig) {
-  __shared__ uint2 s_pk[4][132];  // {centre low 32 bits, length}; 4 entries of read padding
-  __shared__ uint32_t s_ent[4][128], s_key[4][128];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t w = blockIdx.x * 4 + wv;
+// One window (64 positions) of the 32-bit sweep; LDS scratch of the calling
+// wavefront in pk / ent / key.  Returns (wave-uniformly) whether the window
+// still owns undecided entries, and records that in wpend[w].
+__device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8_t *wpend,
+                                               uint32_t *big, uint32_t *nbig, uint2 *pk,
+                                               uint32_t *ent, uint32_t *key, int lane) {
   bool pending = false;
-  if (w < nwin && wpend[w]) {
-    uint2 *pk = s_pk[wv];
-    uint32_t *ent = s_ent[wv], *key = s_key[wv];
+  {
     const uint32_t base = w * 64, m = ax.m;
     uint64_t S0, S1;
     // slot-0 records are loaded with the keys (one memory round trip for
@@ -650,8 +647,43 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_
     }
     const bool wp = __ballot(pending) != 0;
     if (lane == 0) wpend[w] = wp;
+    return wp;
   }
-  count_pending(counters, pending);
+}
+
+// first sweep: one wavefront per window
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_t *big,
+             uint32_t *nbig) {
+  __shared__ uint2 s_pk[4][132];  // {centre low 32 bits, length}; 4 entries of read padding
+  __shared__ uint32_t s_ent[4][128], s_key[4][128];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.x * 4 + wv;
+  bool pending = false;
+  if (w < nwin && wpend[w])
+    pending = sweep_window32(ax, w, wpend, big, nbig, s_pk[wv], s_ent[wv], s_key[wv], lane);
+  count_pending(counters, pending && lane == 0);
+}
+
+// later sweeps: one wavefront per 64 windows, which reads their flags with
+// one coalesced load and handles the still-pending ones in turn
+__global__ void __launch_bounds__(256) k_sweep_fast_more(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
+  __shared__ uint2 s_pk[4][132];
+  __shared__ uint32_t s_ent[4][128], s_key[4][128];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x * 4 + wv, w0 = g * 64;
+  bool pending = false;
+  if (w0 < nwin) {
+    uint64_t todo = __ballot(w0 + lane < nwin && wpend[w0 + lane]);
+    while (todo) {
+      const int b = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      wave_sync_lds();  // the previous window's LDS reads are done
+      pending |= sweep_window32(ax, w0 + b, wpend, nullptr, nullptr, s_pk[wv], s_ent[wv],
+                                s_key[wv], lane);
+    }
+  }
+  count_pending(counters, pending && lane == 0);
 }
 
 // ---- one wavefront walks one long run --------------------------------------
@@ -919,12 +951,15 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   // the window flags (their real work is what the first one left open)
   if (rl.nwin) {
     kt_begin(st);
-    if (rl.fast32)
-      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters,
-                                                      first ? rl.big : nullptr, rl.nbig_dev);
+    if (rl.fast32 && first)
+      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters, rl.big,
+                                                      rl.nbig_dev);
+    else if (rl.fast32)
+      k_sweep_fast_more<<<((rl.nwin + 63) / 64 + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin,
+                                                                       counters);
     else
       k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
-    kt_end(st, rl.fast32 ? KID_SWEEP_FAST : KID_SWEEP_TILE,
+    kt_end(st, rl.fast32 ? (first ? KID_SWEEP_FAST : KID_SWEEP_MORE) : KID_SWEEP_TILE,
            first ? (rl.fast32 ? 26.0 : 30.0) * ax.m : (double)rl.nwin);
   }
   if (rl.fast32) {  // the long-run count lives on the device: a fixed grid reads it
