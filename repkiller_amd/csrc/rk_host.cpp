@@ -39,12 +39,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "repkiller_amd.h"
+#include "rk_format.h"
 
 struct rk_db {
   std::vector<uint64_t> x_start, y_start, x_end, y_end, length, score, ident;
@@ -299,23 +301,8 @@ extern "C" int rk_db_view(const rk_db *db, rk_frags_soa *soa, uint64_t *len_x_hd
 
 namespace {
 
-inline char *put_u64(char *o, uint64_t v) {
-  char t[24];
-  int k = 0;
-  do {
-    t[k++] = (char)('0' + v % 10);
-    v /= 10;
-  } while (v);
-  while (k) *o++ = t[--k];
-  return o;
-}
-
-// ostream << float: num_put widens to double and formats "%.*g" with the
-// default precision 6.
-inline char *put_float(char *o, float f) {
-  int w = std::snprintf(o, 40, "%.6g", (double)f);
-  return o + w;
-}
+using rk::put_float;
+using rk::put_u64;
 
 // store_frag (commonFunctions.cpp:101-104)
 inline char *format_row(char *o, const rk_db *db, uint32_t i, uint64_t gid, unsigned rep) {
@@ -351,49 +338,81 @@ inline char *format_row(char *o, const rk_db *db, uint32_t i, uint64_t gid, unsi
 }
 
 int write_csv(const rk_db *db, const char *path, const uint32_t *gid, const uint8_t *rep,
-              const uint32_t *order, uint64_t n_out) {
-  FILE *f = std::fopen(path, "wb");
-  if (!f) return RK_E_IO;
-  bool ok = std::fwrite(db->header.data(), 1, db->header.size(), f) == db->header.size();
+               const uint32_t *order, uint64_t n_out) {
+  const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return RK_E_IO;
   const uint64_t n_rows = db->x_start.size();
-  // format in parallel into per-chunk buffers, write in order
+  // every chunk of rows is formatted into its own buffer in parallel, then
+  // the chunks are written in parallel at their prefix-sum offsets (pwrite)
   const uint64_t chunk = 1u << 16;
   const uint64_t n_chunks = (n_out + chunk - 1) / chunk;
   unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   if (n_out < 4 * chunk) nt = 1;
-  const uint64_t batch = (uint64_t)nt * 4;
-  std::vector<std::string> bufs(batch);
+  // a row is at most 5 + 10 * 21 + 2 * 16 + 4 bytes < 256; the buffers are
+  // not zero-filled (only the formatted bytes are ever touched)
+  std::vector<std::unique_ptr<char[]>> bufs(n_chunks);
+  std::vector<size_t> blen(n_chunks, 0);
   std::atomic<bool> bad{false};
-  for (uint64_t c0 = 0; c0 < n_chunks && ok; c0 += batch) {
-    uint64_t c1 = std::min(n_chunks, c0 + batch);
-    std::atomic<uint64_t> next{c0};
-    auto work = [&]() {
-      for (uint64_t c; (c = next.fetch_add(1)) < c1;) {
-        std::string &s = bufs[c - c0];
-        uint64_t k0 = c * chunk, k1 = std::min(n_out, k0 + chunk);
-        s.resize((size_t)(k1 - k0) * 256);
-        char *o = &s[0];
-        for (uint64_t k = k0; k < k1; ++k) {
-          uint32_t i = order[k];
-          if (i >= n_rows) {
-            bad = true;
-            break;
-          }
-          o = format_row(o, db, i, gid[k], rep[k]);
-        }
-        s.resize((size_t)(o - s.data()));
+  std::atomic<uint64_t> next{0};
+  auto fmt = [&]() {
+    for (uint64_t c; (c = next.fetch_add(1)) < n_chunks;) {
+      const uint64_t k0 = c * chunk, k1 = std::min(n_out, k0 + chunk);
+      bufs[c].reset(new (std::nothrow) char[(size_t)(k1 - k0) * 256]);
+      if (!bufs[c]) {
+        bad = true;
+        break;
       }
-    };
+      char *const b0 = bufs[c].get();
+      char *o = b0;
+      for (uint64_t k = k0; k < k1; ++k) {
+        const uint32_t i = order[k];
+        if (i >= n_rows) {
+          bad = true;
+          break;
+        }
+        o = format_row(o, db, i, gid[k], rep[k]);
+      }
+      blen[c] = (size_t)(o - b0);
+    }
+  };
+  {
     std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; ++t) th.emplace_back(work);
-    work();
+    for (unsigned t = 1; t < nt; ++t) th.emplace_back(fmt);
+    fmt();
     for (auto &t : th) t.join();
-    if (bad) ok = false;
-    for (uint64_t c = c0; c < c1 && ok; ++c)
-      ok = std::fwrite(bufs[c - c0].data(), 1, bufs[c - c0].size(), f) == bufs[c - c0].size();
   }
-  if (std::fclose(f) != 0) ok = false;
-  return ok ? RK_OK : (bad ? RK_E_ARG : RK_E_IO);
+  if (bad) {
+    ::close(fd);
+    return RK_E_ARG;
+  }
+  std::vector<uint64_t> off(n_chunks + 1);
+  off[0] = db->header.size();
+  for (uint64_t c = 0; c < n_chunks; ++c) off[c + 1] = off[c] + blen[c];
+  auto put = [fd](const char *p, size_t len, uint64_t at) {
+    while (len) {
+      const ssize_t w = ::pwrite(fd, p, len, (off_t)at);
+      if (w <= 0) {
+        if (w < 0 && errno == EINTR) continue;
+        return false;
+      }
+      p += w, len -= (size_t)w, at += (uint64_t)w;
+    }
+    return true;
+  };
+  std::atomic<bool> ok{put(db->header.data(), db->header.size(), 0)};
+  next = 0;
+  auto wr = [&]() {
+    for (uint64_t c; (c = next.fetch_add(1)) < n_chunks;)
+      if (!put(bufs[c].get(), blen[c], off[c])) ok = false;
+  };
+  {
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; ++t) th.emplace_back(wr);
+    wr();
+    for (auto &t : th) t.join();
+  }
+  if (::close(fd) != 0) ok = false;
+  return ok ? RK_OK : RK_E_IO;
 }
 
 }  // namespace
