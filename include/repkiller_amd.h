@@ -102,6 +102,18 @@ int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p, rk_resu
 int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params *p,
                        rk_result *out_dev);
 
+/* Several (len_ratio, pos_ratio) pairs over ONE fragment set -- the loop of
+ * repkiller.cpp:60-72, which runs execWithParams (repkiller.cpp:80-97) once
+ * per pair on the same FragmentsDatabase.  The ratio-independent work
+ * (processing order, both occupancy axes, in-group sort keys) is done once;
+ * p[i] / out[i] belong to pair i.  Every p[i] must carry the same
+ * len_x_hdr / len_y_hdr (RK_E_ARG otherwise).  rk_get_stats reports the last
+ * pair; phase profiling covers the shared part and the first pair. */
+int rk_classify_pairs(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p, uint32_t npairs,
+                      rk_result *out);
+int rk_classify_device_pairs(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params *p,
+                             uint32_t npairs, rk_result *out_dev);
+
 int rk_get_stats(const rk_ctx *ctx, rk_stats *st);
 
 /* The in-group ordering primitive on its own: libstdc++ 11 std::sort (the

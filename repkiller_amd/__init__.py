@@ -41,6 +41,7 @@ STATUS = {
 # every symbol include/repkiller_amd.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "rk_create", "rk_destroy", "rk_last_error", "rk_classify", "rk_classify_device",
+    "rk_classify_pairs", "rk_classify_device_pairs",
     "rk_get_stats", "rk_std_sort_segments", "rk_set_profiling", "rk_get_phase_ms", "rk_reset_phases", "rk_phase_name",
     "rk_get_kernel_timing", "rk_kernel_count", "rk_kernel_name",
     "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
@@ -118,6 +119,12 @@ def load_library() -> ctypes.CDLL:
                                        ctypes.POINTER(Result)]),
         "rk_classify_device": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA),
                                               ctypes.POINTER(Params), ctypes.POINTER(Result)]),
+        "rk_classify_pairs": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA),
+                                             ctypes.POINTER(Params), ctypes.c_uint32,
+                                             ctypes.POINTER(Result)]),
+        "rk_classify_device_pairs": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA),
+                                                    ctypes.POINTER(Params), ctypes.c_uint32,
+                                                    ctypes.POINTER(Result)]),
         "rk_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(Stats)]),
         "rk_set_profiling": (ctypes.c_int, [vp, ctypes.c_int]),
         "rk_std_sort_segments": (ctypes.c_int, [vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32,
@@ -376,6 +383,34 @@ class Context:
             raise RkError(rc, self.last_error())
         k = res.n_out
         return ClassifyResult(gid[:k].copy(), rep[:k].copy(), order[:k].copy(), int(res.n_groups))
+
+    def classify_pairs(self, f: Frags, len_x_hdr: int, len_y_hdr: int,
+                       pairs) -> list:
+        """Several (len_ratio, pos_ratio) pairs over one fragment set
+        (rk_classify_pairs; the pair loop of repkiller.cpp:60-72)."""
+        pairs = list(pairs)
+        n, q = f.n, len(pairs)
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+                ((f.x_start, np.uint64), (f.y_start, np.uint64), (f.length, np.uint64),
+                 (f.strand, np.uint8))]
+        soa = FragsSoA(_ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), _ptr(arrs[3]), n)
+        gid = np.empty((q, n), np.uint32)
+        rep = np.empty((q, n), np.uint8)
+        order = np.empty((q, n), np.uint32)
+        res = (Result * max(q, 1))()
+        prm = (Params * max(q, 1))()
+        for i, (lr, pr) in enumerate(pairs):
+            res[i] = Result(_ptr(order[i]), _ptr(gid[i]), _ptr(rep[i]), 0, 0)
+            prm[i] = Params(len_x_hdr, len_y_hdr, lr, pr)
+        rc = load_library().rk_classify_pairs(self._h, ctypes.byref(soa), prm, q, res)
+        if rc != RK_OK:
+            raise RkError(rc, self.last_error())
+        out = []
+        for i in range(q):
+            k = res[i].n_out
+            out.append(ClassifyResult(gid[i, :k].copy(), rep[i, :k].copy(), order[i, :k].copy(),
+                                      int(res[i].n_groups)))
+        return out
 
     def classify_device(self, x, y, length, strand, gid, repval, out_order, len_x_hdr: int,
                         len_y_hdr: int, len_ratio: float = 0.3, pos_ratio: float = 0.3):

@@ -281,19 +281,32 @@ int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss, b
   return RK_OK;
 }
 
-int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, rk_result *out) {
-  if (!ctx || !in || !prm || !out) return RK_E_ARG;
+// All pairs share one fragment set: the ratio-independent part (processing
+// order, the two occupancy axes, the in-group sort keys) is built once, then
+// every (len_ratio, pos_ratio) pair runs the sweeps, groups and in-group order
+// (repkiller.cpp:60-72 runs each pair through the whole path).  Phase
+// profiling covers the shared part and the first pair.
+int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, uint32_t npairs,
+                    rk_result *outs) {
+  if (!ctx || !in || !prms || !outs || npairs == 0) return RK_E_ARG;
   if (in->n >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
-  if (prm->len_ratio <= 0 || prm->pos_ratio <= 0) {  // NaN passes, as in the reference
-    ctx->err = "ratios must be greater than zero (commonFunctions.cpp:26-27)";
-    return RK_E_ARG;
+  for (uint32_t q = 0; q < npairs; ++q) {
+    const rk_params &pq = prms[q];
+    if (pq.len_ratio <= 0 || pq.pos_ratio <= 0) {  // NaN passes, as in the reference
+      ctx->err = "ratios must be greater than zero (commonFunctions.cpp:26-27)";
+      return RK_E_ARG;
+    }
+    if (pq.len_x_hdr != prms[0].len_x_hdr || pq.len_y_hdr != prms[0].len_y_hdr) {
+      ctx->err = "all pairs must describe the same fragment set (header lengths differ)";
+      return RK_E_ARG;
+    }
+    if (in->n && (!outs[q].gid || !outs[q].repval || !outs[q].out_order)) return RK_E_ARG;
   }
-  if (in->n && (!in->x_start || !in->y_start || !in->length || !in->strand || !out->gid ||
-                !out->repval || !out->out_order))
-    return RK_E_ARG;
+  if (in->n && (!in->x_start || !in->y_start || !in->length || !in->strand)) return RK_E_ARG;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   std::memset(&ctx->stats, 0, sizeof ctx->stats);
   hipStream_t st = ctx->stream;
+  const rk_params *prm = &prms[0];
 
   Plan pl{};
   pl.n = in->n;
@@ -331,8 +344,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   const bool fast32 = !(ctx->host[0] & rk::ERRB_WIDE_LENGTH);
   const uint32_t m = ctx->host[1];
   ctx->stats.n_proc = m;
-  out->n_out = m;
-  out->n_groups = 0;
+  for (uint32_t q = 0; q < npairs; ++q) outs[q].n_out = m, outs[q].n_groups = 0;
   if (m == 0) {
     mark(ctx, RK_N_PHASES);
     collect_phases(ctx);
@@ -364,59 +376,70 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prm, r
   rk::csr_fill_x(w.cx, w.p.xrec, m, pl.max_x, st);
   HIPCHK(ctx, hipGetLastError());
 
-  // 5: X, then Y (X hits join the Y lists; X misses query Y)
-  mark(ctx, RK_PH_SWEEP_X);
-  rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, nullptr,
-              w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, prm->len_ratio,
-              prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ax, w, ss, fast32, &ctx->stats.x_sweeps))) return rc;
-  // X hits: parent = X winner; X results into the Y records
-  rk::x_results(w.cx, w.p.xres, w.p.yrec, w.p.par, m, w.ctrl, st);
-  mark(ctx, RK_PH_SWEEP_Y);
-  HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
-  rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, pl.max_y, st);
-  // X misses: the Y sweeps write parent = Y winner, or itself (new group)
-  rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.p.par,
-              w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, prm->len_ratio,
-              prm->pos_ratio};
-  if ((rc = resolve_axis(ctx, ay, w, ss, fast32, &ctx->stats.y_sweeps))) return rc;
+  for (uint32_t q = 0; q < npairs; ++q) {
+    const rk_params &pq = prms[q];
+    rk_result *out = &outs[q];
+    const bool prof = q == 0;
+    if (q > 0) HIPCHK(ctx, hipMemsetAsync(w.cx.state, rk::ST_UNKNOWN, m, st));
 
-  // 6: group roots and ids
-  mark(ctx, RK_PH_ROOTS);
-  HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
-  for (;;) {
-    HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
-    rk::jump_round(w.p, m, w.ctrl + 5, ctx->stats.jump_rounds == 0 ? w.isnew : nullptr, w.ctrl,
-                   st);
-    if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
-    ctx->stats.jump_rounds++;
-    if (!ctx->host[0]) break;
-    if (ctx->stats.jump_rounds > 64) {
-      ctx->err = "pointer jumping did not converge";
-      return RK_E_INTERNAL;
+    // 5: X, then Y (X hits join the Y lists; X misses query Y)
+    if (prof) mark(ctx, RK_PH_SWEEP_X);
+    rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, nullptr,
+                w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
+                pq.pos_ratio};
+    uint32_t sweeps = 0;
+    if ((rc = resolve_axis(ctx, ax, w, ss, fast32, &sweeps))) return rc;
+    ctx->stats.x_sweeps = sweeps;
+    // X hits: parent = X winner; X results into the Y records
+    rk::x_results(w.cx, w.p.xres, w.p.yrec, w.p.par, m, w.ctrl, st);
+    if (prof) mark(ctx, RK_PH_SWEEP_Y);
+    if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
+    rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, pl.max_y, st);
+    // X misses: the Y sweeps write parent = Y winner, or itself (new group)
+    rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.p.par,
+                w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
+                pq.pos_ratio};
+    if ((rc = resolve_axis(ctx, ay, w, ss, fast32, &sweeps))) return rc;
+    ctx->stats.y_sweeps = sweeps;
+
+    // 6: group roots and ids
+    if (prof) mark(ctx, RK_PH_ROOTS);
+    HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
+    uint32_t rounds = 0;
+    for (;;) {
+      HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
+      rk::jump_round(w.p, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st);
+      if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
+      ++rounds;
+      if (!ctx->host[0]) break;
+      if (rounds > 64) {
+        ctx->err = "pointer jumping did not converge";
+        return RK_E_INTERNAL;
+      }
     }
-  }
-  rk::exclusive_scan_u32(w.isnew, w.newrank, (size_t)m + 1, ss, st);
-  if ((rc = readback(ctx, w.newrank + m, 1))) return rc;
-  const uint32_t G = ctx->host[0];
-  out->n_groups = G;
-  ctx->stats.n_groups = G;
-  rk::assign_gid(w.p, m, w.newrank, st);
+    ctx->stats.jump_rounds = rounds;
+    rk::exclusive_scan_u32(w.isnew, w.newrank, (size_t)m + 1, ss, st);
+    if ((rc = readback(ctx, w.newrank + m, 1))) return rc;
+    const uint32_t G = ctx->host[0];
+    out->n_groups = G;
+    ctx->stats.n_groups = G;
+    rk::assign_gid(w.p, m, w.newrank, st);
 
-  // 7-9: members (stable by gid => processing order), in-group order, flags
-  mark(ctx, RK_PH_MEMBERS);
-  rk::radix_sort_pairs(w.p.gid, nullptr, w.sgid, w.gmem, w.tk, w.tv, m,
-                       rk::bit_length(G - 1), w.radix, w.radix_words, st);
-  rk::group_offsets(w.sgid, m, G, w.goff, st);
-  rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
-  mark(ctx, RK_PH_GROUP_SORT);
-  rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
-                        ctx->host + 128, st);
-  mark(ctx, RK_PH_EMIT);
-  rk::emit_result(w.otag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval, out->out_order,
-                  st);
-  HIPCHK(ctx, hipGetLastError());
-  mark(ctx, RK_N_PHASES);
+    // 7-9: members (stable by gid => processing order), in-group order, flags
+    if (prof) mark(ctx, RK_PH_MEMBERS);
+    rk::radix_sort_pairs(w.p.gid, nullptr, w.sgid, w.gmem, w.tk, w.tv, m,
+                         rk::bit_length(G - 1), w.radix, w.radix_words, st);
+    rk::group_offsets(w.sgid, m, G, w.goff, st);
+    rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
+    if (prof) mark(ctx, RK_PH_GROUP_SORT);
+    rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
+                          ctx->host + 128, st);
+    if (prof) mark(ctx, RK_PH_EMIT);
+    rk::emit_result(w.otag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval,
+                    out->out_order, st);
+    HIPCHK(ctx, hipGetLastError());
+    if (prof) mark(ctx, RK_N_PHASES);
+  }
   HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
   if ((rc = readback(ctx, w.ctrl, 1))) return rc;
   collect_phases(ctx);
@@ -537,13 +560,14 @@ extern "C" int rk_get_stats(const rk_ctx *ctx, rk_stats *st) {
   return RK_OK;
 }
 
-extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params *p,
-                                  rk_result *out_dev) {
+extern "C" int rk_classify_device_pairs(rk_ctx *ctx, const rk_frags_soa *in_dev,
+                                        const rk_params *p, uint32_t npairs,
+                                        rk_result *out_dev) {
   if (!ctx) return RK_E_ARG;
   ctx->err.clear();
   int rc;
   try {
-    rc = classify_device(ctx, in_dev, p, out_dev);
+    rc = classify_device(ctx, in_dev, p, npairs, out_dev);
   } catch (...) {
     ctx->err = "unexpected C++ exception";
     rc = RK_E_INTERNAL;
@@ -552,6 +576,11 @@ extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const
   // an early error return may leave the second stream's work in flight
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   return rc;
+}
+
+extern "C" int rk_classify_device(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_params *p,
+                                  rk_result *out_dev) {
+  return rk_classify_device_pairs(ctx, in_dev, p, 1, out_dev);
 }
 
 extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t n,
@@ -598,18 +627,19 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
   return rc;
 }
 
-extern "C" int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p,
-                           rk_result *out) {
-  if (!ctx || !in || !p || !out) return RK_E_ARG;
+extern "C" int rk_classify_pairs(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p,
+                                 uint32_t npairs, rk_result *out) {
+  if (!ctx || !in || !p || !out || npairs == 0) return RK_E_ARG;
   ctx->err.clear();
   const size_t n = in->n;
   if (n >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
-  if (n && (!in->x_start || !in->y_start || !in->length || !in->strand || !out->gid ||
-            !out->repval || !out->out_order))
-    return RK_E_ARG;
+  if (n && (!in->x_start || !in->y_start || !in->length || !in->strand)) return RK_E_ARG;
+  for (uint32_t q = 0; q < npairs; ++q)
+    if (n && (!out[q].gid || !out[q].repval || !out[q].out_order)) return RK_E_ARG;
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  // device staging: x, y, len (u64), strand (u8) in; gid, order (u32), rep (u8) out
-  size_t need = align_up(n * 8 + 16) * 3 + align_up(n + 16) * 2 + align_up(n * 4 + 16) * 2;
+  // device staging: x, y, len (u64), strand (u8) in; per pair gid, order (u32), rep (u8) out
+  size_t need = align_up(n * 8 + 16) * 3 + align_up(n + 16) +
+                (size_t)npairs * (align_up(n + 16) + align_up(n * 4 + 16) * 2);
   if (need > ctx->io_cap) {
     if (ctx->io) (void)hipFree(ctx->io);
     ctx->io = nullptr;
@@ -619,8 +649,13 @@ extern "C" int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params 
   }
   Carve c{(char *)ctx->io};
   uint64_t *dx = c.take<uint64_t>(n), *dy = c.take<uint64_t>(n), *dl = c.take<uint64_t>(n);
-  uint8_t *ds = c.take<uint8_t>(n), *drep = c.take<uint8_t>(n);
-  uint32_t *dgid = c.take<uint32_t>(n), *dord = c.take<uint32_t>(n);
+  uint8_t *ds = c.take<uint8_t>(n);
+  std::vector<rk_result> dres(npairs);
+  for (uint32_t q = 0; q < npairs; ++q) {
+    uint8_t *drep = c.take<uint8_t>(n);
+    uint32_t *dgid = c.take<uint32_t>(n), *dord = c.take<uint32_t>(n);
+    dres[q] = rk_result{dord, dgid, drep, 0, 0};
+  }
   hipStream_t st = ctx->stream;
   if (n) {
     HIPCHK(ctx, hipMemcpyAsync(dx, in->x_start, n * 8, hipMemcpyHostToDevice, st));
@@ -629,18 +664,24 @@ extern "C" int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params 
     HIPCHK(ctx, hipMemcpyAsync(ds, in->strand, n, hipMemcpyHostToDevice, st));
   }
   rk_frags_soa din{dx, dy, dl, ds, n};
-  rk_result dres{dord, dgid, drep, 0, 0};
-  int rc = rk_classify_device(ctx, &din, p, &dres);
+  int rc = rk_classify_device_pairs(ctx, &din, p, npairs, dres.data());
   if (rc) return rc;
-  out->n_out = dres.n_out;
-  out->n_groups = dres.n_groups;
-  if (n) {
-    if (dres.n_out) {
-      HIPCHK(ctx, hipMemcpyAsync(out->out_order, dord, dres.n_out * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(out->gid, dgid, dres.n_out * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(out->repval, drep, dres.n_out, hipMemcpyDeviceToHost, st));
+  for (uint32_t q = 0; q < npairs; ++q) {
+    out[q].n_out = dres[q].n_out;
+    out[q].n_groups = dres[q].n_groups;
+    if (n && dres[q].n_out) {
+      const uint64_t k = dres[q].n_out;
+      HIPCHK(ctx, hipMemcpyAsync(out[q].out_order, dres[q].out_order, k * 4,
+                                 hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(out[q].gid, dres[q].gid, k * 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(out[q].repval, dres[q].repval, k, hipMemcpyDeviceToHost, st));
     }
-    HIPCHK(ctx, hipStreamSynchronize(st));
   }
+  if (n) HIPCHK(ctx, hipStreamSynchronize(st));
   return RK_OK;
+}
+
+extern "C" int rk_classify(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p,
+                           rk_result *out) {
+  return rk_classify_pairs(ctx, in, p, 1, out);
 }

@@ -191,6 +191,50 @@ def test_repeat_calls_same_context(gpu_ctx):
     assert np.array_equal(r1.out_order, r3.out_order)
 
 
+PAIRS = [(0.3, 0.3), (0.05, 0.05), (1.5, 0.7), (0.3, 2.0), (float("nan"), 0.3), (0.3, 0.3)]
+
+
+@pytest.mark.parametrize("n,L,kw", [
+    (200_000, 10_000_000, {}),
+    (50_000, 200_000, dict(family_frac=0.95, copies=(100, 600))),
+])
+def test_classify_pairs_vs_oracle(gpu_ctx, n, L, kw):
+    """rk_classify_pairs: the shared prefix is built once and every pair's
+    result equals the oracle's for that pair alone (repkiller.cpp:60-72)."""
+    f = rk.synth(n, L, seed=23, **kw)
+    got = gpu_ctx.classify_pairs(f, L, L, PAIRS)
+    assert len(got) == len(PAIRS)
+    for (lr, pr), r in zip(PAIRS, got):
+        rc, gid, rep, order, ng = ro.classify(f.x_start, f.y_start, f.length, f.strand, L, L,
+                                              lr, pr)
+        assert rc == 0 and r.n_groups == ng, (lr, pr)
+        assert np.array_equal(r.out_order, order), (lr, pr)
+        assert np.array_equal(r.gid, gid), (lr, pr)
+        assert np.array_equal(r.repval, rep), (lr, pr)
+
+
+def test_classify_pairs_wide_and_errors(gpu_ctx):
+    """Pairs over the 64-bit sweep path; invalid pair lists are rejected whole."""
+    f = rk.synth(20_000, 1_000_000, seed=43)
+    f.length[:25] += np.uint64(2**31)
+    L = 5_000_000_000
+    pairs = [(0.3, 0.3), (2.0, 0.1), (0.01, 3.0)]
+    got = gpu_ctx.classify_pairs(f, L, L, pairs)
+    for (lr, pr), r in zip(pairs, got):
+        want = gpu_ctx.classify(f, L, L, lr, pr)
+        assert r.n_groups == want.n_groups
+        assert np.array_equal(r.out_order, want.out_order)
+        assert np.array_equal(r.repval, want.repval)
+    gpu_vs_oracle(gpu_ctx, f, L, L, 2.0, 0.1)
+    with pytest.raises(rk.RkError):
+        gpu_ctx.classify_pairs(f, L, L, [(0.3, 0.3), (0.0, 0.3)])
+    with pytest.raises(rk.RkError):
+        gpu_ctx.classify_pairs(f, L, L, [])
+    e = rk.Frags(np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint64),
+                 np.zeros(0, np.uint8))
+    assert [r.n_groups for r in gpu_ctx.classify_pairs(e, 100, 100, pairs)] == [0, 0, 0]
+
+
 def test_cli_matches_reference(tmp_path):
     """rk_repkiller (C++ host driver) end to end: CSV in, CSV out, byte-exact."""
     inp, out = tmp_path / "in.csv", tmp_path / "out.csv"
