@@ -368,7 +368,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->fork, 0));
   rk::radix_sort_pairs(w.p.keyy, nullptr, w.cy.key, w.cy.ent, w.tk2, w.tv2, m,
                        rk::bit_length(2ull * pl.nby - 1), w.radix2, w.radix_words, ctx->stream2);
-  rk::sort_keys(w.p, m, ctx->stream2);
+  rk::sort_keys(w.p, m, w.ctrl + 6, ctx->stream2);
   HIPCHK(ctx, hipEventRecord(ctx->join, ctx->stream2));
   mark(ctx, RK_PH_OCC_CSR);
   rk::radix_sort_pairs(w.p.keyx, nullptr, w.cx.key, w.cx.ent, w.tk, w.tv, m,
@@ -409,7 +409,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     for (;;) {
       HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
       rk::jump_round(w.p, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st);
-      if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
+      if ((rc = readback(ctx, w.ctrl + 5, 2))) return rc;  // + the wide-key flag
       ++rounds;
       if (!ctx->host[0]) break;
       if (rounds > 64) {
@@ -418,6 +418,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
       }
     }
     ctx->stats.jump_rounds = rounds;
+    const bool narrow_keys = ctx->host[1] == 0;
     rk::exclusive_scan_u32(w.isnew, w.newrank, (size_t)m + 1, ss, st);
     if ((rc = readback(ctx, w.newrank + m, 1))) return rc;
     const uint32_t G = ctx->host[0];
@@ -433,7 +434,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
     rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
-                          ctx->host + 128, st);
+                          ctx->host + 128, narrow_keys, st);
     if (prof) mark(ctx, RK_PH_EMIT);
     rk::emit_result(w.otag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval,
                     out->out_order, st);
@@ -615,8 +616,10 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
       hipMemcpyAsync(doff, seg_off, (nseg + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
     rc = RK_E_HIP;
   } else {
+    bool narrow = true;
+    for (uint32_t x = 0; x < m; ++x) narrow &= (keys[x] >> 32) == 0;
     rk::sort_groups_exact(dg, doff, nseg, m, dk, dt, dot, dgs, rk::ScanScratch{dsc, sc},
-                          ctx->host + 128, st);
+                          ctx->host + 128, narrow, st);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(perm, dot, m * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)

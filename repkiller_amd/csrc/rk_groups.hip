@@ -92,7 +92,7 @@ __global__ void k_gather_proc(Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
 // of the LAST fragment of processing bucket b, i.e. of the end of k's run of
 // equal processing keys.  Run ends inside the wavefront come from a ballot and
 // a shuffle; only runs that cross the wave's end read further.
-__global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m) {
+__global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m, uint32_t *wide) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; base < m;
        base += gridDim.x * blockDim.x) {
@@ -109,7 +109,9 @@ __global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m) {
       while (e + 1 < m && p.pkey[e + 1] == key) ++e;
       d = p.ys[e];
     }
-    if (in) p.ha[k] = y > d ? y - d : d - y;
+    const uint64_t h = y > d ? y - d : d - y;
+    if (in) p.ha[k] = h;
+    if (__ballot(in && (h >> 32) != 0) && lane == 0) atomicOr(wide, 1u);
   }
 }
 
@@ -257,10 +259,10 @@ void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby,
   k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(p, m, nbx, nby);
   kt_end(st, KID_GATHER, 84.0 * m);  // row + record in; ys, xrec, yrec, keyx, keyy out
 }
-void sort_keys(Proc p, uint32_t m, hipStream_t st) {
+void sort_keys(Proc p, uint32_t m, uint32_t *wide, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m);
+  k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m, wide);
   kt_end(st, KID_SORT_KEYS, 20.0 * m);  // key + yStart in, sort key out
 }
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st) {

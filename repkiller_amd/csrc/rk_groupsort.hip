@@ -57,15 +57,22 @@ __device__ __forceinline__ void sync_mem() {
   else wave_sync();
 }
 
-struct View {
-  uint64_t *K;
+// a group's working arrays: keys, tags, the stopper position lists and leaf
+// marks; the LDS tiers keep 32-bit keys (when every key fits) and 16-bit
+// positions, the global tier 64-bit keys and 32-bit positions
+template <class KT_, class PT_>
+struct ViewT {
+  using key_t = KT_;
+  KT_ *K;
   uint32_t *T;
-  uint32_t *PL, *PR;  // stopper position lists (capacity n)
-  uint8_t *B;         // 1 = leaf start, 2 = inside a heap-sorted segment
+  PT_ *PL, *PR;  // stopper position lists (capacity n)
+  uint8_t *B;    // 1 = leaf start, 2 = inside a heap-sorted segment
 };
+using GView = ViewT<uint64_t, uint32_t>;
 
-__device__ __forceinline__ void vswap(const View &v, uint32_t a, uint32_t b) {
-  const uint64_t k = v.K[a];
+template <class V>
+__device__ __forceinline__ void vswap(const V &v, uint32_t a, uint32_t b) {
+  const typename V::key_t k = v.K[a];
   v.K[a] = v.K[b];
   v.K[b] = k;
   const uint32_t t = v.T[a];
@@ -74,9 +81,10 @@ __device__ __forceinline__ void vswap(const View &v, uint32_t a, uint32_t b) {
 }
 
 // __move_median_to_first(result=f, a=f+1, b=mid, c=l-1)
-__device__ __forceinline__ void median_to_first(const View &v, uint32_t f, uint32_t l) {
+template <class V>
+__device__ __forceinline__ void median_to_first(const V &v, uint32_t f, uint32_t l) {
   const uint32_t a = f + 1, b = f + (l - f) / 2, c = l - 1;
-  const uint64_t ka = v.K[a], kb = v.K[b], kc = v.K[c];
+  const typename V::key_t ka = v.K[a], kb = v.K[b], kc = v.K[c];
   uint32_t m;
   if (ka < kb) m = kb < kc ? b : (ka < kc ? c : a);
   else m = ka < kc ? a : (kb < kc ? c : b);
@@ -84,11 +92,12 @@ __device__ __forceinline__ void median_to_first(const View &v, uint32_t f, uint3
 }
 
 // __adjust_heap + __push_heap on v.K/T[base ..)
-__device__ void adjust_heap(const View &v, uint32_t base, long hole, long len, uint64_t vk,
-                            uint32_t vt) {
+template <class V>
+__device__ void adjust_heap(const V &v, uint32_t base, long hole, long len,
+                            typename V::key_t vk, uint32_t vt) {
   const long top = hole;
   long child = hole;
-  uint64_t *K = v.K + base;
+  typename V::key_t *K = v.K + base;
   uint32_t *T = v.T + base;
   while (child < (len - 1) / 2) {
     child = 2 * (child + 1);
@@ -115,7 +124,8 @@ __device__ void adjust_heap(const View &v, uint32_t base, long hole, long len, u
 }
 
 // __partial_sort(first, last, last): __make_heap + __sort_heap; marks B = 2
-__device__ void heap_sort_segment(const View &v, uint32_t f, uint32_t l) {
+template <class V>
+__device__ void heap_sort_segment(const V &v, uint32_t f, uint32_t l) {
   const long len = (long)(l - f);
   if (len >= 2) {
     for (long parent = (len - 2) / 2;; --parent) {
@@ -125,7 +135,7 @@ __device__ void heap_sort_segment(const View &v, uint32_t f, uint32_t l) {
   }
   for (long last = len; last > 1;) {
     --last;
-    const uint64_t vk = v.K[f + last];
+    const typename V::key_t vk = v.K[f + last];
     const uint32_t vt = v.T[f + last];
     v.K[f + last] = v.K[f];
     v.T[f + last] = v.T[f];
@@ -135,19 +145,21 @@ __device__ void heap_sort_segment(const View &v, uint32_t f, uint32_t l) {
     for (uint32_t x = f; x < l; ++x) v.B[x] = 2;
 }
 
-// position of the r-th (0-based, from bit 0) set bit of m; m has more than r bits
-__device__ __forceinline__ int select_bit(uint64_t m, int r) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const int c = __popcll(m & ((1ull << w) - 1ull));
-    if (r >= c) {
-      r -= c;
-      m >>= w;
-      pos += w;
-    }
-  }
-  return pos;
+// cross-lane moves: pull from lane `src` (ds_bpermute) / push to lane `dst`
+// (ds_permute; the destinations must form a permutation)
+__device__ __forceinline__ uint32_t pull(int src, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ uint64_t pull(int src, uint64_t v) {
+  return (uint64_t)pull(src, (uint32_t)v) | (uint64_t)pull(src, (uint32_t)(v >> 32)) << 32;
+}
+__device__ __forceinline__ uint32_t push(int dst, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_permute(dst << 2, (int)v);
+}
+// popcount of the bits of m below this lane
+__device__ __forceinline__ int below_count(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // __introsort_loop on segments of at most 64 elements, in registers (lane x
@@ -155,21 +167,29 @@ __device__ __forceinline__ int select_bit(uint64_t m, int r) {
 // so every sub-segment of one recursion level is partitioned at once (each
 // keeps its own depth budget, as in the sequential recursion); each Hoare
 // partition is the stopper matching of wave_partition done with ballots and
-// shuffles.  Each lane ends with its final segment [sf, sl) (lane indices) --
-// a leaf, or a heap-sorted range when `heaped`: a depth-exhausted sub-segment
-// is written to memory (lane x at mpos), heap-sorted there by its first lane
-// and read back.
-template <bool GLOBAL, class KT>
-__device__ void reg_sort_core(const View &v, bool in, uint32_t mpos, int &sf, int &sl, int sd,
+// lane permutes.  With L_k / R_k the k-th L-stopper from the left / R-stopper
+// from the right of a segment:
+//   * L_k < R_k  <=>  more than k R-stoppers lie above L_k, so the swap count
+//     K is the rank of the first L-stopper without that property;
+//   * the swap partners come from two compacted lists (lane j of LL / RL holds
+//     the j-th L- / R-stopper of the whole wave; a segment's stoppers are a
+//     contiguous slice of them), built with one ds_permute each;
+//   * the cut min(R_{K-1}, L_K) (L_0 when K == 0) is the lowest lane that is
+//     one of those two, one ballot.
+// Each lane ends with its final segment [sf, sl) (lane indices) -- a leaf, or
+// a heap-sorted range when `heaped`: a depth-exhausted sub-segment is written
+// to memory (lane x at mpos), heap-sorted there by its first lane and read
+// back.
+template <bool GLOBAL, class KT, class V>
+__device__ void reg_sort_core(const V &v, bool in, uint32_t mpos, int &sf, int &sl, int sd,
                               uint32_t lane, KT &k, uint32_t &t, bool &heaped) {
   const int x = (int)lane;
   heaped = false;
-  const uint64_t below = (1ull << x) - 1ull, above = ~below & ~(1ull << x);
   for (;;) {
     bool active = in && !heaped && sl - sf > THRESH;
     const bool need_heap = active && sd == 0;
     if (__ballot(need_heap)) {  // rare: heap fallback in memory
-      if (in) v.K[mpos] = k, v.T[mpos] = t;
+      if (in) v.K[mpos] = (typename V::key_t)k, v.T[mpos] = t;
       sync_mem<GLOBAL>();
       if (need_heap && x == sf) heap_sort_segment(v, mpos, mpos + (sl - sf));
       sync_mem<GLOBAL>();
@@ -181,54 +201,44 @@ __device__ void reg_sort_core(const View &v, bool in, uint32_t mpos, int &sf, in
     const int len = sl - sf;
     // __move_median_to_first(f, f+1, mid, l-1)
     const int a = active ? sf + 1 : x, b = active ? sf + len / 2 : x, c = active ? sl - 1 : x;
-    const KT ka = __shfl(k, a), kb = __shfl(k, b), kc = __shfl(k, c);
+    const KT ka = pull(a, k), kb = pull(b, k), kc = pull(c, k);
     int med;
     if (ka < kb) med = kb < kc ? b : (ka < kc ? c : a);
     else med = ka < kc ? a : (kb < kc ? c : b);
     int src = x;
     if (active) src = x == sf ? med : (x == med ? sf : x);
-    k = __shfl(k, src);
-    t = __shfl(t, src);
-    const KT p = __shfl(k, active ? sf : x);
+    k = pull(src, k);
+    t = pull(src, t);
+    const KT p = pull(active ? sf : x, k);
     // stoppers of __unguarded_partition(f+1, l, f)
     const uint64_t segm = (sl >= 64 ? ~0ull : (1ull << sl) - 1ull) & ~((1ull << sf) - 1ull);
     const bool lf = active && x > sf && !(k < p);
     const bool rf = active && !(p < k);
-    const uint64_t Ls = __ballot(lf) & segm, Rs = __ballot(rf) & segm;
+    const uint64_t BL = __ballot(lf), BR = __ballot(rf);
+    const uint64_t Ls = BL & segm, Rs = BR & segm;
     const int nL = __popcll(Ls), nR = __popcll(Rs);
-    int rl = 0, partner = 0;
-    bool stop = false;
-    if (lf) {
-      rl = __popcll(Ls & below);
-      if (rl < nR) {
-        partner = select_bit(Rs, nR - 1 - rl);
-        stop = x >= partner;
-      } else {
-        stop = true;
-      }
-    }
-    const uint64_t stopm = __ballot(stop) & segm;
+    const int pL = below_count(BL), pR = below_count(BR);
+    const uint64_t lowseg = (1ull << sf) - 1ull;
+    const int offL = __popcll(BL & lowseg), offR = __popcll(BR & lowseg);
+    const int rl = pL - offL;                          // rank from the left (L lanes)
+    const int rr = nR - 1 - (pR - offR);               // rank from the right (R lanes)
+    const int rabove = nR - (pR - offR) - (rf ? 1 : 0);  // R-stoppers above this lane
+    const uint64_t stopm = __ballot(lf && rabove <= rl) & segm;
     const int lim = nL < nR ? nL : nR;
     const int K = stopm ? __popcll(Ls & ((1ull << __builtin_ctzll(stopm)) - 1ull)) : lim;
-    int s2 = x;
-    if (lf && rl < K) s2 = partner;
-    if (rf) {
-      const int rr = __popcll(Rs & above);  // rank from the right
-      if (rr < K) s2 = select_bit(Ls, rr);
-    }
-    k = __shfl(k, s2);
-    t = __shfl(t, s2);
+    // compacted stopper lists (stable partition of the lanes, one push each)
+    const int nBL = __popcll(BL), nBR = __popcll(BR);
+    const uint32_t LL = push(lf ? pL : nBL + (x - pL), (uint32_t)x);
+    const uint32_t RL = push(rf ? pR : nBR + (x - pR), (uint32_t)x);
+    const bool swl = lf && rl < K, swr = rf && rr < K;
+    const int idx = swl ? offR + nR - 1 - rl : swr ? offL + rr : x;
+    const uint32_t g = pull(idx, LL | RL << 8);
+    const int s2 = swl ? (int)(g >> 8) : swr ? (int)(g & 0xff) : x;
+    k = pull(s2, k);
+    t = pull(s2, t);
+    const uint64_t cm = __ballot((lf && rl == K) || (K > 0 && rf && rr == K - 1)) & segm;
     if (active) {
-      int cut;
-      if (K == 0) {
-        cut = select_bit(Ls, 0);
-      } else {
-        cut = select_bit(Rs, nR - K);
-        if (K < nL) {
-          const int lk = select_bit(Ls, K);
-          if (lk < cut) cut = lk;
-        }
-      }
+      const int cut = __builtin_ctzll(cm);
       if (x < cut) sl = cut;
       else sf = cut;
       --sd;
@@ -242,20 +252,20 @@ __device__ void reg_sort_core(const View &v, bool in, uint32_t mpos, int &sf, in
 // 32-bit registers (half the shuffle traffic).  The final order -- stable
 // leaf ranks, or heap-sorted ranges in place -- is written to out[] and the
 // positions are marked B = 3.
-template <bool GLOBAL, class KT>
-__device__ void reg_finish(const View &v, bool in, int bl, uint32_t bm, int len, int d,
+template <bool GLOBAL, class KT, class V>
+__device__ void reg_finish(const V &v, bool in, int bl, uint32_t bm, int len, int d,
                            uint32_t lane, uint64_t k64, uint32_t t, uint32_t *out) {
   const int x = (int)lane;
   KT k = in ? (KT)k64 : (KT)~(KT)0;
   int sf = in ? bl : x, sl = in ? bl + len : x + 1;
   bool heaped;
   const uint32_t mpos = bm + (uint32_t)(x - bl);
-  reg_sort_core<GLOBAL, KT>(v, in, mpos, sf, sl, d, lane, k, t, heaped);
+  reg_sort_core<GLOBAL, KT, V>(v, in, mpos, sf, sl, d, lane, k, t, heaped);
   uint32_t r = 0;
 #pragma unroll
   for (int j = 0; j < THRESH; ++j) {
     const int y = sf + j;
-    const KT ky = __shfl(k, y < 64 ? y : 63);
+    const KT ky = pull(y < 64 ? y : 63, k);
     r += (y < sl) && (ky < k || (ky == k && y < x));
   }
   if (in) {
@@ -264,30 +274,30 @@ __device__ void reg_finish(const View &v, bool in, int bl, uint32_t bm, int len,
   }
 }
 
-template <bool GLOBAL>
-__device__ void reg_batch(const View &v, bool in, int bl, uint32_t bm, int len, int d,
+template <bool GLOBAL, class V>
+__device__ void reg_batch(const V &v, bool in, int bl, uint32_t bm, int len, int d,
                           uint32_t lane, uint32_t *out) {
   const uint32_t mpos = bm + (uint32_t)((int)lane - bl);
-  const uint64_t k = in ? v.K[mpos] : ~0ull;
+  const uint64_t k = in ? (uint64_t)v.K[mpos] : ~0ull;
   const uint32_t t = in ? v.T[mpos] : 0u;
-  if (__ballot(in && (k >> 32) != 0))
-    reg_finish<GLOBAL, uint64_t>(v, in, bl, bm, len, d, lane, k, t, out);
+  if (sizeof(typename V::key_t) == 8 && __ballot(in && (k >> 32) != 0))
+    reg_finish<GLOBAL, uint64_t, V>(v, in, bl, bm, len, d, lane, k, t, out);
   else
-    reg_finish<GLOBAL, uint32_t>(v, in, bl, bm, len, d, lane, k, t, out);
+    reg_finish<GLOBAL, uint32_t, V>(v, in, bl, bm, len, d, lane, k, t, out);
 }
 
 // wavefront-parallel __unguarded_partition_pivot on [f, l); returns the cut
-template <bool GLOBAL>
-__device__ uint32_t wave_partition(const View &v, uint32_t f, uint32_t l, uint32_t lane) {
+template <bool GLOBAL, class V>
+__device__ uint32_t wave_partition(const V &v, uint32_t f, uint32_t l, uint32_t lane) {
   if (lane == 0) median_to_first(v, f, l);
   sync_mem<GLOBAL>();
-  const uint64_t p = v.K[f];
+  const typename V::key_t p = v.K[f];
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t nL = 0, nR = 0;
   for (uint32_t c = f; c < l; c += 64) {
     const uint32_t x = c + lane;
     const bool in = x < l;
-    const uint64_t k = in ? v.K[x] : 0;
+    const typename V::key_t k = in ? v.K[x] : 0;
     const bool lf = in && x > f && !(k < p);
     const bool rf = in && !(p < k);
     const uint64_t bl = __ballot(lf), br = __ballot(rf);
@@ -331,8 +341,8 @@ struct Frame {
 
 // the whole libstdc++ std::sort of one group [0, n) of view v, then stable
 // leaf ranks written to out[0..n) (tags only)
-template <bool GLOBAL>
-__device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *stack,
+template <bool GLOBAL, class V>
+__device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stack,
                               Frame *smallq, Frame *heapq, uint32_t lane) {
   for (uint32_t x = lane; x < n; x += 64) v.B[x] = 0;
   int sp = 0, nsmall = 0, nheap = 0;
@@ -358,7 +368,7 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
         break;
       }
       --d;
-      const uint32_t cut = wave_partition<GLOBAL>(v, f, l, lane);
+      const uint32_t cut = wave_partition<GLOBAL, V>(v, f, l, lane);
       if (lane == 0) stack[sp] = {cut, l, d};
       ++sp;
       l = cut;
@@ -375,7 +385,7 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
     while (j + 1 < q1 && (int)lane >= bl + (int)(smallq[j].l - smallq[j].f))
       bl += (int)(smallq[j].l - smallq[j].f), ++j;
     const Frame fr = smallq[j];
-    reg_batch<GLOBAL>(v, (int)lane < tot, bl, fr.f, (int)(fr.l - fr.f), fr.d, lane, out);
+    reg_batch<GLOBAL, V>(v, (int)lane < tot, bl, fr.f, (int)(fr.l - fr.f), fr.d, lane, out);
     q0 = q1;
   }
   sync_mem<GLOBAL>();
@@ -393,10 +403,10 @@ __device__ void wave_std_sort(const View &v, uint32_t n, uint32_t *out, Frame *s
     while (v.B[s] == 0) --s;
     uint32_t e = x + 1;
     while (e < n && v.B[e] == 0) ++e;
-    const uint64_t kx = v.K[x];
+    const typename V::key_t kx = v.K[x];
     uint32_t r = 0;
     for (uint32_t y = s; y < e; ++y) {
-      const uint64_t ky = v.K[y];
+      const typename V::key_t ky = v.K[y];
       r += (ky < kx) || (ky == kx && y < x);
     }
     out[s + r] = v.T[x];
@@ -415,12 +425,18 @@ __global__ void __launch_bounds__(256) k_sort_groups_reg(const uint32_t *list, u
        w += (gridDim.x * blockDim.x) >> 6) {
     const uint32_t g = list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
-    const View v{key + b, tag + b, nullptr, nullptr, nullptr};
-    reg_batch<true>(v, lane < n, 0, 0, (int)n, 2 * (31 - __clz((int)n)), lane, otag + b);
+    const GView v{key + b, tag + b, nullptr, nullptr, nullptr};
+    reg_batch<true, GView>(v, lane < n, 0, 0, (int)n, 2 * (31 - __clz((int)n)), lane, otag + b);
   }
 }
 
-// LDS tier: one wavefront (block of 64) per group of 17..cap members
+// LDS tier: one wavefront (block of 64) per group of up to `cap` members,
+// staged in LDS with KT keys and 16-bit positions.  The explicit stack holds
+// at most one frame per partition level: 2 * log2(cap) + 2.
+__host__ __device__ constexpr uint32_t lds_stack(uint32_t cap) {
+  return 2 * (31 - __builtin_clz(cap)) + 4;
+}
+template <class KT>
 __global__ void __launch_bounds__(64) k_sort_groups_lds(const uint32_t *list, uint32_t nlist,
                                                         const uint32_t *goff, const uint64_t *key,
                                                         const uint32_t *tag, uint32_t *otag,
@@ -428,20 +444,20 @@ __global__ void __launch_bounds__(64) k_sort_groups_lds(const uint32_t *list, ui
   extern __shared__ __align__(16) uint8_t smem[];
   const uint32_t lane = threadIdx.x;
   const uint32_t nfr = cap / (THRESH + 1) + 2;
-  uint64_t *K = reinterpret_cast<uint64_t *>(smem);
+  KT *K = reinterpret_cast<KT *>(smem);
   uint32_t *T = reinterpret_cast<uint32_t *>(K + cap);
-  uint32_t *PL = T + cap;
-  uint32_t *PR = PL + cap;
-  Frame *stack = reinterpret_cast<Frame *>(PR + cap);
-  Frame *smallq = stack + 72;
+  Frame *stack = reinterpret_cast<Frame *>(T + cap);
+  Frame *smallq = stack + lds_stack(cap);
   Frame *heapq = smallq + nfr;
-  uint8_t *B = reinterpret_cast<uint8_t *>(heapq + nfr);
-  const View v{K, T, PL, PR, B};
+  uint16_t *PL = reinterpret_cast<uint16_t *>(heapq + nfr);
+  uint16_t *PR = PL + cap;
+  uint8_t *B = reinterpret_cast<uint8_t *>(PR + cap);
+  const ViewT<KT, uint16_t> v{K, T, PL, PR, B};
   for (uint32_t w = blockIdx.x; w < nlist; w += gridDim.x) {
     const uint32_t g = list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     for (uint32_t x = lane; x < n; x += 64) {
-      K[x] = key[b + x];
+      K[x] = (KT)key[b + x];
       T[x] = tag[b + x];
     }
     wave_sync();
@@ -465,7 +481,7 @@ __global__ void __launch_bounds__(64) k_sort_groups_global(const uint32_t *list,
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     Frame *fr = frames + (b >> 3) + (size_t)80 * w;
     const uint32_t nfr = n / (THRESH + 1) + 2;
-    const View v{key + b, tag + b, pl + b, pr + b, bnd + b};
+    const GView v{key + b, tag + b, pl + b, pr + b, bnd + b};
     wave_std_sort<true>(v, n, otag + b, fr, fr + 72, fr + 72 + nfr, lane);
     wave_sync_global();
   }
@@ -488,22 +504,37 @@ __global__ void k_sort_small(const uint32_t *gid_sorted, const uint32_t *goff, u
   }
 }
 
-// tier flags per group: 0 = 1..16 members (k_sort_small), 1 = 17..64
-// (registers), 2 = ..cap (LDS), 3 = ..cap2 (LDS), 4 = larger (global memory);
-// members per tier -> tcount[0..4] for the timing accounts (one atomic per
-// block and tier, grid <= 1024 blocks)
-constexpr int NTIER = 5;
+// Tiers by group size: 0 = 1..16 members (k_sort_small), 1 = 17..64
+// (registers), 2..5 = up to LDS_CAPS[t-2] (LDS), 6 = larger (global memory).
+// Small LDS caps keep many wavefronts resident per CU (a 65..128-member group
+// needs ~3 KB of LDS, a 2048-member one ~30 KB).
+constexpr int NTIER = 7;
+constexpr int NLDS = 4;
+struct Caps {
+  uint32_t c[NLDS];
+};
+__host__ __device__ constexpr Caps lds_caps() { return Caps{{128, 256, 512, 2048}}; }
+
+// tier flags per group (one array per listed tier 1..6); members per tier ->
+// tcount[0..6] for the timing accounts (one atomic per block and tier, grid <=
+// 1024 blocks)
 __global__ void __launch_bounds__(256) k_tier_flags(const uint32_t *goff, uint32_t ngroups,
-                                                    uint32_t cap, uint32_t cap2, uint32_t *f,
-                                                    size_t fstride, uint32_t *tcount) {
-  uint32_t c[NTIER] = {0, 0, 0, 0, 0};
+                                                    uint32_t *f, size_t fstride, uint32_t *tcount) {
+  constexpr Caps caps = lds_caps();
+  uint32_t c[NTIER] = {};
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
        g += gridDim.x * blockDim.x) {
     const uint32_t n = goff[g + 1] - goff[g];
-    const int t = n <= (uint32_t)THRESH ? 0 : n <= 64 ? 1 : n <= cap ? 2 : n <= cap2 ? 3 : 4;
+    int t = n <= (uint32_t)THRESH ? 0 : n <= 64 ? 1 : NTIER - 1;
+    if (t == NTIER - 1) {
+#pragma unroll
+      for (int j = NLDS - 1; j >= 0; --j)
+        if (n <= caps.c[j]) t = 2 + j;
+    }
 #pragma unroll
     for (int u = 1; u < NTIER; ++u) f[(u - 1) * fstride + g] = t == u;
-    c[t] += n;
+#pragma unroll
+    for (int u = 0; u < NTIER; ++u) c[u] += t == u ? n : 0;
   }
   __shared__ uint32_t part[NTIER][4];
 #pragma unroll
@@ -525,19 +556,18 @@ __global__ void k_compact(const uint32_t *flag, const uint32_t *pos, uint32_t n,
     if (flag[g]) list[pos[g]] = g;
 }
 
-size_t lds_bytes(uint32_t cap) {
+size_t lds_bytes(uint32_t cap, size_t key_bytes) {
   const uint32_t nfr = cap / (THRESH + 1) + 2;
-  return (size_t)cap * (8 + 4 + 4 + 4) + (72 + 2 * nfr) * sizeof(Frame) + cap + 16;
+  return (size_t)cap * (key_bytes + 4 + 2 + 2 + 1) + (lds_stack(cap) + 2 * nfr) * sizeof(Frame) +
+         16;
 }
 
 }  // namespace
 
-constexpr uint32_t LDS_CAP = 512;    // groups up to this size: small LDS tier
-constexpr uint32_t LDS_CAP2 = 2048;  // up to this size: large LDS tier (3 waves / CU)
-
 size_t groupsort_scratch_bytes(uint32_t n) {
+  constexpr uint32_t cap = lds_caps().c[NLDS - 1];
   const size_t g1 = (size_t)n + 1;
-  const size_t frames = (size_t)n / 8 + 80 * ((size_t)n / (LDS_CAP2 + 1) + 1) + 80;
+  const size_t frames = (size_t)n / 8 + 80 * ((size_t)n / (cap + 1) + 1) + 80;
   // pl, pr; 3 x (NTIER-1) per-group arrays (flags, positions, lists); bounds;
   // counters; frames
   return (size_t)n * 4 * 2 + g1 * 4 * 3 * (NTIER - 1) + (size_t)n + 64 + 64 +
@@ -546,10 +576,11 @@ size_t groupsort_scratch_bytes(uint32_t n) {
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
-                       ScanScratch ss, uint32_t *host_words, hipStream_t st) {
+                       ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st) {
   if (!m) return;
   const size_t g1 = (size_t)ngroups + 1;
-  constexpr int NL = NTIER - 1;  // listed tiers 1..4
+  constexpr int NL = NTIER - 1;  // listed tiers 1..6
+  constexpr Caps caps = lds_caps();
   uint32_t *pl = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *pr = pl + m;
   uint32_t *fl = pr + m, *ps = fl + NL * g1, *ls = ps + NL * g1;
@@ -563,8 +594,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   kt_end(st, KID_SORT_SMALL, 0.0);  // bytes filled in below from the tier sizes
   const int small_slot = g_ktimer ? g_ktimer->n - 1 : -1;
   (void)hipMemsetAsync(tcount, 0, NTIER * sizeof(uint32_t), st);
-  k_tier_flags<<<grid_for(ngroups, 256, 1024), 256, 0, st>>>(goff, ngroups, LDS_CAP, LDS_CAP2, fl,
-                                                             g1, tcount);
+  k_tier_flags<<<grid_for(ngroups, 256, 1024), 256, 0, st>>>(goff, ngroups, fl, g1, tcount);
   for (int t = 0; t < NL; ++t) {
     uint32_t *f = fl + t * g1, *p = ps + t * g1, *l = ls + t * g1;
     (void)hipMemsetAsync(f + ngroups, 0, 4, st);
@@ -574,33 +604,36 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   }
   (void)hipMemcpyAsync(members, tcount, NTIER * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
   (void)hipStreamSynchronize(st);
-  const uint32_t n1 = host_words[0], n2 = host_words[1], n3 = host_words[2], n4 = host_words[3];
-  uint32_t *l1 = ls, *l2 = ls + g1, *l3 = ls + 2 * g1, *l4 = ls + 3 * g1;
+  uint32_t cnt[NL];
+  for (int t = 0; t < NL; ++t) cnt[t] = host_words[t];
   // algorithmic bytes of every tier: each member's (key, tag) read, its tag
   // written once at its final slot
   if (small_slot >= 0) g_ktimer->bytes[small_slot] = 16.0 * members[0];
-  if (n1) {
+  if (cnt[0]) {
     kt_begin(st);
-    k_sort_groups_reg<<<grid_for(n1, 4, 16384), 256, 0, st>>>(l1, n1, goff, key, tag, otag);
+    k_sort_groups_reg<<<grid_for(cnt[0], 4, 16384), 256, 0, st>>>(ls, cnt[0], goff, key, tag,
+                                                                  otag);
     kt_end(st, KID_SORT_REG, 16.0 * members[1]);
   }
-  if (n2) {
+  for (int j = 0; j < NLDS; ++j) {
+    const uint32_t n = cnt[1 + j], cap = caps.c[j];
+    if (!n) continue;
+    const uint32_t *l = ls + (1 + j) * g1;
+    const uint32_t grid = n < 16384 ? n : 16384;
     kt_begin(st);
-    k_sort_groups_lds<<<n2 < 16384 ? n2 : 16384, 64, lds_bytes(LDS_CAP), st>>>(
-        l2, n2, goff, key, tag, otag, LDS_CAP);
-    kt_end(st, KID_SORT_LDS, 16.0 * members[2]);
+    if (narrow_keys)
+      k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), st>>>(l, n, goff, key, tag,
+                                                                       otag, cap);
+    else
+      k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), st>>>(l, n, goff, key, tag,
+                                                                       otag, cap);
+    kt_end(st, KID_SORT_LDS, 16.0 * members[2 + j]);
   }
-  if (n3) {
+  if (const uint32_t n = cnt[NL - 1]) {
     kt_begin(st);
-    k_sort_groups_lds<<<n3 < 2048 ? n3 : 2048, 64, lds_bytes(LDS_CAP2), st>>>(
-        l3, n3, goff, key, tag, otag, LDS_CAP2);
-    kt_end(st, KID_SORT_LDS, 16.0 * members[3]);
-  }
-  if (n4) {
-    kt_begin(st);
-    k_sort_groups_global<<<n4 < 1024 ? n4 : 1024, 64, 0, st>>>(l4, n4, goff, key, tag, otag, pl,
-                                                               pr, bnd, frames);
-    kt_end(st, KID_SORT_GLOBAL, 16.0 * members[4]);
+    k_sort_groups_global<<<n < 1024 ? n : 1024, 64, 0, st>>>(ls + (NL - 1) * g1, n, goff, key,
+                                                            tag, otag, pl, pr, bnd, frames);
+    kt_end(st, KID_SORT_GLOBAL, 16.0 * members[NTIER - 1]);
   }
 }
 

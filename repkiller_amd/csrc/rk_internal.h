@@ -172,7 +172,8 @@ void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, u
                ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st);
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
 // in-group sort key |yStart - diag_func[xStart/10]| per fragment (p.ha)
-void sort_keys(Proc p, uint32_t m, hipStream_t st);
+// in-group sort keys; *wide |= 1 when one of them needs more than 32 bits
+void sort_keys(Proc p, uint32_t m, uint32_t *wide, hipStream_t st);
 // X axis in CSR order: centre/length (+ packed record, neighbour code), state UNKNOWN
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st);
 // X results (X-CSR order, i.e. nearly processing order): into the Y records,
@@ -195,10 +196,11 @@ void build_records(const uint32_t *gmem, const uint64_t *ha, uint32_t m, uint64_
 // ------------------------------------------------------- rk_groupsort.hip --
 size_t groupsort_scratch_bytes(uint32_t n);
 // libstdc++ std::sort of every group's (key, tag) records; sorted tags -> otag.
-// gid_sorted: group id of every record; host_words: >= 2 pinned words.
+// gid_sorted: group id of every record; host_words: >= 16 pinned words;
+// narrow_keys: every key fits 32 bits (LDS tiers stage 4-byte keys).
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
-                       ScanScratch ss, uint32_t *host_words, hipStream_t st);
+                       ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st);
 void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
                  const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st);
