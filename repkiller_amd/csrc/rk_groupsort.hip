@@ -261,12 +261,13 @@ __device__ void reg_finish(const V &v, bool in, int bl, uint32_t bm, int len, in
   bool heaped;
   const uint32_t mpos = bm + (uint32_t)(x - bl);
   reg_sort_core<GLOBAL, KT, V>(v, in, mpos, sf, sl, d, lane, k, t, heaped);
+  // stable rank inside the leaf; the loop runs to the longest leaf of the wave
   uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < THRESH; ++j) {
+  const int my = in && !heaped ? sl - sf : 0;
+  for (int j = 0; __ballot(j < my); ++j) {
     const int y = sf + j;
     const KT ky = pull(y < 64 ? y : 63, k);
-    r += (y < sl) && (ky < k || (ky == k && y < x));
+    r += (j < my) && (ky < k || (ky == k && y < x));
   }
   if (in) {
     out[heaped ? mpos : bm + (uint32_t)(sf - bl) + r] = t;

@@ -22,18 +22,19 @@
 // are mapped to blocks XCD by XCD (xcd_tile).
 #include "rk_internal.h"
 
+#include <cstdlib>
+
 namespace rk {
 namespace {
 
-constexpr int RADIX = 256;
-
-template <int T, int ITEMS>
+// digit widths 8..10 bits (RADIX = 1 << DB bins); tiles of T threads x ITEMS keys
+template <int T, int ITEMS, int DB>
 __global__ void __launch_bounds__(T) k_digit_hist(const uint32_t *__restrict__ key, uint32_t n,
                                                   int shift, uint32_t tiles,
                                                   uint32_t *__restrict__ counts) {
-  constexpr int TILE = T * ITEMS;
+  constexpr int TILE = T * ITEMS, RADIX = 1 << DB;
   __shared__ uint32_t hist[RADIX];
-  if (threadIdx.x < RADIX) hist[threadIdx.x] = 0;
+  for (int d = threadIdx.x; d < RADIX; d += T) hist[d] = 0;
   __syncthreads();
   const uint32_t base = blockIdx.x * (uint32_t)TILE;
   uint32_t kk[ITEMS];
@@ -46,15 +47,18 @@ __global__ void __launch_bounds__(T) k_digit_hist(const uint32_t *__restrict__ k
   for (int r = 0; r < ITEMS; ++r)
     if (base + r * T + threadIdx.x < n) atomicAdd(&hist[(kk[r] >> shift) & (RADIX - 1)], 1u);
   __syncthreads();
-  if (threadIdx.x < RADIX) counts[(size_t)blockIdx.x * RADIX + threadIdx.x] = hist[threadIdx.x];
+  for (int d = threadIdx.x; d < RADIX; d += T)
+    counts[(size_t)blockIdx.x * RADIX + d] = hist[d];
 }
 
-// Column scan of the [tiles][256] digit counts: thread d of block b sums
+// Column scan of the [tiles][RADIX] digit counts: thread d of block b sums
 // digit d over the rows [b*ROWS, (b+1)*ROWS) (each row read coalesced)...
 constexpr uint32_t ROWS = 16;
-__global__ void __launch_bounds__(RADIX) k_col_partial(const uint32_t *__restrict__ counts,
-                                                       uint32_t tiles,
-                                                       uint32_t *__restrict__ part) {
+template <int DB>
+__global__ void __launch_bounds__(1 << DB) k_col_partial(const uint32_t *__restrict__ counts,
+                                                         uint32_t tiles,
+                                                         uint32_t *__restrict__ part) {
+  constexpr int RADIX = 1 << DB;
   const uint32_t t0 = blockIdx.x * ROWS, t1 = min(t0 + ROWS, tiles);
   uint32_t s = 0;
   for (uint32_t t = t0; t < t1; ++t) s += counts[(size_t)t * RADIX + threadIdx.x];
@@ -62,8 +66,9 @@ __global__ void __launch_bounds__(RADIX) k_col_partial(const uint32_t *__restric
 }
 // ...block d scans digit d's partial sums over the row blocks (exclusive) and
 // stores the digit total...
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *tot) {
-  __shared__ uint32_t wsum[RADIX / 64];
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *tot) {
+  __shared__ uint32_t wsum[NT / 64];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t inc = v;
   for (int off = 1; off < 64; off <<= 1) {
@@ -73,7 +78,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *tot
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
   uint32_t pre = 0, all = 0;
-  for (uint32_t k = 0; k < RADIX / 64; ++k) {
+  for (uint32_t k = 0; k < NT / 64; ++k) {
     pre += k < w ? wsum[k] : 0u;
     all += wsum[k];
   }
@@ -81,15 +86,17 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *tot
   *tot = all;
   return pre + inc - v;
 }
-__global__ void __launch_bounds__(RADIX) k_col_digit(uint32_t *__restrict__ part, uint32_t nb,
-                                                     uint32_t *__restrict__ dtot) {
+template <int DB>
+__global__ void __launch_bounds__(256) k_col_digit(uint32_t *__restrict__ part, uint32_t nb,
+                                                   uint32_t *__restrict__ dtot) {
+  constexpr int RADIX = 1 << DB;
   const uint32_t d = blockIdx.x;
   uint32_t carry = 0;
-  for (uint32_t b0 = 0; b0 < nb; b0 += RADIX) {
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
     const uint32_t b = b0 + threadIdx.x;
     const uint32_t v = b < nb ? part[(size_t)b * RADIX + d] : 0u;
     uint32_t tot;
-    const uint32_t e = block_excl_scan256(v, &tot);
+    const uint32_t e = block_excl_scan<256>(v, &tot);
     if (b < nb) part[(size_t)b * RADIX + d] = carry + e;
     carry += tot;
   }
@@ -97,13 +104,16 @@ __global__ void __launch_bounds__(RADIX) k_col_digit(uint32_t *__restrict__ part
 }
 // ...and every block rewrites its rows with running offsets (in place).
 // (the digit base -- keys of all smaller digits -- is re-derived per block
-// from the 256 digit totals)
-__global__ void __launch_bounds__(RADIX) k_col_final(uint32_t *__restrict__ counts, uint32_t tiles,
-                                                     const uint32_t *__restrict__ part,
-                                                     const uint32_t *__restrict__ dtot) {
+// from the digit totals)
+template <int DB>
+__global__ void __launch_bounds__(1 << DB) k_col_final(uint32_t *__restrict__ counts,
+                                                       uint32_t tiles,
+                                                       const uint32_t *__restrict__ part,
+                                                       const uint32_t *__restrict__ dtot) {
+  constexpr int RADIX = 1 << DB;
   const uint32_t t0 = blockIdx.x * ROWS, t1 = min(t0 + ROWS, tiles);
   uint32_t all;
-  const uint32_t base = block_excl_scan256(dtot[threadIdx.x], &all);
+  const uint32_t base = block_excl_scan<RADIX>(dtot[threadIdx.x], &all);
   uint32_t run = base + part[blockIdx.x * RADIX + threadIdx.x];
   for (uint32_t t = t0; t < t1; ++t) {
     const uint32_t c = counts[(size_t)t * RADIX + threadIdx.x];
@@ -123,27 +133,27 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t tiles) {
 // Stable scatter of one tile through LDS.  Each wavefront ranks its own
 // contiguous slice of the tile (ITEMS rounds of 64 keys) against a
 // wave-private digit counter in LDS -- no workgroup barrier inside the rounds;
-// 8 ballots give each key's peers (same digit) in the round, so
+// DB ballots give each key's peers (same digit) in the round, so
 // rank = counter[d] + #peers in lower lanes.  One barrier then turns the
 // waves' digit counts into tile-local offsets; every key is placed at its
 // tile-local sorted slot in LDS and the tile is written out slot by slot
 // (consecutive lanes -> consecutive addresses of one digit segment).
 // Tile order = (wave, round, lane) = index order, hence stable.  Every load of
 // the tile is issued before the first ballot (2*ITEMS loads in flight/lane).
-template <int T, int ITEMS>
+template <int T, int ITEMS, int DB>
 __global__ void __launch_bounds__(T) k_digit_scatter(const uint32_t *__restrict__ key_in,
                                                      const uint32_t *__restrict__ val_in,
                                                      uint32_t n, int shift, uint32_t tiles,
                                                      const uint32_t *__restrict__ offs,
                                                      uint32_t *__restrict__ key_out,
                                                      uint32_t *__restrict__ val_out) {
-  constexpr int NW = T / 64, TILE = T * ITEMS, DW = RADIX / 64;
-  static_assert(T >= RADIX, "one thread per digit in the tile scan");
+  constexpr int RADIX = 1 << DB, NW = T / 64, TILE = T * ITEMS, DPT = RADIX / T;
+  static_assert(RADIX % T == 0, "whole digits per thread in the tile scan");
   __shared__ uint32_t sk[TILE];
   __shared__ uint32_t sv[TILE];
   __shared__ uint32_t wcnt[NW][RADIX];  // per-wave digit counters, then per-wave starts
   __shared__ uint32_t lbase[RADIX];     // tile-local start of digit d
-  __shared__ uint32_t wsum[DW];
+  __shared__ uint32_t wsum[NW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
   const uint32_t tile = xcd_tile(blockIdx.x, tiles);
@@ -172,7 +182,7 @@ __global__ void __launch_bounds__(T) k_digit_scatter(const uint32_t *__restrict_
     const uint32_t d = (kk[r] >> shift) & (RADIX - 1);
     uint64_t peer = __ballot(live);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < DB; ++b) {
       const bool bit = (d >> b) & 1u;
       const uint64_t bb = __ballot(bit);
       peer &= bit ? bb : ~bb;
@@ -185,29 +195,38 @@ __global__ void __launch_bounds__(T) k_digit_scatter(const uint32_t *__restrict_
     rk[r] = live ? before + below : 0xFFFFFFFFu;
   }
   __syncthreads();
-  // digit d (threads 0..255): tile total -> exclusive scan (lbase); wave starts
-  // inside the digit
-  uint32_t run = 0, inc = 0;
-  if (threadIdx.x < RADIX) {
-    const uint32_t d = threadIdx.x;
+  // thread t owns digits [t*DPT, (t+1)*DPT): tile totals -> exclusive scan
+  // (lbase); wave starts inside each digit
+  uint32_t run[DPT], tsum = 0;
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const uint32_t d = threadIdx.x * DPT + j;
+    uint32_t r0 = 0;
 #pragma unroll
     for (int k2 = 0; k2 < NW; ++k2) {
       const uint32_t c = wcnt[k2][d];
-      wcnt[k2][d] = run;
-      run += c;
+      wcnt[k2][d] = r0;
+      r0 += c;
     }
-    inc = run;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t o = __shfl_up(inc, off);
-      if (lane >= off) inc += o;
-    }
-    if (lane == 63) wsum[w] = inc;
+    run[j] = r0;
+    tsum += r0;
   }
+  uint32_t inc = tsum;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(inc, off);
+    if (lane >= off) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  if (threadIdx.x < RADIX) {
+  {
     uint32_t pre = 0;
     for (int k2 = 0; k2 < w; ++k2) pre += wsum[k2];
-    lbase[threadIdx.x] = pre + inc - run;
+    uint32_t at = pre + inc - tsum;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      lbase[threadIdx.x * DPT + j] = at;
+      at += run[j];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -229,26 +248,40 @@ __global__ void __launch_bounds__(T) k_digit_scatter(const uint32_t *__restrict_
 }
 
 // Tile shape: 256 threads x 16 keys.  Measured on MI355X at 50M keys (scatter,
-// per pass): 256x16 0.181 ms, 512x16 0.184, 256x32 0.229, 1024x16 0.252,
-// 1024x8 0.282 -- four 37-KB blocks per CU beat fewer, larger tiles.
+// per pass, 8-bit digits): 256x16 0.181 ms, 512x16 0.184, 256x32 0.229,
+// 1024x16 0.252, 1024x8 0.282 -- four 37-KB blocks per CU beat fewer, larger
+// tiles.
 constexpr int RT = 256, RITEMS = 16;
 constexpr uint32_t RTILE = RT * RITEMS;
+constexpr int MAX_DB = 10;  // the column kernels use one thread per digit (<= 1024)
 
-template <int T, int I>
+template <int T, int I, int DB>
 void launch_pass(const uint32_t *ki, const uint32_t *vi, uint32_t n, int shift, uint32_t tiles,
                  uint32_t *counts, ScanScratch ss, uint32_t *ko, uint32_t *vo, hipStream_t st) {
+  constexpr int RADIX = 1 << DB;
   kt_begin(st);
-  k_digit_hist<T, I><<<tiles, T, 0, st>>>(ki, n, shift, tiles, counts);
+  k_digit_hist<T, I, DB><<<tiles, T, 0, st>>>(ki, n, shift, tiles, counts);
   kt_end(st, KID_HIST, 4.0 * n);  // keys read once
   const uint32_t nb = (tiles + ROWS - 1) / ROWS;
-  uint32_t *part = ss.block_sums;  // nb * 256 words
+  uint32_t *part = ss.block_sums;  // nb * RADIX words
   uint32_t *dtot = part + (size_t)nb * RADIX;
-  k_col_partial<<<nb, RADIX, 0, st>>>(counts, tiles, part);
-  k_col_digit<<<RADIX, RADIX, 0, st>>>(part, nb, dtot);
-  k_col_final<<<nb, RADIX, 0, st>>>(counts, tiles, part, dtot);
+  k_col_partial<DB><<<nb, RADIX, 0, st>>>(counts, tiles, part);
+  k_col_digit<DB><<<RADIX, 256, 0, st>>>(part, nb, dtot);
+  k_col_final<DB><<<nb, RADIX, 0, st>>>(counts, tiles, part, dtot);
   kt_begin(st);
-  k_digit_scatter<T, I><<<tiles, T, 0, st>>>(ki, vi, n, shift, tiles, counts, ko, vo);
+  k_digit_scatter<T, I, DB><<<tiles, T, 0, st>>>(ki, vi, n, shift, tiles, counts, ko, vo);
   kt_end(st, KID_SCATTER, (vi ? 16.0 : 12.0) * n);  // key (+value) read, key+value written
+}
+
+// widest digit (9 bits measured best at cfg3: 26-bit occupancy keys take 3
+// passes instead of 4); RK_RADIX_BITS (8..10) overrides it, for measurements
+int max_digit_bits() {
+  static const int v = [] {
+    const char *e = getenv("RK_RADIX_BITS");
+    const int b = e ? atoi(e) : 9;
+    return b < 8 ? 8 : b > MAX_DB ? MAX_DB : b;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -257,6 +290,7 @@ thread_local KernelTimer *g_ktimer = nullptr;
 
 size_t radix_scratch_words(uint32_t n) {
   const size_t tiles = (n + RTILE - 1) / RTILE;
+  constexpr size_t RADIX = 1u << MAX_DB;
   const size_t cnt = tiles * RADIX + 1;
   const size_t part = ((tiles + ROWS - 1) / ROWS + 1) * RADIX;  // column-scan partials, totals
   return ((cnt + 3) & ~(size_t)3) + part + 64;
@@ -271,19 +305,30 @@ void radix_sort_pairs(const uint32_t *key_in, const uint32_t *val_in, uint32_t *
                       int bits, uint32_t *scratch, size_t scratch_words, hipStream_t st) {
   if (n == 0) return;
   if (bits < 1) bits = 1;
-  const int passes = (bits + 7) / 8;
+  // as few passes as the widest digit allows, widths as even as possible
+  const int maxdb = max_digit_bits();
+  const int passes = (bits + maxdb - 1) / maxdb;
   const uint32_t tiles = (n + RTILE - 1) / RTILE;
-  const size_t cnt = (size_t)tiles * RADIX + 1;
+  const size_t cnt = (size_t)tiles * (1u << MAX_DB) + 1;
   uint32_t *counts = scratch;
   ScanScratch ss{scratch + ((cnt + 3) & ~(size_t)3),
                  scratch_words - ((cnt + 3) & ~(size_t)3)};
   // ping-pong so that the last pass writes key_out/val_out
   const uint32_t *ki = key_in, *vi = val_in;
+  int shift = 0;
   for (int p = 0; p < passes; ++p) {
     // pass p writes out when (passes-1-p) is even, tmp otherwise
     uint32_t *ko = ((passes - 1 - p) % 2 == 0) ? key_out : key_tmp;
     uint32_t *vo = ((passes - 1 - p) % 2 == 0) ? val_out : val_tmp;
-    launch_pass<RT, RITEMS>(ki, vi, n, 8 * p, tiles, counts, ss, ko, vo, st);
+    const int left = bits - shift, w0 = (left + (passes - p) - 1) / (passes - p);
+    const int db = w0 < 8 ? 8 : w0;  // a narrower digit still uses 256 bins
+    switch (db) {
+      case 8: launch_pass<RT, RITEMS, 8>(ki, vi, n, shift, tiles, counts, ss, ko, vo, st); break;
+      case 9: launch_pass<RT, RITEMS, 9>(ki, vi, n, shift, tiles, counts, ss, ko, vo, st); break;
+      case 10: launch_pass<RT, RITEMS, 10>(ki, vi, n, shift, tiles, counts, ss, ko, vo, st); break;
+      default: launch_pass<RT, RITEMS, 10>(ki, vi, n, shift, tiles, counts, ss, ko, vo, st); break;
+    }
+    shift += w0;
     ki = ko;
     vi = vo;
   }
