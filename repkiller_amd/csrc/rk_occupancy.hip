@@ -42,6 +42,8 @@
 // the reference's expression shape; this TU is built with -ffp-contract=off so
 // 0.4*sl + 0.6*sp is never fused (the reference binary is baseline x86-64).
 #include "rk_internal.h"
+#include <cstdio>
+#include <cstdlib>
 
 namespace rk {
 namespace {
@@ -314,22 +316,30 @@ __global__ void __launch_bounds__(256) k_sweep_tile(Axis ax, uint8_t *wpend, uin
     }
     // rounds of ballots: an ACTIVE candidate means a hit; an UNKNOWN one
     // blocks the final decision (it may still become ACTIVE and win)
+    // (the round structure of sweep_window32 below)
     for (;;) {
       const M128 A{__ballot(own[0] && st[0] == ST_ACTIVE), __ballot(own[1] && st[1] == ST_ACTIVE)};
       const M128 U{__ballot(own[0] && st[0] == ST_UNKNOWN), __ballot(own[1] && st[1] == ST_UNKNOWN)};
       bool changed = false;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
+        if (!own[s] || st[s] != ST_UNKNOWN) continue;
         const bool has_act = any_and(rown[s], A) || any_and(rnb[s], A) || fs[s].any_active;
         const bool has_unk = any_and(rown[s], U) || any_and(rnb[s], U) || fs[s].any_unknown;
-        if (st[s] == ST_UNKNOWN) {
-          if (has_act) st[s] = ST_HIT_PENDING, changed = true;
-          else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
-        }
-        if (st[s] == ST_HIT_PENDING && !has_unk) st[s] = ST_HIT, changed = true;
+        if (has_act) st[s] = ST_HIT_PENDING, changed = true;
+        else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
       }
-      if (!__ballot(changed)) break;
+      const M128 V{__ballot(own[0] && st[0] == ST_UNKNOWN), __ballot(own[1] && st[1] == ST_UNKNOWN)};
+      bool left = false;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (!own[s]) continue;
+        if (st[s] == ST_HIT_PENDING && !any_and(rown[s], V) && !any_and(rnb[s], V) &&
+            !fs[s].any_unknown)
+          st[s] = ST_HIT, changed = true;
+        left |= st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING;
+      }
+      if (!__ballot(changed) || !__ballot(left)) break;
     }
     const M128 A{__ballot(own[0] && st[0] == ST_ACTIVE), __ballot(own[1] && st[1] == ST_ACTIVE)};
     // winners (the matching ACTIVE candidates in scan order) and write-back
@@ -454,6 +464,10 @@ __device__ __forceinline__ void foreign_scan32(const Axis &ax, uint32_t g0, int 
   }
 }
 
+#ifndef RK_OWN_U
+#define RK_OWN_U 4
+#endif
+constexpr int OWN_U = RK_OWN_U;
 // One window (64 positions) of the 32-bit sweep; LDS scratch of the calling
 // wavefront in pk / ent / key.  Returns (wave-uniformly) whether the window
 // still owns undecided entries, and records that in wpend[w].
@@ -516,26 +530,37 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     uint64_t rown[2], rnb[2];
     int nbs[2];
     Scan fs[2];
+    Q32 qs[2];
+    bool open[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       rown[s] = rnb[s] = 0;
       nbs[s] = 0;
       fs[s] = Scan{0.0, NONE, 0, false, false};
-      if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
+      open[s] = own[s] && (st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING);
+      if (!open[s]) continue;
       const int P = 64 * s + lane;
       const uint2 me = pk[P];
       const Q32 q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
+      qs[s] = q;
       const int n = P - rs[s];
-      // four independent LDS reads per step (pk is padded past position 127)
-      for (int j = 0; j < n; j += 4) {
-        const uint2 o0 = pk[rs[s] + j], o1 = pk[rs[s] + j + 1], o2 = pk[rs[s] + j + 2],
-                    o3 = pk[rs[s] + j + 3];
-        uint64_t b4 = (uint64_t)m32(q, o0) | (uint64_t)m32(q, o1) << 1 |
-                      (uint64_t)m32(q, o2) << 2 | (uint64_t)m32(q, o3) << 3;
-        if (n - j < 4) b4 &= (1ull << (n - j)) - 1ull;
+      // OWN_U independent LDS reads per step (pk is padded past position 127)
+      for (int j = 0; j < n; j += OWN_U) {
+        uint2 o[OWN_U];
+#pragma unroll
+        for (int u = 0; u < OWN_U; ++u) o[u] = pk[rs[s] + j + u];
+        uint64_t b4 = 0;
+#pragma unroll
+        for (int u = 0; u < OWN_U; ++u) b4 |= (uint64_t)m32(q, o[u]) << u;
+        if (n - j < OWN_U) b4 &= (1ull << (n - j)) - 1ull;
         rown[s] |= b4 << j;
       }
-      if (!nd[s]) continue;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (!open[s] || !nd[s]) continue;
+      const int P = 64 * s + lane;
+      const Q32 q = qs[s];
       const int dir = nd[s] == 1 ? -1 : 1;
       const uint32_t i = ent[P], k = key[P];
       uint32_t g0 = 0;  // first position of a foreign neighbour scan
@@ -581,6 +606,11 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     }
     // rounds of ballots: a matching ACTIVE candidate means a hit; a matching
     // UNKNOWN one blocks the final decision (it may still become ACTIVE and win)
+    // A round: UNKNOWN entries with an ACTIVE candidate become HIT_PENDING and
+    // those with only decided, inactive candidates ACTIVE; then, against the
+    // UNKNOWN set left after that, pending hits whose candidates are all
+    // decided become final.  Rounds stop when nothing changes or nothing is
+    // left open.
     uint64_t A0, A1;
     for (;;) {
       A0 = __ballot(own[0] && st[0] == ST_ACTIVE);
@@ -590,17 +620,27 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
       bool changed = false;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        if (!own[s] || (st[s] != ST_UNKNOWN && st[s] != ST_HIT_PENDING)) continue;
+        if (!own[s] || st[s] != ST_UNKNOWN) continue;
         const bool has_act = ((A0 & cm[s].lo) | (A1 & cm[s].hi)) != 0 || fs[s].any_active;
         const bool has_unk = ((U0 & cm[s].lo) | (U1 & cm[s].hi)) != 0 || fs[s].any_unknown;
-        if (st[s] == ST_UNKNOWN) {
-          if (has_act) st[s] = ST_HIT_PENDING, changed = true;
-          else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
-        }
-        if (st[s] == ST_HIT_PENDING && !has_unk) st[s] = ST_HIT, changed = true;
+        if (has_act) st[s] = ST_HIT_PENDING, changed = true;
+        else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
       }
-      if (!__ballot(changed)) break;
+      const uint64_t V0 = __ballot(own[0] && st[0] == ST_UNKNOWN);
+      const uint64_t V1 = __ballot(own[1] && st[1] == ST_UNKNOWN);
+      bool left = false;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (!own[s]) continue;
+        if (st[s] == ST_HIT_PENDING && ((V0 & cm[s].lo) | (V1 & cm[s].hi)) == 0 &&
+            !fs[s].any_unknown)
+          st[s] = ST_HIT, changed = true;
+        left |= st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING;
+      }
+      if (!__ballot(changed) || !__ballot(left)) break;
     }
+    A0 = __ballot(own[0] && st[0] == ST_ACTIVE);
+    A1 = __ballot(own[1] && st[1] == ST_ACTIVE);
     // winners: the first strict maximum in scan order among the matching
     // ACTIVE candidates (own run newest first, then the neighbour run); a
     // single candidate needs no deviation
@@ -655,7 +695,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
 k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_t *big,
              uint32_t *nbig) {
-  __shared__ uint2 s_pk[4][132];  // {centre low 32 bits, length}; 4 entries of read padding
+  __shared__ uint2 s_pk[4][128 + OWN_U];  // {centre low 32 bits, length}; read padding
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t w = blockIdx.x * 4 + wv;
@@ -668,7 +708,7 @@ k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_
 // later sweeps: one wavefront per 64 windows, which reads their flags with
 // one coalesced load and handles the still-pending ones in turn
 __global__ void __launch_bounds__(256) k_sweep_fast_more(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
-  __shared__ uint2 s_pk[4][132];
+  __shared__ uint2 s_pk[4][128 + OWN_U];
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t g = blockIdx.x * 4 + wv, w0 = g * 64;
