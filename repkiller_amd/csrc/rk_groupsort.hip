@@ -33,6 +33,8 @@
 // In every tier the result goes to `otag` (member order, group-major).
 #include "rk_internal.h"
 
+#include <vector>
+
 namespace rk {
 namespace {
 
@@ -414,17 +416,32 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
   }
 }
 
+// The listed tiers' groups, tier-major in one array: tier u (1..6) owns
+// list[off[(u-1)*nblk] .. off[u*nblk]) (off = exclusive scan of per-block
+// tier counts, see k_tier_lists).  Kernels read their range on the device, so
+// no host round trip sizes the launches.
+struct TierLists {
+  const uint32_t *list, *off;
+  uint32_t nblk;
+  __device__ __forceinline__ void range(int u, uint32_t &lo, uint32_t &hi) const {
+    lo = off[(size_t)(u - 1) * nblk];
+    hi = off[(size_t)u * nblk];
+  }
+};
+
 // Register tier: one wavefront per group of 17..64 members, no LDS.  The
 // group lives in registers (lane x = member x), the introsort runs there and
 // __final_insertion_sort is the stable rank inside each leaf (<= 16 lanes,
 // by shuffles); heap-sorted ranges are already in order.
-__global__ void __launch_bounds__(256) k_sort_groups_reg(const uint32_t *list, uint32_t nlist,
+__global__ void __launch_bounds__(256) k_sort_groups_reg(TierLists tl, int tier,
                                                          const uint32_t *goff, uint64_t *key,
                                                          uint32_t *tag, uint32_t *otag) {
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nlist;
+  uint32_t lo, hi;
+  tl.range(tier, lo, hi);
+  for (uint32_t w = lo + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); w < hi;
        w += (gridDim.x * blockDim.x) >> 6) {
-    const uint32_t g = list[w];
+    const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     const GView v{key + b, tag + b, nullptr, nullptr, nullptr};
     reg_batch<true, GView>(v, lane < n, 0, 0, (int)n, 2 * (31 - __clz((int)n)), lane, otag + b);
@@ -438,7 +455,7 @@ __host__ __device__ constexpr uint32_t lds_stack(uint32_t cap) {
   return 2 * (31 - __builtin_clz(cap)) + 4;
 }
 template <class KT>
-__global__ void __launch_bounds__(64) k_sort_groups_lds(const uint32_t *list, uint32_t nlist,
+__global__ void __launch_bounds__(64) k_sort_groups_lds(TierLists tl, int tier,
                                                         const uint32_t *goff, const uint64_t *key,
                                                         const uint32_t *tag, uint32_t *otag,
                                                         uint32_t cap) {
@@ -454,8 +471,10 @@ __global__ void __launch_bounds__(64) k_sort_groups_lds(const uint32_t *list, ui
   uint16_t *PR = PL + cap;
   uint8_t *B = reinterpret_cast<uint8_t *>(PR + cap);
   const ViewT<KT, uint16_t> v{K, T, PL, PR, B};
-  for (uint32_t w = blockIdx.x; w < nlist; w += gridDim.x) {
-    const uint32_t g = list[w];
+  uint32_t lo, hi;
+  tl.range(tier, lo, hi);
+  for (uint32_t w = lo + blockIdx.x; w < hi; w += gridDim.x) {
+    const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     for (uint32_t x = lane; x < n; x += 64) {
       K[x] = (KT)key[b + x];
@@ -471,16 +490,18 @@ __global__ void __launch_bounds__(64) k_sort_groups_lds(const uint32_t *list, ui
 // storage of the w-th listed group starts at (b >> 3) + 80 * w: regions of
 // consecutive listed groups never overlap (a group of n members needs at most
 // 72 + 2 * (n / 17 + 2) frames).
-__global__ void __launch_bounds__(64) k_sort_groups_global(const uint32_t *list, uint32_t nlist,
+__global__ void __launch_bounds__(64) k_sort_groups_global(TierLists tl, int tier,
                                                            const uint32_t *goff, uint64_t *key,
                                                            uint32_t *tag, uint32_t *otag,
                                                            uint32_t *pl, uint32_t *pr,
                                                            uint8_t *bnd, Frame *frames) {
   const uint32_t lane = threadIdx.x;
-  for (uint32_t w = blockIdx.x; w < nlist; w += gridDim.x) {
-    const uint32_t g = list[w];
+  uint32_t lo, hi;
+  tl.range(tier, lo, hi);
+  for (uint32_t w = lo + blockIdx.x; w < hi; w += gridDim.x) {
+    const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
-    Frame *fr = frames + (b >> 3) + (size_t)80 * w;
+    Frame *fr = frames + (b >> 3) + (size_t)80 * (w - lo);
     const uint32_t nfr = n / (THRESH + 1) + 2;
     const GView v{key + b, tag + b, pl + b, pr + b, bnd + b};
     wave_std_sort<true>(v, n, otag + b, fr, fr + 72, fr + 72 + nfr, lane);
@@ -516,45 +537,77 @@ struct Caps {
 };
 __host__ __device__ constexpr Caps lds_caps() { return Caps{{128, 256, 512, 2048}}; }
 
-// tier flags per group (one array per listed tier 1..6); members per tier ->
-// tcount[0..6] for the timing accounts (one atomic per block and tier, grid <=
-// 1024 blocks)
-__global__ void __launch_bounds__(256) k_tier_flags(const uint32_t *goff, uint32_t ngroups,
-                                                    uint32_t *f, size_t fstride, uint32_t *tcount) {
+__device__ __forceinline__ int tier_of(uint32_t n) {
   constexpr Caps caps = lds_caps();
-  uint32_t c[NTIER] = {};
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
-       g += gridDim.x * blockDim.x) {
-    const uint32_t n = goff[g + 1] - goff[g];
-    int t = n <= (uint32_t)THRESH ? 0 : n <= 64 ? 1 : NTIER - 1;
-    if (t == NTIER - 1) {
+  if (n <= (uint32_t)THRESH) return 0;
+  if (n <= 64) return 1;
 #pragma unroll
-      for (int j = NLDS - 1; j >= 0; --j)
-        if (n <= caps.c[j]) t = 2 + j;
-    }
-#pragma unroll
-    for (int u = 1; u < NTIER; ++u) f[(u - 1) * fstride + g] = t == u;
-#pragma unroll
-    for (int u = 0; u < NTIER; ++u) c[u] += t == u ? n : 0;
-  }
-  __shared__ uint32_t part[NTIER][4];
-#pragma unroll
-  for (int t = 0; t < NTIER; ++t) {
-    uint32_t v = c[t];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if ((threadIdx.x & 63) == 0) part[t][threadIdx.x >> 6] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < NTIER) {
-    const uint32_t v = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] +
-                       part[threadIdx.x][3];
-    if (v) atomicAdd(&tcount[threadIdx.x], v);
-  }
+  for (int j = 0; j < NLDS; ++j)
+    if (n <= caps.c[j]) return 2 + j;
+  return NTIER - 1;
 }
 
-__global__ void k_compact(const uint32_t *flag, const uint32_t *pos, uint32_t n, uint32_t *list) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < n; g += gridDim.x * blockDim.x)
-    if (flag[g]) list[pos[g]] = g;
+// Tier lists in two passes over the groups, TCH groups per block: count the
+// listed tiers per block (and, for the timing accounts, their members), then
+// -- after an exclusive scan of the tier-major block counts -- write every
+// group at its tier's block offset + its rank in the block.
+constexpr uint32_t TCH = 4096;
+__global__ void __launch_bounds__(256) k_tier_count(const uint32_t *goff, uint32_t ngroups,
+                                                    uint32_t nblk, uint32_t *bc, uint32_t *bm) {
+  __shared__ uint32_t cnt[NTIER], mem[NTIER];
+  if (threadIdx.x < NTIER) cnt[threadIdx.x] = mem[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t g0 = blockIdx.x * TCH, g1 = min(g0 + TCH, ngroups);
+  uint32_t c[NTIER] = {}, mm[NTIER] = {};
+  for (uint32_t g = g0 + threadIdx.x; g < g1; g += 256) {
+    const uint32_t n = goff[g + 1] - goff[g];
+    const int t = tier_of(n);
+#pragma unroll
+    for (int u = 0; u < NTIER; ++u) c[u] += t == u, mm[u] += t == u ? n : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < NTIER; ++u) {
+    uint32_t v = c[u], x = mm[u];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off), x += __shfl_xor(x, off);
+    if ((threadIdx.x & 63) == 0 && (v || x)) atomicAdd(&cnt[u], v), atomicAdd(&mem[u], x);
+  }
+  __syncthreads();
+  if (threadIdx.x >= 1 && threadIdx.x < NTIER)
+    bc[(size_t)(threadIdx.x - 1) * nblk + blockIdx.x] = cnt[threadIdx.x];
+  if (bm && threadIdx.x < NTIER) bm[(size_t)threadIdx.x * nblk + blockIdx.x] = mem[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) k_tier_lists(const uint32_t *goff, uint32_t ngroups,
+                                                    uint32_t nblk, const uint32_t *off,
+                                                    uint32_t *list) {
+  __shared__ uint32_t wc[4][NTIER];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t run[NTIER];
+#pragma unroll
+  for (int u = 1; u < NTIER; ++u) run[u] = off[(size_t)(u - 1) * nblk + blockIdx.x];
+  const uint32_t g0 = blockIdx.x * TCH, g1 = min(g0 + TCH, ngroups);
+  for (uint32_t c0 = g0; c0 < g1; c0 += 256) {
+    const uint32_t g = c0 + threadIdx.x;
+    const int t = g < g1 ? tier_of(goff[g + 1] - goff[g]) : 0;
+    uint32_t rank = 0;
+#pragma unroll
+    for (int u = 1; u < NTIER; ++u) {
+      const uint64_t b = __ballot(t == u);
+      if (t == u) rank = __popcll(b & ((1ull << lane) - 1ull));
+      if (lane == 0) wc[wv][u] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    if (t > 0) {
+      uint32_t before = 0;
+      for (int k = 0; k < wv; ++k) before += wc[k][t];
+#pragma unroll
+      for (int u = 1; u < NTIER; ++u)
+        if (u == t) list[run[u] + before + rank] = g;
+    }
+#pragma unroll
+    for (int u = 1; u < NTIER; ++u) run[u] += wc[0][u] + wc[1][u] + wc[2][u] + wc[3][u];
+    __syncthreads();
+  }
 }
 
 size_t lds_bytes(uint32_t cap, size_t key_bytes) {
@@ -567,75 +620,72 @@ size_t lds_bytes(uint32_t cap, size_t key_bytes) {
 
 size_t groupsort_scratch_bytes(uint32_t n) {
   constexpr uint32_t cap = lds_caps().c[NLDS - 1];
-  const size_t g1 = (size_t)n + 1;
+  const size_t nblk = (size_t)n / TCH + 1;
   const size_t frames = (size_t)n / 8 + 80 * ((size_t)n / (cap + 1) + 1) + 80;
-  // pl, pr; 3 x (NTIER-1) per-group arrays (flags, positions, lists); bounds;
-  // counters; frames
-  return (size_t)n * 4 * 2 + g1 * 4 * 3 * (NTIER - 1) + (size_t)n + 64 + 64 +
-         frames * sizeof(Frame) + 256;
+  // pl, pr; tier lists; bounds; block counts (+ scan), block members; frames
+  return (size_t)n * 4 * 2 + ((size_t)n + 1) * 4 + (size_t)n + 64 +
+         (nblk * (NTIER - 1) + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + frames * sizeof(Frame) + 256;
 }
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
                        ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st) {
   if (!m) return;
-  const size_t g1 = (size_t)ngroups + 1;
   constexpr int NL = NTIER - 1;  // listed tiers 1..6
   constexpr Caps caps = lds_caps();
+  const uint32_t nblk = (ngroups + TCH - 1) / TCH;
   uint32_t *pl = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *pr = pl + m;
-  uint32_t *fl = pr + m, *ps = fl + NL * g1, *ls = ps + NL * g1;
-  uint8_t *bnd = reinterpret_cast<uint8_t *>(ls + NL * g1);
-  uint32_t *tcount = reinterpret_cast<uint32_t *>(
+  uint32_t *list = pr + m;
+  uint8_t *bnd = reinterpret_cast<uint8_t *>(list + ngroups + 1);
+  uint32_t *bc = reinterpret_cast<uint32_t *>(
       (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
-  Frame *frames = reinterpret_cast<Frame *>(tcount + 16);
-  uint32_t *members = host_words + 8;  // device counters live after the tier counts
+  uint32_t *boff = bc + (size_t)NL * nblk + 1;
+  uint32_t *bm = boff + (size_t)NL * nblk + 1;
+  Frame *frames = reinterpret_cast<Frame *>(
+      (reinterpret_cast<uintptr_t>(bm + (size_t)NTIER * nblk) + 63) & ~(uintptr_t)63);
+  const bool timing = g_ktimer != nullptr;
   kt_begin(st);
   k_sort_small<<<grid_for(m, 256), 256, 0, st>>>(gid_sorted, goff, m, key, tag, otag);
   kt_end(st, KID_SORT_SMALL, 0.0);  // bytes filled in below from the tier sizes
-  const int small_slot = g_ktimer ? g_ktimer->n - 1 : -1;
-  (void)hipMemsetAsync(tcount, 0, NTIER * sizeof(uint32_t), st);
-  k_tier_flags<<<grid_for(ngroups, 256, 1024), 256, 0, st>>>(goff, ngroups, fl, g1, tcount);
-  for (int t = 0; t < NL; ++t) {
-    uint32_t *f = fl + t * g1, *p = ps + t * g1, *l = ls + t * g1;
-    (void)hipMemsetAsync(f + ngroups, 0, 4, st);
-    exclusive_scan_u32(f, p, g1, ss, st);
-    k_compact<<<grid_for(ngroups, 256), 256, 0, st>>>(f, p, ngroups, l);
-    (void)hipMemcpyAsync(host_words + t, p + ngroups, 4, hipMemcpyDeviceToHost, st);
+  const int small_slot = timing ? g_ktimer->n - 1 : -1;
+  k_tier_count<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, bc, timing ? bm : nullptr);
+  (void)hipMemsetAsync(bc + (size_t)NL * nblk, 0, 4, st);
+  exclusive_scan_u32(bc, boff, (size_t)NL * nblk + 1, ss, st);
+  k_tier_lists<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, boff, list);
+  const TierLists tl{list, boff, nblk};
+  // algorithmic bytes of every tier (timing only): each member's (key, tag)
+  // read, its tag written once at its final slot
+  double members[NTIER] = {};
+  if (timing) {
+    std::vector<uint32_t> h((size_t)NTIER * nblk);
+    (void)hipMemcpyAsync(h.data(), bm, h.size() * 4, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    for (int u = 0; u < NTIER; ++u)
+      for (uint32_t b2 = 0; b2 < nblk; ++b2) members[u] += h[(size_t)u * nblk + b2];
+    g_ktimer->bytes[small_slot] = 16.0 * members[0];
   }
-  (void)hipMemcpyAsync(members, tcount, NTIER * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
-  (void)hipStreamSynchronize(st);
-  uint32_t cnt[NL];
-  for (int t = 0; t < NL; ++t) cnt[t] = host_words[t];
-  // algorithmic bytes of every tier: each member's (key, tag) read, its tag
-  // written once at its final slot
-  if (small_slot >= 0) g_ktimer->bytes[small_slot] = 16.0 * members[0];
-  if (cnt[0]) {
-    kt_begin(st);
-    k_sort_groups_reg<<<grid_for(cnt[0], 4, 16384), 256, 0, st>>>(ls, cnt[0], goff, key, tag,
-                                                                  otag);
-    kt_end(st, KID_SORT_REG, 16.0 * members[1]);
-  }
+  (void)host_words;
+  // fixed grids: every kernel reads its list range on the device
+  kt_begin(st);
+  k_sort_groups_reg<<<4096, 256, 0, st>>>(tl, 1, goff, key, tag, otag);
+  kt_end(st, KID_SORT_REG, 16.0 * members[1]);
   for (int j = 0; j < NLDS; ++j) {
-    const uint32_t n = cnt[1 + j], cap = caps.c[j];
-    if (!n) continue;
-    const uint32_t *l = ls + (1 + j) * g1;
-    const uint32_t grid = n < 16384 ? n : 16384;
+    const uint32_t cap = caps.c[j];
+    const uint32_t grid = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
     kt_begin(st);
     if (narrow_keys)
-      k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), st>>>(l, n, goff, key, tag,
+      k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), st>>>(tl, 2 + j, goff, key, tag,
                                                                        otag, cap);
     else
-      k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), st>>>(l, n, goff, key, tag,
+      k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), st>>>(tl, 2 + j, goff, key, tag,
                                                                        otag, cap);
     kt_end(st, KID_SORT_LDS, 16.0 * members[2 + j]);
   }
-  if (const uint32_t n = cnt[NL - 1]) {
-    kt_begin(st);
-    k_sort_groups_global<<<n < 1024 ? n : 1024, 64, 0, st>>>(ls + (NL - 1) * g1, n, goff, key,
-                                                            tag, otag, pl, pr, bnd, frames);
-    kt_end(st, KID_SORT_GLOBAL, 16.0 * members[NTIER - 1]);
-  }
+  kt_begin(st);
+  k_sort_groups_global<<<1024, 64, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
+                                            frames);
+  kt_end(st, KID_SORT_GLOBAL, 16.0 * members[NTIER - 1]);
 }
 
 }  // namespace rk
