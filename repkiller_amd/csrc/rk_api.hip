@@ -434,7 +434,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
     rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
-                          ctx->host + 128, narrow_keys, st);
+                          ctx->host + 128, narrow_keys, st, ctx->stream2, ctx->fork, ctx->join);
     if (prof) mark(ctx, RK_PH_EMIT);
     rk::emit_result(w.otag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval,
                     out->out_order, st);

@@ -629,9 +629,13 @@ size_t groupsort_scratch_bytes(uint32_t n) {
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
-                       ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st) {
+                       ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
+                       hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
   if (!m) return;
   constexpr int NL = NTIER - 1;  // listed tiers 1..6
+  // groups of <= 64 members (k_sort_small, registers) run on `side`,
+  // concurrently with the LDS tiers
+  hipStream_t s2 = side ? side : st;
   constexpr Caps caps = lds_caps();
   const uint32_t nblk = (ngroups + TCH - 1) / TCH;
   uint32_t *pl = reinterpret_cast<uint32_t *>(scratch);
@@ -645,9 +649,13 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   Frame *frames = reinterpret_cast<Frame *>(
       (reinterpret_cast<uintptr_t>(bm + (size_t)NTIER * nblk) + 63) & ~(uintptr_t)63);
   const bool timing = g_ktimer != nullptr;
-  kt_begin(st);
-  k_sort_small<<<grid_for(m, 256), 256, 0, st>>>(gid_sorted, goff, m, key, tag, otag);
-  kt_end(st, KID_SORT_SMALL, 0.0);  // bytes filled in below from the tier sizes
+  if (side) {
+    (void)hipEventRecord(ev_fork, st);
+    (void)hipStreamWaitEvent(s2, ev_fork, 0);
+  }
+  kt_begin(s2);
+  k_sort_small<<<grid_for(m, 256), 256, 0, s2>>>(gid_sorted, goff, m, key, tag, otag);
+  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in below from the tier sizes
   const int small_slot = timing ? g_ktimer->n - 1 : -1;
   k_tier_count<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, bc, timing ? bm : nullptr);
   (void)hipMemsetAsync(bc + (size_t)NL * nblk, 0, 4, st);
@@ -667,9 +675,14 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   }
   (void)host_words;
   // fixed grids: every kernel reads its list range on the device
-  kt_begin(st);
-  k_sort_groups_reg<<<4096, 256, 0, st>>>(tl, 1, goff, key, tag, otag);
-  kt_end(st, KID_SORT_REG, 16.0 * members[1]);
+  if (side) {
+    (void)hipEventRecord(ev_fork, st);  // the tier lists are ready
+    (void)hipStreamWaitEvent(s2, ev_fork, 0);
+  }
+  kt_begin(s2);
+  k_sort_groups_reg<<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
+  kt_end(s2, KID_SORT_REG, 16.0 * members[1]);
+  if (side) (void)hipEventRecord(ev_join, s2);
   for (int j = 0; j < NLDS; ++j) {
     const uint32_t cap = caps.c[j];
     const uint32_t grid = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
@@ -686,6 +699,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   k_sort_groups_global<<<1024, 64, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
                                             frames);
   kt_end(st, KID_SORT_GLOBAL, 16.0 * members[NTIER - 1]);
+  if (side) (void)hipStreamWaitEvent(st, ev_join, 0);
 }
 
 }  // namespace rk

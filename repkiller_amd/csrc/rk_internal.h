@@ -198,9 +198,13 @@ size_t groupsort_scratch_bytes(uint32_t n);
 // libstdc++ std::sort of every group's (key, tag) records; sorted tags -> otag.
 // gid_sorted: group id of every record; host_words: >= 16 pinned words;
 // narrow_keys: every key fits 32 bits (LDS tiers stage 4-byte keys).
+// side (optional): a second stream for the tiers of <= 64 members, forked
+// and joined through ev_fork / ev_join.
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
-                       ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st);
+                       ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
+                       hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
+                       hipEvent_t ev_join = nullptr);
 void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
                  const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st);
