@@ -20,6 +20,7 @@
 // next launch (kept rows, work-list sizes, jump convergence, group count).
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>

@@ -86,7 +86,8 @@ size_t radix_scratch_words(uint32_t n);
 // values are input positions.  Inputs must not alias outputs or tmp buffers.
 void radix_sort_pairs(const uint32_t *key_in, const uint32_t *val_in, uint32_t *key_out,
                       uint32_t *val_out, uint32_t *key_tmp, uint32_t *val_tmp, uint32_t n,
-                      int bits, uint32_t *scratch, size_t scratch_words, hipStream_t st);
+                      int bits, uint32_t *scratch, size_t scratch_words, hipStream_t st,
+                      int max_digit = 0);  // widest digit in bits (0: the default)
 
 // ------------------------------------------------------- rk_occupancy.hip --
 struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order

@@ -302,11 +302,12 @@ size_t radix_scratch_words(uint32_t n) {
 // the input positions 0..n-1.
 void radix_sort_pairs(const uint32_t *key_in, const uint32_t *val_in, uint32_t *key_out,
                       uint32_t *val_out, uint32_t *key_tmp, uint32_t *val_tmp, uint32_t n,
-                      int bits, uint32_t *scratch, size_t scratch_words, hipStream_t st) {
+                      int bits, uint32_t *scratch, size_t scratch_words, hipStream_t st,
+                      int max_digit) {
   if (n == 0) return;
   if (bits < 1) bits = 1;
   // as few passes as the widest digit allows, widths as even as possible
-  const int maxdb = max_digit_bits();
+  const int maxdb = max_digit >= 8 && max_digit <= MAX_DB ? max_digit : max_digit_bits();
   const int passes = (bits + maxdb - 1) / maxdb;
   const uint32_t tiles = (n + RTILE - 1) / RTILE;
   const size_t cnt = (size_t)tiles * (1u << MAX_DB) + 1;
