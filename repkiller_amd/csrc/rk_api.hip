@@ -11,7 +11,8 @@
 //   3 gather_proc      processing-order SoA + 100-bp bucket keys + sort key
 //   4 counting_sort x2 -> X and Y occupancy CSRs (SequenceOcupationList buckets)
 //   5 sweeps on X, then Y (rk_occupancy.hip) until every fragment is decided;
-//     X hits get their parent from k_x_results, X misses from the Y sweeps
+//     X decisions write X hits' parents and every X result (into the Y
+//     records) as they are made; X misses get their parent from the Y sweeps
 //   6 pointer jumping -> new-group rank (DPP scan) -> gid
 //   7 counting_sort    -> group member lists in processing order
 //   8 sort_groups      libstdc++ introsort per group; 9 emit flags / order
@@ -58,7 +59,7 @@ namespace rk {
 const char *const kKernelNames[KID_COUNT] = {
     "k_prep_keys",     "k_digit_hist",      "k_digit_scatter", "k_gather_proc",
     "k_sort_keys",     "k_csr_fill_x",      "k_run_bounds",    "k_sweep_tile",
-    "k_sweep_fast",    "k_sweep_fast_more", "k_sweep_wave",    "k_x_results",       "k_merge_xres",    "k_csr_fill_y",    "k_jump",
+    "k_sweep_fast",    "k_sweep_fast_more", "k_sweep_wave",    "k_csr_fill_y",    "k_jump",
     "k_assign_gid",    "k_group_offsets",   "k_build_records",
     "k_sort_small",    "k_sort_groups_reg", "k_sort_groups_lds", "k_sort_groups_global",
     "k_emit",
@@ -135,7 +136,6 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.p.xrec = c.take<ulonglong2>(n);
   w.p.yrec = c.take<ulonglong2>(n);
   w.p.ylenhi = c.take<uint32_t>(n);
-  w.p.xres = c.take<uint32_t>(n);
   w.p.ha = c.take<uint64_t>(n);
   w.p.keyx = c.take<uint32_t>(n);
   w.p.keyy = c.take<uint32_t>(n);
@@ -147,7 +147,6 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
     cs->cen = c.take<uint64_t>(n);
     cs->len = c.take<uint64_t>(n);
     cs->state = c.take<uint8_t>(n);
-    cs->win = c.take<uint32_t>(n);
     cs->pk = c.take<uint2>(n);
     cs->nbd = c.take<uint8_t>(n);
   }
@@ -385,19 +384,19 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
 
     // 5: X, then Y (X hits join the Y lists; X misses query Y)
     if (prof) mark(ctx, RK_PH_SWEEP_X);
-    rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state, w.cx.win, nullptr,
+    // X decisions write X results into the Y records and X hits' parents
+    rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state,
+                reinterpret_cast<uint32_t *>(w.p.yrec), w.p.par,
                 w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
                 pq.pos_ratio};
     uint32_t sweeps = 0;
     if ((rc = resolve_axis(ctx, ax, w, ss, fast32, &sweeps))) return rc;
     ctx->stats.x_sweeps = sweeps;
-    // X hits: parent = X winner; X results into the Y records
-    rk::x_results(w.cx, w.p.xres, w.p.yrec, w.p.par, m, w.ctrl, st);
     if (prof) mark(ctx, RK_PH_SWEEP_Y);
     if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
     rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, pl.max_y, st);
     // X misses: the Y sweeps write parent = Y winner, or itself (new group)
-    rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, w.cy.win, w.p.par,
+    rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, nullptr, w.p.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
     if ((rc = resolve_axis(ctx, ay, w, ss, fast32, &sweeps))) return rc;

@@ -130,38 +130,6 @@ __global__ void k_csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t
   }
 }
 
-// X-CSR order is nearly processing order, so these 4-B writes stay local:
-// the X result of every entry, and an X hit's parent (its X winner), which is
-// final (commonFunctions.cpp:55-61)
-__global__ void k_x_results(Csr c, uint32_t *xres, uint32_t *par, uint32_t m, uint32_t *err) {
-  GRID_STRIDE(q, m) {
-    const uint8_t st = c.state[q];
-    if (st != ST_HIT && st != ST_ACTIVE) atomicOr(err, ERRB_INTERNAL);
-    const uint32_t k = c.ent[q];
-    uint32_t xr = NONE;
-    if (st == ST_HIT) {
-      xr = c.win[q];
-      if (xr >= k) {  // winners are always earlier; never let a bad id reach the gathers
-        atomicOr(err, ERRB_INTERNAL);
-        xr = NONE;
-      } else {
-        par[k] = xr;
-      }
-    }
-    xres[k] = xr;
-  }
-}
-
-// the X result joins the Y record (processing order, full-record rewrite), so
-// the Y-ordered gather of k_csr_fill_y is one 16-B read per entry
-__global__ void k_merge_xres(ulonglong2 *yrec, const uint32_t *xres, uint32_t m) {
-  GRID_STRIDE(k, m) {
-    ulonglong2 r = yrec[k];
-    r.y = (r.y & 0xFFFFFFFFull) | (uint64_t)xres[k] << 32;
-    yrec[k] = r;
-  }
-}
-
 // X hits sit in the Y list (commonFunctions.cpp:59); X misses query Y
 __global__ void k_csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
                              uint64_t max_index) {
@@ -271,16 +239,6 @@ void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, h
   k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m, max_index);
   // id + record in; (centre, length,) packed record, neighbour code, state out
   kt_end(st, KID_CSR_FILL_X, (c.cen ? 46.0 : 30.0) * m);
-}
-void x_results(Csr c, uint32_t *xres, ulonglong2 *yrec, uint32_t *par, uint32_t m,
-               uint32_t *err, hipStream_t st) {
-  if (!m) return;
-  kt_begin(st);
-  k_x_results<<<grid_for(m, 256), 256, 0, st>>>(c, xres, par, m, err);
-  kt_end(st, KID_X_RESULTS, 17.0 * m);  // state, winner, id in; X result (+ parent) out
-  kt_begin(st);
-  k_merge_xres<<<grid_for(m, 256), 256, 0, st>>>(yrec, xres, m);
-  kt_end(st, KID_MERGE_XRES, 36.0 * m);  // Y record + X result in, Y record out
 }
 void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
                 uint64_t max_index, hipStream_t st) {

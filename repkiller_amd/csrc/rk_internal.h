@@ -53,7 +53,7 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch
 // DESIGN.md "Kernels and their rooflines").
 enum KernelId : int {
   KID_PREP, KID_HIST, KID_SCATTER, KID_GATHER, KID_SORT_KEYS, KID_CSR_FILL_X, KID_RUN_BOUNDS,
-  KID_SWEEP_TILE, KID_SWEEP_FAST, KID_SWEEP_MORE, KID_SWEEP_WAVE, KID_X_RESULTS, KID_MERGE_XRES, KID_CSR_FILL_Y, KID_JUMP,
+  KID_SWEEP_TILE, KID_SWEEP_FAST, KID_SWEEP_MORE, KID_SWEEP_WAVE, KID_CSR_FILL_Y, KID_JUMP,
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_COUNT
 };
@@ -96,9 +96,10 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   const uint64_t *cen; // centre
   const uint64_t *len; // length
   uint8_t *state;      // ST_*
-  uint32_t *win;       // winner's processing index (valid when ST_HIT; X axis)
-  uint32_t *par;       // Y axis: parent of every entry decided here (X misses), by
-                       // processing index -- Y winner, or itself for a new group
+  uint32_t *xres;      // X axis only: the Y records as 32-bit words; word 4k+3 of
+                       // entry k receives its X result (winner id, or NONE)
+  uint32_t *par;       // parent by processing index: X hits -> X winner; Y axis
+                       // (X misses) -> Y winner, or itself for a new group
   const uint2 *pk;     // {centre low 32, length low 32}: the 32-bit sweep's record
   const uint8_t *nbd;  // neighbour_dir code per entry (0, 1 = -1, 2 = +1)
   uint32_t *rlen_at;   // run length, stored at each run's first position
@@ -140,8 +141,7 @@ struct Proc {  // processing-order working set
   uint32_t *row;   // proc -> file row
   ulonglong2 *xrec;  // {x centre, length}
   ulonglong2 *yrec;  // {y centre, length low 32 | X result << 32} (X result: X winner or
-                     // NONE, merged in by x_results)
-  uint32_t *xres;    // X result per fragment
+                     // NONE, written by the X sweeps)
   uint32_t *ylenhi;  // length high 32 bits, only when some length >= 2^31 (else null)
   uint64_t *ha;
   uint32_t *keyx, *keyy;
@@ -151,7 +151,6 @@ struct Csr {  // one axis in CSR order (see Axis)
   uint32_t *key, *ent;
   uint64_t *cen, *len;
   uint8_t *state;
-  uint32_t *win;
   uint2 *pk;     // {centre low 32 bits, length low 32 bits} (the 32-bit sweep)
   uint8_t *nbd;  // neighbour bucket probed: 0 none, 1 = B-1, 2 = B+1
 };
@@ -180,8 +179,6 @@ void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, h
 // X results (X-CSR order, i.e. nearly processing order): into the Y records,
 // and the parent of every X hit (its X winner); X misses get theirs from the
 // Y sweeps (Axis::par)
-void x_results(Csr c, uint32_t *xres, ulonglong2 *yrec, uint32_t *par, uint32_t m,
-               uint32_t *err, hipStream_t st);
 // Y axis in CSR order: centre/length, state ACTIVE for X hits (they sit in the
 // Y list) else UNKNOWN
 void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,

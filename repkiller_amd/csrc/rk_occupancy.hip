@@ -104,6 +104,21 @@ __device__ __forceinline__ bool matches(const Query &q, uint64_t oc, uint64_t oL
 __device__ __forceinline__ uint8_t load_state(const uint8_t *s) { return *(const volatile uint8_t *)s; }
 __device__ __forceinline__ void store_state(uint8_t *s, uint8_t v) { *s = v; }
 
+// A final decision (ST_HIT with winner `win`, or ST_ACTIVE) of entry i
+// (processing index).  X axis: the X result goes into i's Y record (winner,
+// or NONE: the entry queries Y next) and a hit's parent is its X winner
+// (commonFunctions.cpp:55-61).  Y axis (X misses): the parent is the Y
+// winner, or i itself -- a new group (:63-76).
+__device__ __forceinline__ void record_decision(const Axis &ax, uint32_t i, uint8_t st,
+                                                uint32_t win) {
+  if (ax.xres) {
+    ax.xres[4 * (size_t)i + 3] = st == ST_HIT ? win : NONE;
+    if (st == ST_HIT) ax.par[i] = win;
+  } else {
+    ax.par[i] = st == ST_HIT ? win : i;
+  }
+}
+
 struct Scan {
   double best;
   uint32_t win;  // CSR position of the best ACTIVE candidate
@@ -369,10 +384,9 @@ __global__ void __launch_bounds__(256) k_sweep_tile(Axis ax, uint8_t *wpend, uin
           }
         }
         if (fs[s].any_active && fs[s].best > best) best = fs[s].best, win = fwin_ent[s];
-        if (ax.par) ax.par[ent[P]] = win;
-        else ax.win[p] = win;
-      } else if (st[s] == ST_ACTIVE && ax.par) {
-        ax.par[ent[P]] = ent[P];  // a Y miss opens a new group
+        record_decision(ax, ent[P], ST_HIT, win);
+      } else if (st[s] == ST_ACTIVE) {
+        record_decision(ax, ent[P], ST_ACTIVE, NONE);
       }
       store_state(&ax.state[p], st[s]);
     }
@@ -678,10 +692,9 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
           }
           if (fs[s].any_active && fs[s].best > best) win = fs[s].win;
         }
-        if (ax.par) ax.par[ent[64 * s + lane]] = win;
-        else ax.win[p] = win;
-      } else if (st[s] == ST_ACTIVE && ax.par) {
-        ax.par[ent[64 * s + lane]] = ent[64 * s + lane];  // a Y miss opens a new group
+        record_decision(ax, ent[64 * s + lane], ST_HIT, win);
+      } else if (st[s] == ST_ACTIVE) {
+        record_decision(ax, ent[64 * s + lane], ST_ACTIVE, NONE);
       }
       store_state(&ax.state[p], st[s]);
     }
@@ -873,12 +886,8 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big
       wave_combine(s);
       const uint8_t ns = decide(s);
       if (lane == 0) {
-        if (ns != st && ax.par) {  // Y axis: final decisions give the parent
-          if (ns == ST_HIT) ax.par[i] = ax.ent[s.win];
-          else if (ns == ST_ACTIVE) ax.par[i] = i;
-        } else if (ns == ST_HIT) {
-          ax.win[t] = ax.ent[s.win];
-        }
+        if (ns != st && (ns == ST_HIT || ns == ST_ACTIVE))
+          record_decision(ax, i, ns, ns == ST_HIT ? ax.ent[s.win] : NONE);
         if (ns != st) store_state(&ax.state[t], ns);
       }
       pending |= ns == ST_UNKNOWN || ns == ST_HIT_PENDING;
