@@ -136,7 +136,7 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.p.xrec = c.take<ulonglong2>(n);
   w.p.yrec = c.take<ulonglong2>(n);
   w.p.ylenhi = c.take<uint32_t>(n);
-  w.p.ha = c.take<uint64_t>(n);
+  w.p.hrec = c.take<ulonglong2>(n);
   w.p.keyx = c.take<uint32_t>(n);
   w.p.keyy = c.take<uint32_t>(n);
   w.p.par = c.take<uint32_t>(n);
@@ -431,12 +431,12 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::radix_sort_pairs(w.p.gid, nullptr, w.sgid, w.gmem, w.tk, w.tv, m,
                          rk::bit_length(G - 1), w.radix, w.radix_words, st);
     rk::group_offsets(w.sgid, m, G, w.goff, st);
-    rk::build_records(w.gmem, w.p.ha, m, w.reckey, w.tag, st);
+    rk::build_records(w.gmem, w.p.hrec, m, w.reckey, w.tag, st);
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
     rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
                           ctx->host + 128, narrow_keys, st, ctx->stream2, ctx->fork, ctx->join);
     if (prof) mark(ctx, RK_PH_EMIT);
-    rk::emit_result(w.otag, w.p.gid, w.goff, w.p.row, m, out->gid, out->repval,
+    rk::emit_result(w.otag, w.sgid, w.goff, w.gmem, m, out->gid, out->repval,
                     out->out_order, st);
     HIPCHK(ctx, hipGetLastError());
     if (prof) mark(ctx, RK_N_PHASES);

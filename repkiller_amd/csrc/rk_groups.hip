@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m, uint32_t 
       d = p.ys[e];
     }
     const uint64_t h = y > d ? y - d : d - y;
-    if (in) p.ha[k] = h;
+    if (in) p.hrec[k] = make_ulonglong2(h, p.row[k]);
     if (__ballot(in && (h >> 32) != 0) && lane == 0) atomicOr(wide, 1u);
   }
 }
@@ -185,24 +185,25 @@ __global__ void k_assign_gid(Proc p, uint32_t m, const uint32_t *newrank) {
   GRID_STRIDE(k, m) p.gid[k] = newrank[p.par[k]];
 }
 
-__global__ void k_build_records(const uint32_t *gmem, const uint64_t *ha, uint32_t m,
+// one 16-B gather per member: sort key and file row; the tag is the member's
+// slot, so the emit below reads the row back from inside its own group
+__global__ void k_build_records(uint32_t *gmem, const ulonglong2 *hrec, uint32_t m,
                                 uint64_t *key, uint32_t *tag) {
   GRID_STRIDE(t, m) {
-    const uint32_t k = gmem[t];
-    key[t] = ha[k];
-    tag[t] = k;
+    const ulonglong2 r = hrec[gmem[t]];
+    key[t] = r.x;
+    tag[t] = t;
+    gmem[t] = (uint32_t)r.y;
   }
 }
 
-__global__ void k_emit(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
-                       const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
+__global__ void k_emit(const uint32_t *otag, const uint32_t *sgid, const uint32_t *goff,
+                       const uint32_t *mrow, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                        uint32_t *out_order) {
   GRID_STRIDE(t, m) {
-    const uint32_t k = tag[t];
-    const uint32_t g = gid_proc[k];
+    const uint32_t g = sgid[t];
     const uint32_t b = goff[g], e = goff[g + 1];
-    const uint32_t r = row[k];
-    out_order[t] = r;
+    out_order[t] = mrow[otag[t]];
     out_gid[t] = g;
     out_rep[t] = e - b == 1 ? 0 : (t == b ? 1 : 2);
   }
@@ -231,7 +232,7 @@ void sort_keys(Proc p, uint32_t m, uint32_t *wide, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
   k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m, wide);
-  kt_end(st, KID_SORT_KEYS, 20.0 * m);  // key + yStart in, sort key out
+  kt_end(st, KID_SORT_KEYS, 32.0 * m);  // key, yStart, row in; (sort key, row) out
 }
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st) {
   if (!m) return;
@@ -267,21 +268,21 @@ void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {
   k_assign_gid<<<grid_for(m, 256), 256, 0, st>>>(p, m, newrank);
   kt_end(st, KID_ASSIGN_GID, 12.0 * m);  // root, root's rank in; gid out
 }
-void build_records(const uint32_t *gmem, const uint64_t *ha, uint32_t m, uint64_t *key,
+void build_records(uint32_t *gmem, const ulonglong2 *hrec, uint32_t m, uint64_t *key,
                    uint32_t *tag, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_build_records<<<grid_for(m, 256), 256, 0, st>>>(gmem, ha, m, key, tag);
-  kt_end(st, KID_BUILD_RECORDS, 24.0 * m);  // member, sort key in; (key, tag) out
+  k_build_records<<<grid_for(m, 256), 256, 0, st>>>(gmem, hrec, m, key, tag);
+  kt_end(st, KID_BUILD_RECORDS, 36.0 * m);  // member, (key, row) in; key, tag, row out
 }
-void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
-                 const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
+void emit_result(const uint32_t *otag, const uint32_t *sgid, const uint32_t *goff,
+                 const uint32_t *mrow, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_emit<<<grid_for(m, 256), 256, 0, st>>>(tag, gid_proc, goff, row, m, out_gid, out_rep,
+  k_emit<<<grid_for(m, 256), 256, 0, st>>>(otag, sgid, goff, mrow, m, out_gid, out_rep,
                                            out_order);
-  kt_end(st, KID_EMIT, 29.0 * m);  // tag, gid, group bounds, row in; gid, flag, order out
+  kt_end(st, KID_EMIT, 29.0 * m);  // slot, gid, group bounds, row in; gid, flag, order out
 }
 
 }  // namespace rk

@@ -143,7 +143,7 @@ struct Proc {  // processing-order working set
   ulonglong2 *yrec;  // {y centre, length low 32 | X result << 32} (X result: X winner or
                      // NONE, written by the X sweeps)
   uint32_t *ylenhi;  // length high 32 bits, only when some length >= 2^31 (else null)
-  uint64_t *ha;
+  ulonglong2 *hrec;  // {in-group sort key, file row}: one gather per member
   uint32_t *keyx, *keyy;
   uint32_t *par, *gid;
 };
@@ -171,14 +171,11 @@ __device__ __forceinline__ int neighbour_dir(uint64_t c, uint64_t max_index) {
 void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, uint32_t *pkey,
                ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st);
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st);
-// in-group sort key |yStart - diag_func[xStart/10]| per fragment (p.ha)
-// in-group sort keys; *wide |= 1 when one of them needs more than 32 bits
+// in-group sort key |yStart - diag_func[xStart/10]| per fragment, with its
+// file row (p.hrec); *wide |= 1 when a key needs more than 32 bits
 void sort_keys(Proc p, uint32_t m, uint32_t *wide, hipStream_t st);
 // X axis in CSR order: centre/length (+ packed record, neighbour code), state UNKNOWN
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st);
-// X results (X-CSR order, i.e. nearly processing order): into the Y records,
-// and the parent of every X hit (its X winner); X misses get theirs from the
-// Y sweeps (Axis::par)
 // Y axis in CSR order: centre/length, state ACTIVE for X hits (they sit in the
 // Y list) else UNKNOWN
 void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
@@ -189,7 +186,9 @@ void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st);
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st);
-void build_records(const uint32_t *gmem, const uint64_t *ha, uint32_t m, uint64_t *key,
+// members (gmem, processing ids, group-major) -> sort keys, tags = member
+// slots, and the members' file rows IN PLACE of gmem
+void build_records(uint32_t *gmem, const ulonglong2 *hrec, uint32_t m, uint64_t *key,
                    uint32_t *tag, hipStream_t st);
 // ------------------------------------------------------- rk_groupsort.hip --
 size_t groupsort_scratch_bytes(uint32_t n);
@@ -203,8 +202,10 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
                        ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
                        hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
                        hipEvent_t ev_join = nullptr);
-void emit_result(const uint32_t *tag, const uint32_t *gid_proc, const uint32_t *goff,
-                 const uint32_t *row, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
+// sorted member slots (otag), group of every slot (sgid), group bounds, the
+// members' file rows -> the output columns
+void emit_result(const uint32_t *otag, const uint32_t *sgid, const uint32_t *goff,
+                 const uint32_t *mrow, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st);
 
 }  // namespace rk
