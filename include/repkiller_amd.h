@@ -116,6 +116,82 @@ int rk_classify_device_pairs(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_p
 
 int rk_get_stats(const rk_ctx *ctx, rk_stats *st);
 
+/* ---- ONE fragment set sharded over several GPUs ----------------------
+ *
+ * The reference runs the whole path on one host thread per ratio pair
+ * (repkiller.cpp:60-72 -> execWithParams :80-97).  rk_classify_sharded runs
+ * the same path for ONE fragment set spread over P ranks, one rk_ctx per GPU
+ * (one process or thread each), and produces exactly the output of
+ * rk_classify on the concatenated input: the processing order is partitioned
+ * by xStart/10 ranges (balanced by an all-reduced histogram), the X and Y
+ * occupancy lists by centre-bucket ranges with halo exchanges, group roots are
+ * resolved across ranks, and the in-group order by gid ranges
+ * (DESIGN.md "Multi-GPU").  Collectives go through an rk_comm: RCCL over xGMI
+ * for production, or host callbacks (e.g. torch.distributed gloo) for tests.
+ * Every rank of the comm must call it with the same params.
+ */
+typedef struct rk_comm rk_comm;
+
+#define RK_COMM_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+
+/* Host-callback collectives (buffers are HOST memory; return 0 on success). */
+typedef struct {
+  void *user;
+  /* recv = concatenation over ranks of every rank's `bytes` bytes */
+  int (*allgather)(void *user, const void *send, void *recv, uint64_t bytes);
+  /* rank r's send block for rank q is send_bytes[q] bytes (blocks packed in
+   * rank order); recv receives rank q's block for r, recv_bytes[q] bytes, packed
+   * in rank order */
+  int (*alltoallv)(void *user, const void *send, const uint64_t *send_bytes, void *recv,
+                   const uint64_t *recv_bytes);
+} rk_comm_host_ops;
+
+int rk_comm_create_host(int rank, int size, const rk_comm_host_ops *ops, rk_comm **comm);
+/* RCCL communicator (librccl.so.1 is loaded on first use): rank 0 makes the
+ * id, the caller distributes it (e.g. a torch.distributed broadcast), every
+ * rank then creates its comm on its device. */
+int rk_comm_rccl_id(uint8_t id[RK_COMM_ID_BYTES]);
+int rk_comm_create_rccl(int rank, int size, int device, const uint8_t id[RK_COMM_ID_BYTES],
+                        rk_comm **comm);
+void rk_comm_destroy(rk_comm *comm);
+const char *rk_comm_last_error(const rk_comm *comm);
+
+typedef struct {
+  /* DEVICE arrays owned by the context (valid until its next call), in output
+   * order: this rank's share of the global output, rows
+   * [out_offset, out_offset + n_out) of what rk_classify writes. */
+  const uint32_t *out_order; /* global input row (rank q's rows follow rank q-1's) */
+  const uint32_t *gid;
+  const uint8_t *repval;
+  uint64_t n_out;
+  uint64_t out_offset;
+  uint64_t n_out_total; /* rows of the whole output */
+  uint64_t n_groups;    /* groups of the whole set */
+} rk_shard_result;
+
+typedef struct {
+  uint64_t n_in, n_total;    /* this rank's input rows / all ranks' */
+  uint64_t n_slice;          /* processing-order entries this rank owns */
+  uint64_t x_ghosts;         /* X lead-in entries received from earlier slices */
+  uint64_t y_entries;        /* Y-range entries held (own + halo) */
+  uint32_t x_rounds, y_rounds;   /* halo verification rounds */
+  uint32_t x_reruns, y_reruns;   /* local re-resolutions with owner-fixed halos */
+  uint32_t root_rounds;      /* cross-rank root resolution rounds */
+  uint64_t bytes_sent;       /* payload bytes this rank sent */
+  double ms_total, ms_ingress, ms_x, ms_y, ms_roots, ms_members; /* host wall */
+} rk_shard_stats;
+
+/* in_dev: this rank's block of input rows (device SoA, FILE order); blocks are
+ * consecutive in rank order.  lead_in: halo depth in 100-bp buckets beyond the
+ * probed neighbour (< 0: default 2); any value gives the same output, deeper
+ * halos only make re-resolution rounds rarer. */
+int rk_classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in_dev,
+                        const rk_params *p, int32_t lead_in, rk_shard_result *out);
+int rk_get_shard_stats(const rk_ctx *ctx, rk_shard_stats *st);
+/* Copy a rank's share (n_out rows) into caller buffers (host or device). */
+int rk_shard_copy_result(rk_ctx *ctx, const rk_shard_result *res, uint32_t *out_order,
+                         uint32_t *gid, uint8_t *repval);
+
 /* The in-group ordering primitive on its own: libstdc++ 11 std::sort (the
  * exact permutation, ties included -- commonFunctions.cpp:158) of every
  * segment [seg_off[s], seg_off[s+1]) of `keys`, on the device.  perm[x] =

@@ -46,7 +46,9 @@ EXPORTS = (
     "rk_get_kernel_timing", "rk_kernel_count", "rk_kernel_name",
     "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
     "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
-    "rk_synth_write_csv",
+    "rk_synth_write_csv", "rk_comm_create_host", "rk_comm_rccl_id", "rk_comm_create_rccl",
+    "rk_comm_destroy", "rk_comm_last_error", "rk_classify_sharded", "rk_get_shard_stats",
+    "rk_shard_copy_result",
 )
 
 
@@ -83,6 +85,37 @@ class Stats(ctypes.Structure):
                 ("y_sweeps", ctypes.c_uint32), ("jump_rounds", ctypes.c_uint32),
                 ("x_hits", ctypes.c_uint64), ("y_hits", ctypes.c_uint64),
                 ("device_ms", ctypes.c_double)]
+
+
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_uint64)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_uint64))
+
+
+class CommHostOps(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN),
+                ("alltoallv", ALLTOALLV_FN)]
+
+
+class ShardResult(ctypes.Structure):
+    _fields_ = [("out_order", ctypes.c_void_p), ("gid", ctypes.c_void_p),
+                ("repval", ctypes.c_void_p), ("n_out", ctypes.c_uint64),
+                ("out_offset", ctypes.c_uint64), ("n_out_total", ctypes.c_uint64),
+                ("n_groups", ctypes.c_uint64)]
+
+
+class ShardStats(ctypes.Structure):
+    _fields_ = [("n_in", ctypes.c_uint64), ("n_total", ctypes.c_uint64),
+                ("n_slice", ctypes.c_uint64), ("x_ghosts", ctypes.c_uint64),
+                ("y_entries", ctypes.c_uint64), ("x_rounds", ctypes.c_uint32),
+                ("y_rounds", ctypes.c_uint32), ("x_reruns", ctypes.c_uint32),
+                ("y_reruns", ctypes.c_uint32), ("root_rounds", ctypes.c_uint32),
+                ("bytes_sent", ctypes.c_uint64), ("ms_total", ctypes.c_double),
+                ("ms_ingress", ctypes.c_double), ("ms_x", ctypes.c_double),
+                ("ms_y", ctypes.c_double), ("ms_roots", ctypes.c_double),
+                ("ms_members", ctypes.c_double)]
 
 
 class SynthParams(ctypes.Structure):
@@ -147,6 +180,18 @@ def load_library() -> ctypes.CDLL:
         "rk_synth_generate": (ctypes.c_int, [ctypes.POINTER(SynthParams), vp, vp, vp, vp, vp]),
         "rk_synth_write_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, vp, vp, vp, vp,
                                               vp, ctypes.c_uint64, ctypes.c_uint64]),
+        "rk_comm_create_host": (ctypes.c_int, [ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(CommHostOps), ctypes.POINTER(vp)]),
+        "rk_comm_rccl_id": (ctypes.c_int, [vp]),
+        "rk_comm_create_rccl": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp,
+                                               ctypes.POINTER(vp)]),
+        "rk_comm_destroy": (None, [vp]),
+        "rk_comm_last_error": (ctypes.c_char_p, [vp]),
+        "rk_classify_sharded": (ctypes.c_int, [vp, vp, ctypes.POINTER(FragsSoA),
+                                               ctypes.POINTER(Params), ctypes.c_int32,
+                                               ctypes.POINTER(ShardResult)]),
+        "rk_get_shard_stats": (ctypes.c_int, [vp, ctypes.POINTER(ShardStats)]),
+        "rk_shard_copy_result": (ctypes.c_int, [vp, ctypes.POINTER(ShardResult), vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -429,6 +474,138 @@ class Context:
         if rc != RK_OK:
             raise RkError(rc, self.last_error())
         return int(res.n_out), int(res.n_groups)
+
+
+# ---------------------------------------------------- one set over many GPUs --
+
+class Comm:
+    """rk_comm: the collectives rk_classify_sharded runs on.
+
+    ``Comm.rccl(rank, size, device)`` -- RCCL over xGMI (production); the unique
+    id is broadcast with the default torch.distributed process group.
+    ``Comm.torch_host(rank, size)`` -- host callbacks over the default
+    torch.distributed group (gloo): device blocks are staged through host memory.
+    """
+
+    def __init__(self, handle, rank: int, size: int, keep=None):
+        self._h = handle
+        self.rank, self.size = rank, size
+        self._keep = keep  # ctypes callbacks must outlive the comm
+
+    @classmethod
+    def rccl(cls, rank: int, size: int, device: int) -> "Comm":
+        import torch
+        import torch.distributed as dist
+        lib = load_library()
+        ident = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            _check(lib.rk_comm_rccl_id(ident), "rk_comm_rccl_id")
+        t = torch.tensor(list(bytes(ident)), dtype=torch.uint8)
+        if size > 1:
+            dist.broadcast(t, src=0)
+        ident = (ctypes.c_uint8 * 128)(*t.tolist())
+        h = ctypes.c_void_p()
+        _check(lib.rk_comm_create_rccl(rank, size, device, ident, ctypes.byref(h)),
+               "rk_comm_create_rccl")
+        return cls(h, rank, size)
+
+    @classmethod
+    def torch_host(cls, rank: int, size: int, group=None) -> "Comm":
+        import torch
+        import torch.distributed as dist
+
+        def allgather(_user, send, recv, nbytes):
+            try:
+                src = torch.empty(nbytes, dtype=torch.uint8)
+                if nbytes:
+                    ctypes.memmove(src.data_ptr(), send, nbytes)
+                outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(size)]
+                dist.all_gather(outs, src, group=group)
+                for q, o in enumerate(outs):
+                    if nbytes:
+                        ctypes.memmove(recv + q * nbytes, o.data_ptr(), nbytes)
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported as a status code
+                print(f"rk host allgather failed: {e!r}")
+                return 1
+
+        def alltoallv(_user, send, sb, recv, rb):
+            try:
+                sbl = [int(sb[q]) for q in range(size)]
+                rbl = [int(rb[q]) for q in range(size)]
+                src = torch.empty(sum(sbl), dtype=torch.uint8)
+                if sum(sbl):
+                    ctypes.memmove(src.data_ptr(), send, sum(sbl))
+                dst = torch.empty(sum(rbl), dtype=torch.uint8)
+                dist.all_to_all_single(dst, src, rbl, sbl, group=group)
+                if sum(rbl):
+                    ctypes.memmove(recv, dst.data_ptr(), sum(rbl))
+                return 0
+            except Exception as e:  # noqa: BLE001
+                print(f"rk host alltoallv failed: {e!r}")
+                return 1
+
+        ag, a2a = ALLGATHER_FN(allgather), ALLTOALLV_FN(alltoallv)
+        ops = CommHostOps(None, ag, a2a)
+        h = ctypes.c_void_p()
+        _check(load_library().rk_comm_create_host(rank, size, ctypes.byref(ops),
+                                                  ctypes.byref(h)))
+        return cls(h, rank, size, keep=(ag, a2a, ops))
+
+    def last_error(self) -> str:
+        return load_library().rk_comm_last_error(self._h).decode()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().rk_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class ShardOutput:
+    """This rank's share of the global output: rows [out_offset, out_offset + n_out)."""
+    result: ClassifyResult | None  # host copies (None when not copied)
+    out_offset: int
+    n_out: int
+    n_out_total: int
+    n_groups: int
+    raw: ShardResult
+
+
+def classify_sharded(ctx: "Context", comm: Comm, x, y, length, strand, len_x_hdr: int,
+                     len_y_hdr: int, len_ratio: float = 0.3, pos_ratio: float = 0.3,
+                     lead_in: int = -1, copy: bool = True) -> ShardOutput:
+    """rk_classify_sharded on device tensors holding this rank's block of input rows."""
+    lib = load_library()
+    n = int(x.shape[0])
+    soa = FragsSoA(x.data_ptr(), y.data_ptr(), length.data_ptr(), strand.data_ptr(), n)
+    prm = Params(len_x_hdr, len_y_hdr, len_ratio, pos_ratio)
+    res = ShardResult()
+    rc = lib.rk_classify_sharded(ctx._h, comm._h, ctypes.byref(soa), ctypes.byref(prm),
+                                 lead_in, ctypes.byref(res))
+    if rc != RK_OK:
+        raise RkError(rc, ctx.last_error())
+    out = None
+    if copy:
+        k = int(res.n_out)
+        order, gid, rep = np.empty(k, np.uint32), np.empty(k, np.uint32), np.empty(k, np.uint8)
+        _check(lib.rk_shard_copy_result(ctx._h, ctypes.byref(res), _ptr(order), _ptr(gid),
+                                        _ptr(rep)), ctx.last_error())
+        out = ClassifyResult(gid, rep, order, int(res.n_groups))
+    return ShardOutput(out, int(res.out_offset), int(res.n_out), int(res.n_out_total),
+                       int(res.n_groups), res)
+
+
+def shard_stats(ctx: "Context") -> dict:
+    s = ShardStats()
+    _check(load_library().rk_get_shard_stats(ctx._h, ctypes.byref(s)))
+    return {k: getattr(s, k) for k, _ in ShardStats._fields_}
 
 
 def build(jobs: int = 8) -> None:

@@ -26,34 +26,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/repkiller_amd.h"
-#include "rk_internal.h"
-
-struct rk_ctx {
-  int device = -1;
-  hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;             // Y-axis sort, overlapped with the X sweeps
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  void *ws = nullptr;  // device workspace
-  size_t ws_cap = 0;
-  uint32_t *host = nullptr;  // pinned readback words
-  // device copies for rk_classify (host-buffer entry point)
-  void *io = nullptr;
-  size_t io_cap = 0;
-  rk_stats stats{};
-  std::string err;
-  // phase profiling (rk_set_profiling): one event per phase boundary, on the
-  // context stream, accumulated over calls until rk_reset_phases
-  bool profiling = false;
-  hipEvent_t pev[RK_N_PHASES + 1] = {};
-  bool pev_used[RK_N_PHASES + 1] = {};
-  double phase_ms[RK_N_PHASES] = {};
-  uint32_t phase_calls[RK_N_PHASES] = {};
-  rk::KernelTimer kt{};   // timed launches of the current call
-  double kt_ms[rk::KID_COUNT] = {}, kt_bytes[rk::KID_COUNT] = {};
-  uint64_t kt_launches[rk::KID_COUNT] = {};
-};
+#include "rk_ctx.h"
 
 namespace rk {
 const char *const kKernelNames[KID_COUNT] = {
@@ -66,6 +39,61 @@ const char *const kKernelNames[KID_COUNT] = {
 };
 }  // namespace rk
 
+namespace rk {
+
+int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count) {
+  HIPCHK(ctx, hipMemcpyAsync(ctx->host, dev, count * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return RK_OK;
+}
+
+int err_status(rk_ctx *ctx, uint32_t bits) {
+  if (bits & ERRB_UB_BUCKET) {
+    ctx->err = "xStart/10 >= vsize: the reference indexes FragmentsDatabase out of bounds "
+               "(FragmentsDatabase.cpp:96-97)";
+    return RK_E_UB_BUCKET;
+  }
+  if (bits & ERRB_UB_CENTER) {
+    ctx->err = "a fragment centre probes past an occupancy array "
+               "(SequenceOcupationList.cpp:17,80)";
+    return RK_E_UB_CENTER;
+  }
+  if (bits & ERRB_INTERNAL) {
+    ctx->err = "device consistency check failed";
+    return RK_E_INTERNAL;
+  }
+  return RK_OK;
+}
+
+// run sweeps on one axis until no bucket has undecided entries
+int resolve_axis(rk_ctx *ctx, const Axis &ax, SweepScratch sc, bool fast32, uint32_t *sweeps) {
+  uint32_t *counters = sc.counters;
+  uint8_t *rpend = sc.rpend;
+  RunList rl{sc.runs, sc.wpend, 0, 0, fast32, nullptr};
+  build_runs(ax, rl, sc.dev_count, ctx->host + 128, ctx->stream);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));
+  *sweeps = 0;
+  for (;;) {
+    if (*sweeps > ax.m + 2) {
+      ctx->err = "occupancy sweeps did not converge";
+      return RK_E_INTERNAL;
+    }
+    occupancy_sweep(ax, rl, rpend, counters, *sweeps == 0, ctx->stream);
+    HIPCHK(ctx, hipGetLastError());
+    ++*sweeps;
+    int rc = readback(ctx, counters, PEND_WORDS);
+    if (rc) return rc;
+    uint64_t pending = 0;
+    for (uint32_t k = 0; k < PEND_WORDS; ++k) pending += ctx->host[k];
+    if (!pending) break;
+  }
+  return RK_OK;
+}
+
+}  // namespace rk
+
 static const char *kPhaseNames[RK_N_PHASES] = {
     "prep_keys",      "order_csr",  "gather_proc", "occupancy_csr", "sweep_x", "sweep_y",
     "group_roots",    "member_csr", "group_sort",  "emit",
@@ -73,29 +101,10 @@ static const char *kPhaseNames[RK_N_PHASES] = {
 
 namespace {
 
-#define HIPCHK(ctx, call)                                                          \
-  do {                                                                             \
-    hipError_t e_ = (call);                                                        \
-    if (e_ != hipSuccess) {                                                        \
-      (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);              \
-      return RK_E_HIP;                                                             \
-    }                                                                              \
-  } while (0)
-
-constexpr size_t ALIGN = 256;
-inline size_t align_up(size_t v) { return (v + ALIGN - 1) & ~(ALIGN - 1); }
-
-// bump allocator over the workspace (sizes first, then pointers)
-struct Carve {
-  char *base;
-  size_t off = 0;
-  template <class T>
-  T *take(size_t count) {
-    T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
-    off += align_up(count * sizeof(T) + 16);  // +16: uint4 tails of the scan
-    return p;
-  }
-};
+using rk::align_up;
+using rk::Carve;
+using rk::readback;
+using rk::err_status;
 
 struct Plan {
   uint64_t n, vsize, max_x, max_y;
@@ -189,6 +198,11 @@ int ensure_ws(rk_ctx *ctx, const Plan &pl, Work &w) {
   return RK_OK;
 }
 
+rk::SweepScratch sweep_scratch(const Work &w) {
+  return rk::SweepScratch{w.runs, w.wpend, reinterpret_cast<uint8_t *>(w.rpend), w.ctrl + 64,
+                          w.ctrl + 2};
+}
+
 // mark the START of phase `ph` (ph == RK_N_PHASES marks the end of the last)
 void mark(rk_ctx *ctx, int ph) {
   if (!ctx->profiling) return;
@@ -227,58 +241,6 @@ void collect_phases(rk_ctx *ctx) {
     }
   }
   for (auto &u : ctx->pev_used) u = false;
-}
-
-int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count) {
-  HIPCHK(ctx, hipMemcpyAsync(ctx->host, dev, count * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                             ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-  return RK_OK;
-}
-
-int err_status(rk_ctx *ctx, uint32_t bits) {
-  if (bits & rk::ERRB_UB_BUCKET) {
-    ctx->err = "xStart/10 >= vsize: the reference indexes FragmentsDatabase out of bounds "
-               "(FragmentsDatabase.cpp:96-97)";
-    return RK_E_UB_BUCKET;
-  }
-  if (bits & rk::ERRB_UB_CENTER) {
-    ctx->err = "a fragment centre probes past an occupancy array "
-               "(SequenceOcupationList.cpp:17,80)";
-    return RK_E_UB_CENTER;
-  }
-  if (bits & rk::ERRB_INTERNAL) {
-    ctx->err = "device consistency check failed";
-    return RK_E_INTERNAL;
-  }
-  return RK_OK;
-}
-
-// run sweeps on one axis until no bucket has undecided entries
-int resolve_axis(rk_ctx *ctx, const rk::Axis &ax, Work &w, rk::ScanScratch ss, bool fast32,
-                 uint32_t *sweeps) {
-  uint32_t *counters = w.ctrl + 64;
-  uint8_t *rpend = reinterpret_cast<uint8_t *>(w.rpend);
-  rk::RunList rl{w.runs, w.wpend, 0, 0, fast32, nullptr};
-  rk::build_runs(ax, rl, w.ctrl + 2, ctx->host + 128, ctx->stream);
-  HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));
-  *sweeps = 0;
-  for (;;) {
-    if (*sweeps > ax.m + 2) {
-      ctx->err = "occupancy sweeps did not converge";
-      return RK_E_INTERNAL;
-    }
-    rk::occupancy_sweep(ax, rl, rpend, counters, *sweeps == 0, ctx->stream);
-    HIPCHK(ctx, hipGetLastError());
-    ++*sweeps;
-    int rc = readback(ctx, counters, rk::PEND_WORDS);
-    if (rc) return rc;
-    uint64_t pending = 0;
-    for (uint32_t k = 0; k < rk::PEND_WORDS; ++k) pending += ctx->host[k];
-    if (!pending) break;
-  }
-  return RK_OK;
 }
 
 // All pairs share one fragment set: the ratio-independent part (processing
@@ -390,7 +352,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
                 w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
                 pq.pos_ratio};
     uint32_t sweeps = 0;
-    if ((rc = resolve_axis(ctx, ax, w, ss, fast32, &sweeps))) return rc;
+    if ((rc = rk::resolve_axis(ctx, ax, sweep_scratch(w), fast32, &sweeps))) return rc;
     ctx->stats.x_sweeps = sweeps;
     if (prof) mark(ctx, RK_PH_SWEEP_Y);
     if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
@@ -399,7 +361,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, nullptr, w.p.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
-    if ((rc = resolve_axis(ctx, ay, w, ss, fast32, &sweeps))) return rc;
+    if ((rc = rk::resolve_axis(ctx, ay, sweep_scratch(w), fast32, &sweeps))) return rc;
     ctx->stats.y_sweeps = sweeps;
 
     // 6: group roots and ids
@@ -497,6 +459,8 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->io) (void)hipFree(ctx->io);
+  for (void *p : ctx->pool.ptr)
+    if (p) (void)hipFree(p);
   if (ctx->host) (void)hipHostFree(ctx->host);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

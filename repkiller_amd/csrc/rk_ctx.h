@@ -1,0 +1,91 @@
+// rk_ctx.h -- the context object behind the C ABI and the host-side helpers
+// shared by the single-device driver (rk_api.hip) and the sharded driver
+// (rk_shard.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/repkiller_amd.h"
+#include "rk_internal.h"
+
+// Grow-only device buffers of the sharded driver, one per slot (the exchange
+// sizes are only known mid-call, so they cannot share the single carve).
+struct rk_pool {
+  std::vector<void *> ptr;
+  std::vector<size_t> cap;
+};
+
+struct rk_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;             // Y-axis sort, overlapped with the X sweeps
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  void *ws = nullptr;  // device workspace
+  size_t ws_cap = 0;
+  uint32_t *host = nullptr;  // pinned readback words
+  // device copies for rk_classify (host-buffer entry point)
+  void *io = nullptr;
+  size_t io_cap = 0;
+  rk_pool pool;  // rk_classify_sharded buffers
+  rk_stats stats{};
+  rk_shard_stats shard_stats{};
+  std::string err;
+  // phase profiling (rk_set_profiling): one event per phase boundary, on the
+  // context stream, accumulated over calls until rk_reset_phases
+  bool profiling = false;
+  hipEvent_t pev[RK_N_PHASES + 1] = {};
+  bool pev_used[RK_N_PHASES + 1] = {};
+  double phase_ms[RK_N_PHASES] = {};
+  uint32_t phase_calls[RK_N_PHASES] = {};
+  rk::KernelTimer kt{};   // timed launches of the current call
+  double kt_ms[rk::KID_COUNT] = {}, kt_bytes[rk::KID_COUNT] = {};
+  uint64_t kt_launches[rk::KID_COUNT] = {};
+};
+
+namespace rk {
+
+#define HIPCHK(ctx, call)                                                          \
+  do {                                                                             \
+    hipError_t e_ = (call);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);              \
+      return RK_E_HIP;                                                             \
+    }                                                                              \
+  } while (0)
+
+constexpr size_t ALIGN = 256;
+inline size_t align_up(size_t v) { return (v + ALIGN - 1) & ~(ALIGN - 1); }
+
+// bump allocator over a workspace (sizes first with a null base, then pointers)
+struct Carve {
+  char *base;
+  size_t off = 0;
+  template <class T>
+  T *take(size_t count) {
+    T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
+    off += align_up(count * sizeof(T) + 16);  // +16: uint4 tails of the scan
+    return p;
+  }
+};
+
+// copy `count` device words into ctx->host and wait
+int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count);
+// device error bits (ERRB_*) -> status + message
+int err_status(rk_ctx *ctx, uint32_t bits);
+
+// Device scratch of the occupancy sweeps for an axis of up to m entries.
+struct SweepScratch {
+  uint32_t *runs;      // runs_scratch_words(m)
+  uint8_t *wpend;      // m / 64 + 1
+  uint8_t *rpend;      // m
+  uint32_t *counters;  // PEND_WORDS
+  uint32_t *dev_count; // 1
+};
+// run sweeps on one axis until no bucket has undecided entries
+int resolve_axis(rk_ctx *ctx, const Axis &ax, SweepScratch sc, bool fast32, uint32_t *sweeps);
+
+}  // namespace rk

@@ -1,0 +1,1252 @@
+// rk_shard.hip -- ONE fragment set classified across P GPUs (rk_classify_sharded).
+//
+// Produces exactly what rk_classify writes for the concatenated input
+// (reference: generate_fragment_groups + generate_diagonal_func + sort_groups,
+// commonFunctions.cpp:41-177), with every rank holding a contiguous share of
+// each structure:
+//
+//   ingress     processing order = stable sort by xStart/10 (FragmentsDatabase
+//               buckets, FragmentsDatabase.cpp:84-97); ranks own contiguous
+//               xStart/10 ranges chosen from an all-gathered histogram (the
+//               global coverage histogram) and receive their rows by all-to-all.
+//               Blocks arrive in rank order = file order, so a stable local sort
+//               gives the global processing order; global index = slice offset
+//               + local index.
+//   X axis      a query only sees EARLIER entries (SequenceOcupationList.cpp:33-91
+//               over lists filled in processing order), so slice g needs the
+//               entries of slices < g whose X centre bucket is >= its first
+//               bucket - 1 ("relevant") -- plus a lead-in of `lead_in` more
+//               buckets so that those entries' own decisions come out right
+//               locally.  Each rank resolves [lead-in + own] with the
+//               single-device sweeps, then the owners' final states of the
+//               relevant entries are exchanged and compared; a rank whose halo
+//               disagrees re-resolves with the halo FIXED to the owners' states
+//               (only owner-ACTIVE relevant entries kept: they stay ACTIVE
+//               locally, because the winner rule never lets an ACTIVE entry have
+//               an ACTIVE earlier candidate with positive deviation).  Slice 0
+//               is exact, and after round t slices <= t are, so this ends.
+//   Y axis      X misses query the Y lists (commonFunctions.cpp:63-69); entries
+//               are redistributed to Y-centre-bucket ranges (+ the same lead-in
+//               halo on both sides), arrive in global processing order, and are
+//               resolved and verified like X (halo neighbours on both sides; a
+//               consistent assignment is unique, and the smallest wrong index
+//               increases every round).
+//   roots       parents (X winner, else Y winner, else self) go back to the
+//               slice owners; chains are compressed inside each slice, the
+//               remaining cross-slice links are resolved by request/response
+//               rounds (pointer doubling); gid = global rank of the root among
+//               new groups (slice offsets from an all-gather).
+//   members     (in-group key, file row) records go to gid-range owners, which
+//               run the exact libstdc++ introsort emulation and the emit of the
+//               single-device path on their gid range = a contiguous range of
+//               the global output.
+//
+// Every collective is an all-gather of small host metadata or an all-to-all of
+// device blocks (rk_comm: RCCL send/recv over xGMI, or host callbacks).
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+
+#include "rk_comm.h"
+#include "rk_ctx.h"
+
+namespace rk {
+namespace {
+
+constexpr uint32_t MAXP = 32;
+constexpr uint32_t NBINS = 4096;  // coarse histogram bins (LDS resident)
+
+#define GRID_STRIDE(i, n)                                                      \
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (n);           \
+       i += gridDim.x * blockDim.x)
+
+// owner q holds keys [b[q], b[q+1]); keys >= b[P] belong to nobody
+struct Bounds {
+  uint64_t b[MAXP + 1];
+  uint32_t P;
+};
+__device__ __forceinline__ uint32_t owner_of(const Bounds &B, uint64_t key) {
+  uint32_t lo = 0, hi = B.P;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (B.b[mid] <= key) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------- records --
+struct ShardRow {  // an input row on its way to its slice owner (32 B)
+  uint64_t x, y, len;
+  uint32_t row, strand;
+};
+struct GhostX {  // an X-axis halo entry (24 B)
+  uint64_t xc, len;
+  uint32_t gidx, s;
+};
+struct YRec {  // a Y-axis entry on its way to its Y-range owner (24 B)
+  uint64_t yc, len;
+  uint32_t gidx, flags;  // bit 0: reverse strand, bit 1: X hit
+};
+struct ParRec {
+  uint32_t gidx, par;
+};
+
+// ----------------------------------------------------- partition / exchange --
+// An Op describes, per element i < n, the set of destination ranks (mask) and
+// writes the record bound for rank d at send position pos (emit).  Positions
+// are stable: rank-d records keep element order.
+template <class Op>
+__global__ void __launch_bounds__(256) k_part_count(Op op, uint32_t n, uint32_t P, uint32_t nblk,
+                                                    uint32_t *cnt) {
+  __shared__ uint32_t wc[4][MAXP];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t mask = i < n ? op.mask(i) : 0u;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t d = 0; d < P; ++d) {
+    const uint64_t b = __ballot((mask >> d) & 1u);
+    if (lane == 0) wc[w][d] = (uint32_t)__popcll(b);
+  }
+  __syncthreads();
+  if (threadIdx.x < P) {
+    const uint32_t d = threadIdx.x;
+    cnt[(size_t)d * nblk + blockIdx.x] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
+  }
+}
+
+template <class Op>
+__global__ void __launch_bounds__(256) k_part_scatter(Op op, uint32_t n, uint32_t P,
+                                                      uint32_t nblk, const uint32_t *off) {
+  __shared__ uint32_t wc[4][MAXP];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t mask = i < n ? op.mask(i) : 0u;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint32_t d = 0; d < P; ++d) {
+    const uint64_t b = __ballot((mask >> d) & 1u);
+    if (lane == 0) wc[w][d] = (uint32_t)__popcll(b);
+  }
+  __syncthreads();
+  for (uint32_t d = 0; d < P; ++d) {
+    const uint64_t b = __ballot((mask >> d) & 1u);
+    if ((mask >> d) & 1u) {
+      uint32_t pos = off[(size_t)d * nblk + blockIdx.x] + (uint32_t)__popcll(b & lt);
+      for (uint32_t v = 0; v < w; ++v) pos += wc[v][d];
+      op.emit(i, d, pos);
+    }
+  }
+}
+
+__global__ void k_totals(const uint32_t *off, uint32_t nblk, uint32_t P, uint32_t *tot) {
+  const uint32_t d = threadIdx.x;
+  if (d <= P) tot[d] = off[(size_t)d * nblk];
+}
+
+template <class Op>
+__global__ void __launch_bounds__(256) k_hist(Op op, uint32_t n, uint32_t *hist) {
+  __shared__ uint32_t h[NBINS];
+  for (uint32_t b = threadIdx.x; b < NBINS; b += 256) h[b] = 0;
+  __syncthreads();
+  GRID_STRIDE(i, n) {
+    const uint32_t b = op.bin(i);
+    if (b < NBINS) atomicAdd(&h[b], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < NBINS; b += 256)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// -------------------------------------------------------------------- ops --
+__device__ __forceinline__ uint32_t strand_code(uint64_t s) { return s == 'f' ? 0u : 1u; }
+
+struct RowOp {  // input rows -> slice owners (by xStart/10)
+  const uint32_t *pkey;
+  const ulonglong2 *rec;
+  Bounds B;
+  uint32_t drop, shift, row_base;
+  ShardRow *out;
+  __device__ uint32_t bin(uint32_t i) const {
+    const uint32_t k = pkey[i];
+    return k < drop ? k >> shift : NBINS;
+  }
+  __device__ uint32_t mask(uint32_t i) const {
+    const uint32_t k = pkey[i];
+    return k < drop ? 1u << owner_of(B, k) : 0u;
+  }
+  __device__ void emit(uint32_t i, uint32_t, uint32_t pos) const {
+    const ulonglong2 a = rec[2 * (size_t)i], b = rec[2 * (size_t)i + 1];
+    out[pos] = ShardRow{a.x, a.y, b.x, row_base + i, (uint32_t)b.y};
+  }
+};
+
+// own entries in processing order -> later slices whose lead-in they fall in
+struct GhostOp {
+  const uint32_t *row;
+  const ulonglong2 *rec;
+  uint64_t thr[MAXP];  // lead-in start bucket of every slice (~0: none)
+  uint32_t P, me, poff;
+  GhostX *out;          // records, or
+  uint8_t *sout;        // the entries' X states (1 = ACTIVE), same order
+  const uint32_t *xg;
+  __device__ uint32_t mask(uint32_t k) const {
+    const uint32_t r = row[k];
+    const uint64_t xc = rec[2 * (size_t)r].x + rec[2 * (size_t)r + 1].x / 2;
+    const uint64_t bk = xc / 100;
+    uint32_t m = 0;
+    for (uint32_t g = me + 1; g < P; ++g)
+      if (bk >= thr[g]) m |= 1u << g;
+    return m;
+  }
+  __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
+    if (sout) {
+      sout[pos] = xg[k] == NONE ? 1 : 0;
+      return;
+    }
+    const uint32_t r = row[k];
+    const ulonglong2 a = rec[2 * (size_t)r], b = rec[2 * (size_t)r + 1];
+    out[pos] = GhostX{a.x + b.x / 2, b.x, poff + k, strand_code(b.y)};
+  }
+};
+
+// relevant halo entries the owner calls ACTIVE (the fixed-halo X problem)
+struct SelXOp {
+  const GhostX *gh;
+  const uint8_t *owner_state;
+  uint64_t rel;
+  GhostX *out;
+  __device__ uint32_t mask(uint32_t j) const {
+    return gh[j].xc / 100 >= rel && owner_state[j] ? 1u : 0u;
+  }
+  __device__ void emit(uint32_t j, uint32_t, uint32_t pos) const { out[pos] = gh[j]; }
+};
+
+struct YOp {  // own entries -> Y-range owners (+ their halos)
+  const uint32_t *row;
+  const ulonglong2 *rec;
+  const uint32_t *xg;
+  int64_t lo[MAXP], hi[MAXP];  // halo-extended ranges
+  uint32_t P, poff, shift;
+  YRec *out;
+  __device__ uint64_t yc(uint32_t k, uint64_t *len, uint32_t *s) const {
+    const uint32_t r = row[k];
+    const ulonglong2 a = rec[2 * (size_t)r], b = rec[2 * (size_t)r + 1];
+    *len = b.x;
+    *s = strand_code(b.y);
+    return a.y + b.x / 2;
+  }
+  __device__ uint32_t bin(uint32_t k) const {
+    uint64_t L;
+    uint32_t s;
+    return (uint32_t)((yc(k, &L, &s) / 100) >> shift);
+  }
+  __device__ uint32_t mask(uint32_t k) const {
+    uint64_t L;
+    uint32_t s;
+    const int64_t bk = (int64_t)(yc(k, &L, &s) / 100);
+    uint32_t m = 0;
+    for (uint32_t q = 0; q < P; ++q)
+      if (bk >= lo[q] && bk < hi[q]) m |= 1u << q;
+    return m;
+  }
+  __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
+    uint64_t L;
+    uint32_t s;
+    const uint64_t c = yc(k, &L, &s);
+    out[pos] = YRec{c, L, poff + k, s | (xg[k] != NONE ? 2u : 0u)};
+  }
+};
+
+// Y records held here: own range [lo, hi); relevant halo = buckets lo-1 and hi
+struct YView {
+  const YRec *yr;
+  uint64_t lo, hi;
+  __device__ uint64_t bk(uint32_t r) const { return yr[r].yc / 100; }
+  __device__ bool own(uint32_t r) const {
+    const uint64_t b = bk(r);
+    return b >= lo && b < hi;
+  }
+  __device__ bool rel(uint32_t r) const {
+    const uint64_t b = bk(r);
+    return b + 1 == lo || b == hi;
+  }
+};
+
+struct YStateOp {  // owner side: own entries in a neighbour's relevant halo
+  YView v;
+  uint64_t lo[MAXP], hi[MAXP];  // every rank's own range
+  uint32_t P, me;
+  const uint8_t *ystate;
+  uint8_t *out;
+  __device__ uint32_t mask(uint32_t r) const {
+    if (!v.own(r)) return 0u;
+    const uint64_t b = v.bk(r);
+    uint32_t m = 0;
+    for (uint32_t q = 0; q < P; ++q)
+      if (q != me && (b + 1 == lo[q] || b == hi[q])) m |= 1u << q;
+    return m;
+  }
+  __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const { out[pos] = ystate[r]; }
+};
+
+struct RelOp {  // receiver side: relevant halo entries grouped by owner
+  YView v;
+  Bounds B;
+  uint32_t *out;
+  __device__ uint32_t mask(uint32_t r) const {
+    return v.rel(r) ? 1u << owner_of(B, v.bk(r)) : 0u;
+  }
+  __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const { out[pos] = r; }
+};
+
+struct SelYOp {  // the fixed-halo Y problem: own + relevant halo the owner calls ACTIVE
+  YView v;
+  const uint8_t *used;
+  uint32_t *out;
+  __device__ uint32_t mask(uint32_t r) const {
+    if (v.own(r)) return 1u;
+    return v.rel(r) && ((v.yr[r].flags & 2u) || used[r]) ? 1u : 0u;
+  }
+  __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const { out[pos] = r; }
+};
+
+struct ParOp {  // Y decisions of own X misses -> slice owners
+  YView v;
+  Bounds slices;
+  const uint32_t *ywin;
+  ParRec *out;
+  __device__ uint32_t mask(uint32_t r) const {
+    return v.own(r) && !(v.yr[r].flags & 2u) ? 1u << owner_of(slices, v.yr[r].gidx) : 0u;
+  }
+  __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const {
+    out[pos] = ParRec{v.yr[r].gidx, ywin[r]};
+  }
+};
+
+struct ReqOp {  // unresolved cross-slice roots -> the owner of their current target
+  const uint32_t *lpar, *lab, *cur;
+  Bounds slices;
+  uint32_t *req, *src;
+  __device__ uint32_t mask(uint32_t k) const {
+    return lpar[k] == k && lab[k] == NONE ? 1u << owner_of(slices, cur[k]) : 0u;
+  }
+  __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
+    req[pos] = cur[k];
+    src[pos] = k;
+  }
+};
+
+struct MemOp {  // (in-group key, file row, gid) -> gid-range owners
+  const uint32_t *gid;
+  const ulonglong2 *hrec;
+  const uint32_t *grow;
+  Bounds B;
+  uint32_t shift;
+  ulonglong2 *out;
+  __device__ uint32_t bin(uint32_t k) const { return gid[k] >> shift; }
+  __device__ uint32_t mask(uint32_t k) const { return 1u << owner_of(B, gid[k]); }
+  __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
+    const ulonglong2 h = hrec[k];
+    out[pos] = make_ulonglong2(h.x, (uint64_t)grow[(uint32_t)h.y] | ((uint64_t)gid[k] << 32));
+  }
+};
+
+// ---------------------------------------------------------- small kernels --
+__global__ void k_unpack_rows(const ShardRow *in, uint32_t m, ulonglong2 *rec, uint32_t *pkey,
+                              uint32_t *grow) {
+  GRID_STRIDE(k, m) {
+    const ShardRow r = in[k];
+    rec[2 * (size_t)k] = make_ulonglong2(r.x, r.y);
+    rec[2 * (size_t)k + 1] = make_ulonglong2(r.len, r.strand);
+    pkey[k] = (uint32_t)(r.x / 10);
+    grow[k] = r.row;
+  }
+}
+
+__global__ void k_fill_ghost_x(const GhostX *gh, uint32_t G, ulonglong2 *xrec, uint32_t *keyx,
+                               uint32_t nbx) {
+  GRID_STRIDE(j, G) {
+    const GhostX g = gh[j];
+    xrec[j] = make_ulonglong2(g.xc, g.len);
+    keyx[j] = g.s * nbx + (uint32_t)(g.xc / 100);
+  }
+}
+
+// own X results (local winner ids in the Y records' high words) -> global ids
+__global__ void k_x_own(const ulonglong2 *yrec_own, const GhostX *gh, uint32_t G, uint32_t poff,
+                        uint32_t m, uint32_t *xg) {
+  GRID_STRIDE(k, m) {
+    const uint32_t w = (uint32_t)(yrec_own[k].y >> 32);
+    xg[k] = w == NONE ? NONE : (w < G ? gh[w].gidx : poff + (w - G));
+  }
+}
+
+__global__ void k_x_used(const ulonglong2 *yrec, uint32_t G, uint8_t *used) {
+  GRID_STRIDE(j, G) used[j] = (uint32_t)(yrec[j].y >> 32) == NONE ? 1 : 0;
+}
+
+__device__ __forceinline__ void count_flag(bool f, uint32_t *cnt) {
+  const uint64_t b = __ballot(f);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(cnt, (uint32_t)__popcll(b));
+}
+
+__global__ void k_cmp_x(const GhostX *gh, uint32_t G, uint64_t rel, const uint8_t *used,
+                        const uint8_t *owner, uint32_t *mism) {
+  for (uint32_t base = blockIdx.x * blockDim.x; base < G; base += gridDim.x * blockDim.x) {
+    const uint32_t j = base + threadIdx.x;
+    count_flag(j < G && gh[j].xc / 100 >= rel && used[j] != owner[j], mism);
+  }
+}
+
+__global__ void k_fill_y(const YRec *yr, const uint32_t *ymap, uint32_t c, ulonglong2 *yrec,
+                         uint32_t *ylenhi, uint32_t *keyy, uint32_t nby) {
+  GRID_STRIDE(k, c) {
+    const YRec R = yr[ymap ? ymap[k] : k];
+    const uint64_t hi = (R.flags & 2u) ? 0ull : (uint64_t)NONE;
+    yrec[k] = make_ulonglong2(R.yc, (R.len & 0xFFFFFFFFull) | (hi << 32));
+    if (ylenhi) ylenhi[k] = (uint32_t)(R.len >> 32);
+    keyy[k] = (R.flags & 1u) * nby + (uint32_t)(R.yc / 100);
+  }
+}
+
+__global__ void k_y_results(const YRec *yr, const uint32_t *ymap, uint32_t c,
+                            const uint32_t *par, uint8_t *ystate, uint32_t *ywin) {
+  GRID_STRIDE(k, c) {
+    const uint32_t r = ymap ? ymap[k] : k;
+    if (yr[r].flags & 2u) {
+      ystate[r] = 1;
+      ywin[r] = NONE;
+    } else {
+      const uint32_t p = par[k];
+      ystate[r] = p == k ? 1 : 0;
+      ywin[r] = yr[ymap ? ymap[p] : p].gidx;
+    }
+  }
+}
+
+__global__ void k_cmp_y(const uint32_t *relidx, uint32_t nrel, const uint8_t *used,
+                        const uint8_t *owner, uint32_t *mism) {
+  for (uint32_t base = blockIdx.x * blockDim.x; base < nrel; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    count_flag(i < nrel && used[relidx[i]] != owner[i], mism);
+  }
+}
+
+// used[relidx[i]] = src ? src[i] (owner states) : state[relidx[i]] (own decisions)
+__global__ void k_set_used(const uint32_t *relidx, uint32_t nrel, const uint8_t *src,
+                           const uint8_t *state, uint8_t *used) {
+  GRID_STRIDE(i, nrel) {
+    const uint32_t r = relidx[i];
+    used[r] = src ? src[i] : state[r];
+  }
+}
+
+__global__ void k_par_init(const uint32_t *xg, uint32_t m, uint32_t *par) {
+  GRID_STRIDE(k, m) par[k] = xg[k];
+}
+
+__global__ void k_par_scatter(const ParRec *pr, uint32_t np, uint32_t poff, uint32_t m,
+                              uint32_t *par, uint32_t *err) {
+  GRID_STRIDE(i, np) {
+    const ParRec p = pr[i];
+    const uint32_t k = p.gidx - poff;
+    if (k < m) par[k] = p.par;
+    else atomicOr(err, ERRB_INTERNAL);
+  }
+}
+
+// split parents into the slice-local part (for pointer jumping) and the
+// cross-slice link; roots are the new groups
+__global__ void k_local_par(const uint32_t *par, uint32_t m, uint32_t poff, uint32_t *lpar,
+                            uint32_t *ext, uint32_t *isroot, uint32_t *err) {
+  GRID_STRIDE(k, m) {
+    uint32_t pg = par[k];
+    if (pg == NONE || pg > poff + k) {  // parents are always earlier (or self)
+      atomicOr(err, ERRB_INTERNAL);
+      pg = poff + k;
+    }
+    const bool local = pg >= poff;
+    lpar[k] = local ? pg - poff : k;
+    ext[k] = local ? NONE : pg;
+    isroot[k] = pg == poff + k ? 1u : 0u;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) isroot[m] = 0;
+}
+
+__global__ void k_init_labels(const uint32_t *lpar, const uint32_t *ext, const uint32_t *lrank,
+                              uint32_t goff, uint32_t m, uint32_t *lab, uint32_t *cur) {
+  GRID_STRIDE(k, m) {
+    const bool root = lpar[k] == k;
+    lab[k] = root && ext[k] == NONE ? goff + lrank[k] : NONE;
+    cur[k] = root ? ext[k] : NONE;
+  }
+}
+
+__global__ void k_respond(const uint32_t *rq, uint32_t nq, uint32_t poff, uint32_t m,
+                          const uint32_t *lpar, const uint32_t *lab, const uint32_t *cur,
+                          uint2 *resp, uint32_t *err) {
+  GRID_STRIDE(i, nq) {
+    const uint32_t t = rq[i] - poff;
+    if (t >= m) {
+      atomicOr(err, ERRB_INTERNAL);
+      resp[i] = make_uint2(0, 1);
+      continue;
+    }
+    const uint32_t r = lpar[t];
+    resp[i] = lab[r] != NONE ? make_uint2(lab[r], 1u) : make_uint2(cur[r], 0u);
+  }
+}
+
+__global__ void k_apply(const uint2 *back, const uint32_t *src, uint32_t n, uint32_t *lab,
+                        uint32_t *cur) {
+  GRID_STRIDE(i, n) {
+    const uint2 b = back[i];
+    const uint32_t k = src[i];
+    if (b.y) lab[k] = b.x;
+    else cur[k] = b.x;
+  }
+}
+
+__global__ void k_final_gid(const uint32_t *lpar, const uint32_t *lab, uint32_t m,
+                            uint32_t *gid, uint32_t *err) {
+  GRID_STRIDE(k, m) {
+    const uint32_t g = lab[lpar[k]];
+    if (g == NONE) atomicOr(err, ERRB_INTERNAL);
+    gid[k] = g;
+  }
+}
+
+__global__ void k_mem_keys(const ulonglong2 *mem, uint32_t n, uint32_t g0, uint32_t *lg) {
+  GRID_STRIDE(i, n) lg[i] = (uint32_t)(mem[i].y >> 32) - g0;
+}
+
+__global__ void k_add_u32(uint32_t *a, uint32_t n, uint32_t v) {
+  GRID_STRIDE(i, n) a[i] += v;
+}
+
+// ------------------------------------------------------------- the driver --
+enum Slot : int {
+  SL_CTRL, SL_HIST, SL_PKEY_IN, SL_REC_IN, SL_PCNT, SL_POFF, SL_PSCAN, SL_SEND, SL_ROWS, SL_REC,
+  SL_PKEY2, SL_GROW, SL_PKEY, SL_ROW, SL_TK, SL_TV, SL_RADIX, SL_SCAN, SL_GH, SL_GH2, SL_XREC,
+  SL_YRECF, SL_KEYX, SL_PARF, SL_YS, SL_KEYY, SL_YLENHI, SL_XG, SL_XUSED, SL_XOWN, SL_CKEY,
+  SL_CENT, SL_CCEN, SL_CLEN, SL_CSTATE, SL_CPK, SL_CNBD, SL_RUNS, SL_WPEND, SL_RPEND, SL_RLEN,
+  SL_RBEG, SL_YR, SL_YMAP, SL_YRECL, SL_YLENHIL, SL_KEYYL, SL_PARL, SL_YSTATE, SL_YWIN,
+  SL_YUSED, SL_RELIDX, SL_RYS, SL_PR, SL_PARG, SL_LPAR, SL_EXT, SL_ISROOT, SL_LRANK, SL_JUNK,
+  SL_LAB, SL_CUR, SL_REQ, SL_SRC, SL_RQ, SL_RESP, SL_BACK, SL_HREC, SL_MEM, SL_LG, SL_SGID,
+  SL_GMEM, SL_GOFF, SL_RECKEY, SL_TAG, SL_OTAG, SL_GSORT, SL_OGID, SL_OREP, SL_OORD, SL_COUNT
+};
+
+struct PartPlan {
+  uint32_t n = 0, nblk = 1;
+  uint32_t *off = nullptr;
+  uint64_t cnt[MAXP] = {};
+  uint64_t total = 0;
+};
+
+struct Shard {
+  rk_ctx *ctx;
+  rk_comm *comm;
+  hipStream_t st;
+  uint32_t P, me;
+  uint32_t *ctrl = nullptr;  // [0] err bits, [1] kept, [2] mismatches, [3] jump flag,
+                            // [4] long-run count, [6] wide keys, [64..128) sweep
+                            // counters, [128..161) partition totals
+  uint64_t bytes_sent = 0;
+
+  template <class T>
+  T *take(int slot, size_t count) {
+    rk_pool &pl = ctx->pool;
+    if (pl.ptr.size() < (size_t)SL_COUNT) pl.ptr.resize(SL_COUNT, nullptr), pl.cap.resize(SL_COUNT, 0);
+    const size_t need = align_up(count * sizeof(T) + 16);
+    if (need > pl.cap[slot]) {
+      if (pl.ptr[slot]) (void)hipFree(pl.ptr[slot]);
+      pl.ptr[slot] = nullptr;
+      pl.cap[slot] = 0;
+      if (hipMalloc(&pl.ptr[slot], need) != hipSuccess) {
+        ctx->err = "sharded workspace hipMalloc(" + std::to_string(need) + ") failed";
+        throw RK_E_NOMEM;
+      }
+      pl.cap[slot] = need;
+    }
+    return reinterpret_cast<T *>(pl.ptr[slot]);
+  }
+
+  void check(int rc) {
+    if (rc) throw rc;
+  }
+  void hip(hipError_t e, const char *what) {
+    if (e != hipSuccess) {
+      ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+      throw RK_E_HIP;
+    }
+  }
+  void launched(const char *what) { hip(hipGetLastError(), what); }
+
+  void allgather(const void *mine, void *all, size_t bytes) {
+    if (comm->allgather(mine, all, bytes, st)) {
+      ctx->err = "allgather: " + comm->err;
+      throw RK_E_HIP;
+    }
+  }
+  template <class T>
+  std::vector<T> gather1(T v) {
+    std::vector<T> all(P);
+    allgather(&v, all.data(), sizeof(T));
+    return all;
+  }
+  uint64_t sum_any(uint64_t v) {
+    uint64_t s = 0;
+    for (uint64_t x : gather1<uint64_t>(v)) s += x;
+    return s;
+  }
+  std::vector<uint32_t> d2h(const uint32_t *dev, size_t count) {
+    std::vector<uint32_t> h(count);
+    if (count) {
+      hip(hipMemcpyAsync(h.data(), dev, count * 4, hipMemcpyDeviceToHost, st), "d2h");
+      hip(hipStreamSynchronize(st), "d2h sync");
+    }
+    return h;
+  }
+  uint32_t read1(const uint32_t *dev) { return d2h(dev, 1)[0]; }
+  void zero(void *dev, size_t bytes) {
+    if (bytes) hip(hipMemsetAsync(dev, 0, bytes, st), "memset");
+  }
+
+  ScanScratch scan_scratch(int slot, size_t n) {
+    const size_t cap = scan_blocks(n + 1) + 64;
+    return ScanScratch{take<uint32_t>(slot, cap), cap};
+  }
+
+  template <class Op>
+  void plan(const Op &op, uint32_t n, PartPlan &pp) {
+    pp.n = n;
+    pp.nblk = n ? (n + 255) / 256 : 1;
+    const size_t len = (size_t)P * pp.nblk + 1;
+    uint32_t *cnt = take<uint32_t>(SL_PCNT, len);
+    pp.off = take<uint32_t>(SL_POFF, len);
+    zero(cnt + len - 1, 4);
+    k_part_count<<<pp.nblk, 256, 0, st>>>(op, n, P, pp.nblk, cnt);
+    launched("k_part_count");
+    exclusive_scan_u32(cnt, pp.off, len, scan_scratch(SL_PSCAN, len), st);
+    k_totals<<<1, 64, 0, st>>>(pp.off, pp.nblk, P, ctrl + 128);
+    launched("k_totals");
+    std::vector<uint32_t> t = d2h(ctrl + 128, P + 1);
+    for (uint32_t q = 0; q < P; ++q) pp.cnt[q] = t[q + 1] - t[q];
+    pp.total = t[P];
+  }
+  template <class Op>
+  void emit(const Op &op, const PartPlan &pp) {
+    k_part_scatter<<<pp.nblk, 256, 0, st>>>(op, pp.n, P, pp.nblk, pp.off);
+    launched("k_part_scatter");
+  }
+
+  // all-to-all of records (esz bytes each) laid out by plan pp in `send`;
+  // returns the received count and the per-source counts
+  template <class T>
+  T *exchange(const void *send, const PartPlan &pp, int recv_slot, uint32_t *nrecv,
+              uint64_t *from = nullptr) {
+    const size_t esz = sizeof(T);
+    uint64_t sb[MAXP], rb[MAXP];
+    for (uint32_t q = 0; q < P; ++q) sb[q] = pp.cnt[q] * esz;
+    std::vector<uint64_t> all((size_t)P * P);
+    allgather(sb, all.data(), P * sizeof(uint64_t));
+    uint64_t tot = 0;
+    for (uint32_t q = 0; q < P; ++q) rb[q] = all[(size_t)q * P + me], tot += rb[q];
+    if (tot / esz >= 0xFFFFFFFFull) {
+      ctx->err = "a rank would receive more than 2^32-1 records";
+      throw RK_E_TOO_MANY;
+    }
+    T *recv = take<T>(recv_slot, tot / esz + 1);
+    run_a2a(send, sb, recv, rb);
+    *nrecv = (uint32_t)(tot / esz);
+    if (from)
+      for (uint32_t q = 0; q < P; ++q) from[q] = rb[q] / esz;
+    return recv;
+  }
+  void run_a2a(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb) {
+    for (uint32_t q = 0; q < P; ++q)
+      if (q != me) bytes_sent += sb[q];
+    if (comm->alltoallv(send, sb, recv, rb, st)) {
+      ctx->err = "alltoallv: " + comm->err;
+      throw RK_E_HIP;
+    }
+  }
+
+  // device error bits agreed by every rank
+  void agree_errors() {
+    uint32_t bits = read1(ctrl);
+    uint32_t any = 0;
+    for (uint32_t b : gather1<uint32_t>(bits)) any |= b;
+    check(err_status(ctx, any & ~(uint32_t)ERRB_WIDE_LENGTH));
+  }
+};
+
+uint32_t bin_shift(uint64_t keys) {  // keys in [0, keys) -> < NBINS bins
+  uint32_t s = 0;
+  while (keys > 0 && ((keys - 1) >> s) >= NBINS) ++s;
+  return s;
+}
+
+// balanced ownership bounds over [0, keymax) from a global bin histogram
+Bounds split_bounds(const std::vector<uint64_t> &hist, uint32_t shift, uint64_t keymax,
+                    uint32_t P) {
+  Bounds B{};
+  B.P = P;
+  uint64_t total = 0;
+  for (uint64_t h : hist) total += h;
+  uint64_t acc = 0;
+  size_t bin = 0;
+  B.b[0] = 0;
+  for (uint32_t q = 1; q < P; ++q) {
+    const uint64_t target = (total * q + P - 1) / P;
+    while (bin < hist.size() && acc < target) acc += hist[bin++];
+    uint64_t v = (uint64_t)bin << shift;
+    B.b[q] = v < keymax ? v : keymax;
+  }
+  B.b[P] = keymax;
+  for (uint32_t q = P + 1; q <= MAXP; ++q) B.b[q] = keymax;
+  return B;
+}
+
+template <class Op>
+std::vector<uint64_t> global_hist(Shard &S, const Op &op, uint32_t n) {
+  uint32_t *h = S.take<uint32_t>(SL_HIST, NBINS);
+  S.zero(h, NBINS * 4);
+  if (n) {
+    k_hist<<<grid_for(n, 256, 512), 256, 0, S.st>>>(op, n, h);
+    S.launched("k_hist");
+  }
+  std::vector<uint32_t> mine = S.d2h(h, NBINS);
+  std::vector<uint32_t> all((size_t)S.P * NBINS);
+  S.allgather(mine.data(), all.data(), NBINS * 4);
+  std::vector<uint64_t> g(NBINS, 0);
+  for (uint32_t q = 0; q < S.P; ++q)
+    for (uint32_t b = 0; b < NBINS; ++b) g[b] += all[(size_t)q * NBINS + b];
+  return g;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// One resolved occupancy axis over `n` entries (entry i's record in rec, its
+// bucket key in key).  X: xres = the Y records (winner word), Y: xres null.
+struct AxisIn {
+  const ulonglong2 *rec;  // X: {centre, length}; Y: {centre, length lo | X result << 32}
+  const uint32_t *ylenhi;
+  uint32_t *key;
+  uint32_t *par;
+  uint32_t *xres;
+  uint32_t n, bits;
+  uint64_t max_index;
+  bool is_x, fast32;
+};
+
+uint32_t resolve(Shard &S, const AxisIn &a, const rk_params &p) {
+  const uint32_t n = a.n;
+  if (!n) return 0;
+  Csr c{};
+  c.key = S.take<uint32_t>(SL_CKEY, n);
+  c.ent = S.take<uint32_t>(SL_CENT, n);
+  c.state = S.take<uint8_t>(SL_CSTATE, n);
+  c.pk = S.take<uint2>(SL_CPK, n);
+  c.nbd = S.take<uint8_t>(SL_CNBD, n);
+  c.cen = a.fast32 ? nullptr : S.take<uint64_t>(SL_CCEN, n);
+  c.len = a.fast32 ? nullptr : S.take<uint64_t>(SL_CLEN, n);
+  const size_t rw = radix_scratch_words(n);
+  radix_sort_pairs(a.key, nullptr, c.key, c.ent, S.take<uint32_t>(SL_TK, n),
+                   S.take<uint32_t>(SL_TV, n), n, a.bits, S.take<uint32_t>(SL_RADIX, rw), rw,
+                   S.st);
+  if (a.is_x) csr_fill_x(c, a.rec, n, a.max_index, S.st);
+  else csr_fill_y(c, a.rec, a.ylenhi, n, a.max_index, S.st);
+  S.launched("axis csr");
+  Axis ax{c.key, c.ent, c.cen, c.len, c.state, a.xres, a.par, c.pk, c.nbd,
+          S.take<uint32_t>(SL_RLEN, n), S.take<uint32_t>(SL_RBEG, n), n, a.max_index,
+          p.len_ratio, p.pos_ratio};
+  SweepScratch sc{S.take<uint32_t>(SL_RUNS, runs_scratch_words(n)),
+                  S.take<uint8_t>(SL_WPEND, n / 64 + 1), S.take<uint8_t>(SL_RPEND, n),
+                  S.ctrl + 64, S.ctrl + 4};
+  uint32_t sweeps = 0;
+  S.check(resolve_axis(S.ctx, ax, sc, a.fast32, &sweeps));
+  return sweeps;
+}
+
+int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const rk_params *prm,
+                     int32_t lead_in, rk_shard_result *out) {
+  if (!ctx || !comm || !in || !prm || !out) return RK_E_ARG;
+  if (comm->size < 1 || (uint32_t)comm->size > MAXP) return RK_E_ARG;
+  if (in->n && (!in->x_start || !in->y_start || !in->length || !in->strand)) return RK_E_ARG;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  rk_shard_stats &ss = ctx->shard_stats;
+  std::memset(&ss, 0, sizeof ss);
+  Shard S{ctx, comm, ctx->stream, (uint32_t)comm->size, (uint32_t)comm->rank};
+  const uint32_t P = S.P, me = S.me;
+  const uint64_t H = lead_in < 0 ? 2 : (uint64_t)lead_in;
+  const rk_params p = *prm;
+  const uint64_t len_x = p.len_x_hdr + 1, len_y = p.len_y_hdr + 1;  // FragmentsDatabase.cpp:62,65
+  const uint64_t vsize = 1 + len_x / 10;                             // :84
+  const uint64_t max_x = len_x / 100, max_y = len_y / 100;           // SequenceOcupationList.cpp:4
+  // every rank validates the same arguments, so all return together
+  if (!(p.len_ratio > 0) && !std::isnan(p.len_ratio)) return RK_E_ARG;
+  if (!(p.pos_ratio > 0) && !std::isnan(p.pos_ratio)) return RK_E_ARG;
+  if (vsize - 1 >= 0xFFFFFFF0ull || 2 * (max_x + 1) >= 0xFFFFFFF0ull ||
+      2 * (max_y + 1) >= 0xFFFFFFF0ull) {
+    ctx->err = "sequence length too large for 32-bit bucket ids";
+    return RK_E_ARG;
+  }
+  const uint32_t nbx = (uint32_t)(max_x + 1), nby = (uint32_t)(max_y + 1);
+  const uint32_t drop = (uint32_t)(vsize - 1);  // the never-iterated last bucket
+
+  S.ctrl = S.take<uint32_t>(SL_CTRL, 256);
+  S.zero(S.ctrl, 256 * 4);
+
+  // ---- 0: global row numbering (rank blocks are consecutive in file order)
+  std::vector<uint64_t> nall = S.gather1<uint64_t>(in->n);
+  uint64_t row_base = 0, N = 0;
+  for (uint32_t q = 0; q < P; ++q) N += nall[q], row_base += q < me ? nall[q] : 0;
+  if (N >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
+  const uint32_t nl = (uint32_t)in->n;
+  ss.n_in = nl;
+  ss.n_total = N;
+
+  // ---- 1: processing keys, slice bounds from the global xStart/10 histogram
+  Frags f{in->x_start, in->y_start, in->length, in->strand, nl};
+  uint32_t *pkey_in = S.take<uint32_t>(SL_PKEY_IN, nl + 1);
+  ulonglong2 *rec_in = S.take<ulonglong2>(SL_REC_IN, 2 * (size_t)nl + 2);
+  prep_keys(f, vsize, max_x, max_y, pkey_in, rec_in, S.ctrl + 1, S.ctrl, S.st);
+  S.launched("prep_keys");
+  S.agree_errors();
+  bool fast32 = true;
+  for (uint32_t b : S.gather1<uint32_t>(S.read1(S.ctrl))) fast32 &= !(b & ERRB_WIDE_LENGTH);
+  RowOp rop{pkey_in, rec_in, {}, drop, bin_shift(drop), (uint32_t)row_base, nullptr};
+  const Bounds slice_keys = split_bounds(global_hist(S, rop, nl), rop.shift, drop, P);
+  rop.B = slice_keys;
+
+  // ---- 2: rows -> slice owners; local processing order
+  PartPlan pp;
+  S.plan(rop, nl, pp);
+  rop.out = S.take<ShardRow>(SL_SEND, pp.total + 1);
+  S.emit(rop, pp);
+  uint32_t m = 0;
+  const ShardRow *rows = S.exchange<ShardRow>(rop.out, pp, SL_ROWS, &m);
+  ulonglong2 *rec = S.take<ulonglong2>(SL_REC, 2 * (size_t)m + 2);
+  uint32_t *pkey2 = S.take<uint32_t>(SL_PKEY2, m + 1);
+  uint32_t *grow = S.take<uint32_t>(SL_GROW, m + 1);
+  Proc pr{};
+  pr.rec = rec;
+  pr.pkey = S.take<uint32_t>(SL_PKEY, m + 1);
+  pr.row = S.take<uint32_t>(SL_ROW, m + 1);
+  if (m) {
+    k_unpack_rows<<<grid_for(m, 256), 256, 0, S.st>>>(rows, m, rec, pkey2, grow);
+    S.launched("k_unpack_rows");
+    const size_t rw = radix_scratch_words(m);
+    radix_sort_pairs(pkey2, nullptr, pr.pkey, pr.row, S.take<uint32_t>(SL_TK, m),
+                     S.take<uint32_t>(SL_TV, m), m, bit_length(vsize - 1),
+                     S.take<uint32_t>(SL_RADIX, rw), rw, S.st);
+  }
+  std::vector<uint64_t> mall = S.gather1<uint64_t>(m);
+  uint64_t poff64 = 0, M = 0;
+  for (uint32_t q = 0; q < P; ++q) M += mall[q], poff64 += q < me ? mall[q] : 0;
+  const uint32_t poff = (uint32_t)poff64;
+  Bounds slices{};
+  slices.P = P;
+  for (uint32_t q = 0, acc = 0; q <= MAXP; ++q) {
+    slices.b[q] = acc;
+    if (q < P) acc += (uint32_t)mall[q];
+  }
+  ss.n_slice = m;
+  ss.ms_ingress = ms_since(t0);
+
+  // ---- 3: X lead-in halos from earlier slices
+  const auto tx = std::chrono::steady_clock::now();
+  GhostOp gop{};
+  gop.row = pr.row;
+  gop.rec = rec;
+  gop.P = P;
+  gop.me = me;
+  gop.poff = poff;
+  for (uint32_t g = 0; g < MAXP; ++g) {
+    gop.thr[g] = ~0ull;
+    if (g < P && mall[g]) {
+      const uint64_t bmin = slice_keys.b[g] / 10;  // xStart >= 10*key, centre >= xStart
+      gop.thr[g] = bmin >= 1 + H ? bmin - 1 - H : 0;
+    }
+  }
+  const uint64_t bmin_me = slice_keys.b[me] / 10;
+  const uint64_t rel_x = bmin_me >= 1 ? bmin_me - 1 : 0;  // relevant: probed by own queries
+  S.plan(gop, m, pp);
+  gop.out = S.take<GhostX>(SL_SEND, pp.total + 1);
+  S.emit(gop, pp);
+  uint32_t G = 0;
+  GhostX *gh = S.exchange<GhostX>(gop.out, pp, SL_GH, &G);
+  ss.x_ghosts = G;
+
+  // X problem = [halo (global order)] + own slice; own arrays sit after the halo
+  uint32_t *xg = S.take<uint32_t>(SL_XG, m + 1);
+  uint8_t *xused = S.take<uint8_t>(SL_XUSED, G + 1);
+  pr.ys = S.take<uint64_t>(SL_YS, m + 1);
+  pr.keyy = S.take<uint32_t>(SL_KEYY, m + 1);
+  pr.ylenhi = fast32 ? nullptr : S.take<uint32_t>(SL_YLENHI, m + 1);
+  auto solve_x = [&](const GhostX *halo, uint32_t Gc) {
+    const uint32_t n = Gc + m;
+    ulonglong2 *xrec = S.take<ulonglong2>(SL_XREC, n + 1);
+    ulonglong2 *yrec = S.take<ulonglong2>(SL_YRECF, n + 1);
+    uint32_t *keyx = S.take<uint32_t>(SL_KEYX, n + 1);
+    uint32_t *par = S.take<uint32_t>(SL_PARF, n + 1);
+    if (Gc) {
+      k_fill_ghost_x<<<grid_for(Gc, 256), 256, 0, S.st>>>(halo, Gc, xrec, keyx, nbx);
+      S.launched("k_fill_ghost_x");
+    }
+    Proc q = pr;
+    q.xrec = xrec + Gc;
+    q.yrec = yrec + Gc;
+    q.keyx = keyx + Gc;
+    gather_proc(f, q, m, nbx, nby, S.st);
+    S.launched("gather_proc");
+    AxisIn a{xrec, nullptr, keyx, par, reinterpret_cast<uint32_t *>(yrec), n,
+             (uint32_t)bit_length(2ull * nbx - 1), max_x, true, fast32};
+    resolve(S, a, p);
+    if (m) {
+      k_x_own<<<grid_for(m, 256), 256, 0, S.st>>>(yrec + Gc, halo, Gc, poff, m, xg);
+      S.launched("k_x_own");
+    }
+    return yrec;
+  };
+  {
+    const ulonglong2 *yrec = solve_x(gh, G);
+    if (G) {
+      k_x_used<<<grid_for(G, 256), 256, 0, S.st>>>(yrec, G, xused);
+      S.launched("k_x_used");
+    }
+  }
+  for (;;) {  // verify the relevant halo against its owners' decisions
+    ++ss.x_rounds;
+    if (ss.x_rounds > P + 2) {
+      ctx->err = "X halo verification did not converge";
+      throw RK_E_INTERNAL;
+    }
+    GhostOp sop = gop;
+    sop.out = nullptr;
+    sop.xg = xg;
+    S.plan(sop, m, pp);
+    sop.sout = S.take<uint8_t>(SL_SEND, pp.total + 1);
+    S.emit(sop, pp);
+    uint32_t G2 = 0;
+    uint8_t *xown = S.exchange<uint8_t>(sop.sout, pp, SL_XOWN, &G2);
+    if (G2 != G) {
+      ctx->err = "X halo state count mismatch";
+      throw RK_E_INTERNAL;
+    }
+    S.zero(S.ctrl + 2, 4);
+    if (G) {
+      k_cmp_x<<<grid_for(G, 256, 1024), 256, 0, S.st>>>(gh, G, rel_x, xused, xown, S.ctrl + 2);
+      S.launched("k_cmp_x");
+    }
+    const uint32_t mism = S.read1(S.ctrl + 2);
+    if (S.sum_any(mism) == 0) break;
+    if (mism) {  // re-resolve with the halo fixed to the owners' states
+      ++ss.x_reruns;
+      SelXOp sel{gh, xown, rel_x, nullptr};
+      PartPlan sp;
+      Shard S1 = S;
+      S1.P = 1;
+      S1.me = 0;
+      S1.plan(sel, G, sp);
+      sel.out = S.take<GhostX>(SL_GH2, sp.total + 1);
+      S1.emit(sel, sp);
+      solve_x(sel.out, (uint32_t)sp.total);
+      hipError_t e = hipMemcpyAsync(xused, xown, G, hipMemcpyDeviceToDevice, S.st);
+      S.hip(e, "xused copy");
+    }
+  }
+  ss.ms_x = ms_since(tx);
+
+  // ---- 4: Y axis: entries -> Y-centre-bucket ranges (+ halos)
+  const auto ty = std::chrono::steady_clock::now();
+  YOp yop{};
+  yop.row = pr.row;
+  yop.rec = rec;
+  yop.xg = xg;
+  yop.P = P;
+  yop.poff = poff;
+  yop.shift = bin_shift(nby);
+  const Bounds yb = split_bounds(global_hist(S, yop, m), yop.shift, nby, P);
+  for (uint32_t q = 0; q < MAXP; ++q) {
+    yop.lo[q] = q < P ? (int64_t)yb.b[q] - 1 - (int64_t)H : 0;
+    yop.hi[q] = q < P ? (int64_t)yb.b[q + 1] + 1 + (int64_t)H : 0;
+  }
+  S.plan(yop, m, pp);
+  yop.out = S.take<YRec>(SL_SEND, pp.total + 1);
+  S.emit(yop, pp);
+  uint32_t ny = 0;
+  const YRec *yr = S.exchange<YRec>(yop.out, pp, SL_YR, &ny);
+  ss.y_entries = ny;
+  const YView yv{yr, yb.b[me], yb.b[me + 1]};
+  uint8_t *ystate = S.take<uint8_t>(SL_YSTATE, ny + 1);
+  uint32_t *ywin = S.take<uint32_t>(SL_YWIN, ny + 1);
+  uint8_t *yused = S.take<uint8_t>(SL_YUSED, ny + 1);
+  auto solve_y = [&](const uint32_t *ymap, uint32_t c) {
+    ulonglong2 *yrec = S.take<ulonglong2>(SL_YRECL, c + 1);
+    uint32_t *ylh = fast32 ? nullptr : S.take<uint32_t>(SL_YLENHIL, c + 1);
+    uint32_t *keyy = S.take<uint32_t>(SL_KEYYL, c + 1);
+    uint32_t *par = S.take<uint32_t>(SL_PARL, c + 1);
+    if (!c) return;
+    k_fill_y<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ymap, c, yrec, ylh, keyy, nby);
+    S.launched("k_fill_y");
+    AxisIn a{yrec, ylh, keyy, par, nullptr, c, (uint32_t)bit_length(2ull * nby - 1), max_y, false,
+             fast32};
+    resolve(S, a, p);
+    k_y_results<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ymap, c, par, ystate, ywin);
+    S.launched("k_y_results");
+  };
+  solve_y(nullptr, ny);
+  // relevant halo entries grouped by owner (the order owners send their states in)
+  RelOp relop{yv, yb, nullptr};
+  S.plan(relop, ny, pp);
+  const uint32_t nrel = (uint32_t)pp.total;
+  uint32_t *relidx = S.take<uint32_t>(SL_RELIDX, nrel + 1);
+  relop.out = relidx;
+  S.emit(relop, pp);
+  if (nrel) {
+    k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, nullptr, ystate, yused);
+    S.launched("k_set_used");
+  }
+  YStateOp yso{};
+  yso.v = yv;
+  yso.P = P;
+  yso.me = me;
+  yso.ystate = ystate;
+  for (uint32_t q = 0; q < MAXP; ++q) {
+    yso.lo[q] = q < P ? yb.b[q] : 0;
+    yso.hi[q] = q < P ? yb.b[q + 1] : 0;
+  }
+  for (;;) {
+    ++ss.y_rounds;
+    if (ss.y_rounds > 64) {
+      ctx->err = "Y halo verification did not converge";
+      throw RK_E_INTERNAL;
+    }
+    S.plan(yso, ny, pp);
+    yso.out = S.take<uint8_t>(SL_SEND, pp.total + 1);
+    S.emit(yso, pp);
+    uint32_t n2 = 0;
+    uint8_t *rys = S.exchange<uint8_t>(yso.out, pp, SL_RYS, &n2);
+    if (n2 != nrel) {
+      ctx->err = "Y halo state count mismatch";
+      throw RK_E_INTERNAL;
+    }
+    S.zero(S.ctrl + 2, 4);
+    if (nrel) {
+      k_cmp_y<<<grid_for(nrel, 256, 1024), 256, 0, S.st>>>(relidx, nrel, yused, rys,
+                                                            S.ctrl + 2);
+      S.launched("k_cmp_y");
+    }
+    const uint32_t mism = S.read1(S.ctrl + 2);
+    if (S.sum_any(mism) == 0) break;
+    if (mism) {
+      ++ss.y_reruns;
+      k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, rys, nullptr, yused);
+      S.launched("k_set_used");
+      SelYOp sel{yv, yused, nullptr};
+      Shard S1 = S;
+      S1.P = 1;
+      S1.me = 0;
+      PartPlan sp;
+      S1.plan(sel, ny, sp);
+      sel.out = S.take<uint32_t>(SL_YMAP, sp.total + 1);
+      S1.emit(sel, sp);
+      solve_y(sel.out, (uint32_t)sp.total);
+    }
+  }
+  ss.ms_y = ms_since(ty);
+
+  // ---- 5: parents back to the slice owners; roots; gids
+  const auto tr = std::chrono::steady_clock::now();
+  ParOp pop{yv, slices, ywin, nullptr};
+  S.plan(pop, ny, pp);
+  pop.out = S.take<ParRec>(SL_SEND, pp.total + 1);
+  S.emit(pop, pp);
+  uint32_t npar = 0;
+  const ParRec *prr = S.exchange<ParRec>(pop.out, pp, SL_PR, &npar);
+  uint32_t *parg = S.take<uint32_t>(SL_PARG, m + 1);
+  uint32_t *lpar = S.take<uint32_t>(SL_LPAR, m + 1);
+  uint32_t *ext = S.take<uint32_t>(SL_EXT, m + 1);
+  uint32_t *isroot = S.take<uint32_t>(SL_ISROOT, m + 2);
+  uint32_t *lrank = S.take<uint32_t>(SL_LRANK, m + 2);
+  uint32_t *junk = S.take<uint32_t>(SL_JUNK, m + 1);
+  uint32_t *lab = S.take<uint32_t>(SL_LAB, m + 1);
+  uint32_t *cur = S.take<uint32_t>(SL_CUR, m + 1);
+  if (m) {
+    k_par_init<<<grid_for(m, 256), 256, 0, S.st>>>(xg, m, parg);
+    if (npar)
+      k_par_scatter<<<grid_for(npar, 256), 256, 0, S.st>>>(prr, npar, poff, m, parg, S.ctrl);
+    k_local_par<<<grid_for(m, 256), 256, 0, S.st>>>(parg, m, poff, lpar, ext, isroot, S.ctrl);
+    S.launched("parents");
+    Proc jp{};
+    jp.par = lpar;
+    for (uint32_t rounds = 0;; ++rounds) {
+      if (rounds > 64) {
+        ctx->err = "pointer jumping did not converge";
+        throw RK_E_INTERNAL;
+      }
+      S.zero(S.ctrl + 3, 4);
+      jump_round(jp, m, S.ctrl + 3, rounds == 0 ? junk : nullptr, S.ctrl, S.st);
+      S.launched("jump_round");
+      if (!S.read1(S.ctrl + 3)) break;
+    }
+    exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), S.st);
+  }
+  S.agree_errors();
+  const uint32_t nroots = m ? S.read1(lrank + m) : 0;
+  std::vector<uint64_t> rall = S.gather1<uint64_t>(nroots);
+  uint64_t goff = 0, Gtot = 0;
+  for (uint32_t q = 0; q < P; ++q) Gtot += rall[q], goff += q < me ? rall[q] : 0;
+  if (m) {
+    k_init_labels<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, ext, lrank, (uint32_t)goff, m, lab,
+                                                        cur);
+    S.launched("k_init_labels");
+  }
+  for (;;) {  // cross-slice links: request/response rounds (the owner answers
+              // with its current knowledge, so chains halve every round)
+    ReqOp rq{lpar, lab, cur, slices, nullptr, nullptr};
+    S.plan(rq, m, pp);
+    if (S.sum_any(pp.total) == 0) break;
+    if (++ss.root_rounds > 64) {
+      ctx->err = "cross-slice root resolution did not converge";
+      throw RK_E_INTERNAL;
+    }
+    rq.req = S.take<uint32_t>(SL_REQ, pp.total + 1);
+    rq.src = S.take<uint32_t>(SL_SRC, pp.total + 1);
+    S.emit(rq, pp);
+    uint32_t nq = 0;
+    uint64_t from[MAXP];
+    const uint32_t *rqs = S.exchange<uint32_t>(rq.req, pp, SL_RQ, &nq, from);
+    uint2 *resp = S.take<uint2>(SL_RESP, nq + 1);
+    if (nq) {
+      k_respond<<<grid_for(nq, 256), 256, 0, S.st>>>(rqs, nq, poff, m, lpar, lab, cur, resp,
+                                                      S.ctrl);
+      S.launched("k_respond");
+    }
+    uint64_t sb[MAXP], rb[MAXP];
+    for (uint32_t q = 0; q < P; ++q) sb[q] = from[q] * sizeof(uint2), rb[q] = pp.cnt[q] * sizeof(uint2);
+    uint2 *back = S.take<uint2>(SL_BACK, pp.total + 1);
+    S.run_a2a(resp, sb, back, rb);
+    k_apply<<<grid_for((uint32_t)pp.total, 256), 256, 0, S.st>>>(back, rq.src, (uint32_t)pp.total,
+                                                                  lab, cur);
+    S.launched("k_apply");
+  }
+  uint32_t *gid_own = junk;  // the jump's scratch is free again
+  if (m) {
+    k_final_gid<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, lab, m, gid_own, S.ctrl);
+    S.launched("k_final_gid");
+  }
+  S.agree_errors();
+  ss.ms_roots = ms_since(tr);
+
+  // ---- 6: members -> gid-range owners; exact in-group order; emit
+  const auto tm = std::chrono::steady_clock::now();
+  pr.hrec = S.take<ulonglong2>(SL_HREC, m + 1);
+  S.zero(S.ctrl + 6, 4);
+  sort_keys(pr, m, S.ctrl + 6, S.st);
+  S.launched("sort_keys");
+  bool narrow = true;
+  for (uint32_t w : S.gather1<uint32_t>(S.read1(S.ctrl + 6))) narrow &= w == 0;
+  MemOp mop{gid_own, pr.hrec, grow, {}, bin_shift(Gtot), nullptr};
+  const Bounds gb = split_bounds(global_hist(S, mop, m), mop.shift, Gtot, P);
+  mop.B = gb;
+  S.plan(mop, m, pp);
+  mop.out = S.take<ulonglong2>(SL_SEND, pp.total + 1);
+  S.emit(mop, pp);
+  uint32_t mr = 0;
+  ulonglong2 *mem = S.exchange<ulonglong2>(mop.out, pp, SL_MEM, &mr);
+  const uint32_t g0 = (uint32_t)gb.b[me], Gl = (uint32_t)(gb.b[me + 1] - gb.b[me]);
+  uint32_t *ogid = S.take<uint32_t>(SL_OGID, mr + 1);
+  uint8_t *orep = S.take<uint8_t>(SL_OREP, mr + 1);
+  uint32_t *oord = S.take<uint32_t>(SL_OORD, mr + 1);
+  if (mr) {
+    uint32_t *lg = S.take<uint32_t>(SL_LG, mr + 1);
+    uint32_t *sgid = S.take<uint32_t>(SL_SGID, mr + 1);
+    uint32_t *gmem = S.take<uint32_t>(SL_GMEM, mr + 1);
+    uint32_t *goffs = S.take<uint32_t>(SL_GOFF, (size_t)Gl + 2);
+    uint64_t *reckey = S.take<uint64_t>(SL_RECKEY, mr + 1);
+    uint32_t *tag = S.take<uint32_t>(SL_TAG, mr + 1);
+    uint32_t *otag = S.take<uint32_t>(SL_OTAG, mr + 1);
+    void *gsort = S.take<uint8_t>(SL_GSORT, groupsort_scratch_bytes(mr));
+    k_mem_keys<<<grid_for(mr, 256), 256, 0, S.st>>>(mem, mr, g0, lg);
+    S.launched("k_mem_keys");
+    const size_t rw = radix_scratch_words(mr);
+    radix_sort_pairs(lg, nullptr, sgid, gmem, S.take<uint32_t>(SL_TK, mr),
+                     S.take<uint32_t>(SL_TV, mr), mr, bit_length(Gl ? Gl - 1 : 0),
+                     S.take<uint32_t>(SL_RADIX, rw), rw, S.st);
+    group_offsets(sgid, mr, Gl, goffs, S.st);
+    build_records(gmem, mem, mr, reckey, tag, S.st);
+    sort_groups_exact(sgid, goffs, Gl, mr, reckey, tag, otag, gsort,
+                      S.scan_scratch(SL_SCAN, mr + Gl + 2), ctx->host + 128, narrow, S.st);
+    emit_result(otag, sgid, goffs, gmem, mr, ogid, orep, oord, S.st);
+    if (g0) k_add_u32<<<grid_for(mr, 256), 256, 0, S.st>>>(ogid, mr, g0);
+    S.launched("member order");
+  }
+  std::vector<uint64_t> oall = S.gather1<uint64_t>(mr);
+  uint64_t ooff = 0, otot = 0;
+  for (uint32_t q = 0; q < P; ++q) otot += oall[q], ooff += q < me ? oall[q] : 0;
+  S.hip(hipStreamSynchronize(S.st), "final sync");
+  S.agree_errors();
+  ss.ms_members = ms_since(tm);
+
+  out->out_order = oord;
+  out->gid = ogid;
+  out->repval = orep;
+  out->n_out = mr;
+  out->out_offset = ooff;
+  out->n_out_total = otot;
+  out->n_groups = Gtot;
+  ss.bytes_sent = S.bytes_sent;
+  ss.ms_total = ms_since(t0);
+  ctx->stats = rk_stats{};
+  ctx->stats.n_in = nl;
+  ctx->stats.n_proc = m;
+  ctx->stats.n_groups = Gtot;
+  ctx->stats.device_ms = ss.ms_total;
+  (void)M;
+  return RK_OK;
+}
+
+}  // namespace
+}  // namespace rk
+
+extern "C" int rk_classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in_dev,
+                                   const rk_params *p, int32_t lead_in, rk_shard_result *out) {
+  if (!ctx) return RK_E_ARG;
+  ctx->err.clear();
+  int rc;
+  try {
+    rc = rk::classify_sharded(ctx, comm, in_dev, p, lead_in, out);
+  } catch (int code) {
+    rc = code;
+  } catch (...) {
+    ctx->err = "unexpected C++ exception";
+    rc = RK_E_INTERNAL;
+  }
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  return rc;
+}
+
+extern "C" int rk_get_shard_stats(const rk_ctx *ctx, rk_shard_stats *st) {
+  if (!ctx || !st) return RK_E_ARG;
+  *st = ctx->shard_stats;
+  return RK_OK;
+}
+
+extern "C" int rk_shard_copy_result(rk_ctx *ctx, const rk_shard_result *res, uint32_t *out_order,
+                                    uint32_t *gid, uint8_t *repval) {
+  if (!ctx || !res) return RK_E_ARG;
+  const size_t n = res->n_out;
+  if (!n) return RK_OK;
+  if (!out_order || !gid || !repval) return RK_E_ARG;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipMemcpyAsync(out_order, res->out_order, n * 4, hipMemcpyDefault, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(gid, res->gid, n * 4, hipMemcpyDefault, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(repval, res->repval, n, hipMemcpyDefault, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return RK_OK;
+}

@@ -1,0 +1,66 @@
+"""Rank body of the sharded-classification tests (tests/test_sharded.py).
+
+Every rank rebuilds the same global fragment set, keeps its block of input rows
+(rank r: rows [r*n//P, (r+1)*n//P), the file-order blocks rk_classify_sharded
+expects), runs rk_classify_sharded on cuda:0 (several ranks share the one GPU
+of the test box; collectives are torch.distributed gloo host callbacks) and
+reports its share of the output to the parent.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def load_case(case):
+    import repkiller_amd as rk
+    if case["kind"] == "synth" and case["n"] == 0:
+        import numpy as np
+        e = np.empty(0, np.uint64)
+        return rk.Frags(e, e.copy(), e.copy(), np.empty(0, np.uint8)), case["L"], case["L"]
+    if case["kind"] == "synth":
+        f = rk.synth(case["n"], case["L"], seed=case["seed"], family_frac=case.get("ff", 0.8),
+                     copies=tuple(case.get("copies", (2, 30))))
+        return f, case["L"], case["L"]
+    db = rk.FragmentsDatabase(case["path"])
+    return db.frags, db.len_x_hdr, db.len_y_hdr
+
+
+def worker(rank, world, port, cases, q, comm_kind="host"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import repkiller_amd as rk
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = rk.Context(0)
+        comm = (rk.Comm.rccl(rank, world, 0) if comm_kind == "rccl"
+                else rk.Comm.torch_host(rank, world))
+        for ci, case in enumerate(cases):
+            f, lx, ly = load_case(case)
+            n = f.n
+            a, b = rank * n // world, (rank + 1) * n // world
+            dev = torch.device("cuda:0")
+
+            def t(arr, dt):
+                return torch.from_numpy(arr[a:b].astype(dt, copy=True)).to(dev)
+            x, y = t(f.x_start, "int64"), t(f.y_start, "int64")
+            ln, s = t(f.length, "int64"), t(f.strand, "uint8")
+            try:
+                out = rk.classify_sharded(ctx, comm, x, y, ln, s, lx, ly, case.get("lr", 0.3),
+                                          case.get("pr", 0.3), case.get("lead_in", -1))
+            except rk.RkError as e:
+                q.put((ci, rank, "error", e.code))
+                continue
+            r = out.result
+            q.put((ci, rank, "ok", (out.out_offset, out.n_out_total, out.n_groups,
+                                    r.out_order, r.gid, r.repval, rk.shard_stats(ctx))))
+        comm.close()
+        ctx.close()
+    except Exception:  # noqa: BLE001 -- surfaced to the parent
+        import traceback
+        q.put((-1, rank, "crash", traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,159 @@
+"""ONE fragment set classified across several ranks (rk_classify_sharded).
+
+Parity bar: the concatenation of the ranks' output shares is bit-identical to
+the single-device path on the concatenated input (itself pinned to the oracle
+and the reference's fixtures, tests/test_gpu_parity.py), and to the oracle
+directly for the small sets.  Ranks share the test box's one GPU and exchange
+through torch.distributed gloo (rk_comm host callbacks); the RCCL comm runs the
+same driver and is exercised at world size 1.
+
+Cases cover: ordinary synthetic sets; a dense short genome with lead_in = 0,
+which forces halo disagreements and the fixed-halo re-resolution on both axes;
+tiny and empty inputs (ranks without rows, slices or groups); the reference's
+edge fixtures; out-of-bounds inputs, where every rank must return the same
+error.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import EDGE, edge_cases
+from oracle import rk_oracle as ro
+import shard_worker
+
+import repkiller_amd as rk
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(world, cases, comm_kind="host", timeout=100):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=shard_worker.worker, args=(r, world, port, cases, q, comm_kind))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(world * len(cases)):
+            ci, rank, kind, payload = q.get(timeout=timeout)
+            assert kind != "crash", payload
+            got[(ci, rank)] = (kind, payload)
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    return got
+
+
+def assemble(got, ci, world):
+    parts = []
+    for r in range(world):
+        kind, pl = got[(ci, r)]
+        assert kind == "ok", (r, pl)
+        parts.append(pl)
+    parts.sort(key=lambda t: t[0])
+    total, ngroups = parts[0][1], parts[0][2]
+    off = 0
+    for p in parts:
+        assert p[0] == off and p[1] == total and p[2] == ngroups
+        off += p[3].shape[0]
+    assert off == total
+    cat = lambda i: np.concatenate([p[i] for p in parts]) if parts else np.empty(0)  # noqa: E731
+    return cat(3), cat(4), cat(5), ngroups, [p[6] for p in parts]
+
+
+def reference(gpu_ctx, case):
+    f, lx, ly = shard_worker.load_case(case)
+    return gpu_ctx.classify(f, lx, ly, case.get("lr", 0.3), case.get("pr", 0.3)), f, lx, ly
+
+
+SYNTH = [
+    dict(kind="synth", n=200_000, L=20_000_000, seed=21),
+    dict(kind="synth", n=200_000, L=20_000_000, seed=22, lr=0.05, pr=0.05),
+    dict(kind="synth", n=100_000, L=10_000_000, seed=23, ff=0.95, copies=(100, 600)),
+    # dense: ~40 entries per 100-bp bucket and strand, no lead-in -> reruns
+    dict(kind="synth", n=20_000, L=60_000, seed=24, lead_in=0),
+    dict(kind="synth", n=20_000, L=60_000, seed=25, lead_in=0, lr=1.5, pr=0.7),
+    dict(kind="synth", n=7, L=1_000, seed=26),
+    dict(kind="synth", n=0, L=1_000, seed=27),
+]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_matches_single_device(gpu_ctx, world):
+    got = run_ranks(world, SYNTH)
+    reruns = 0
+    for ci, case in enumerate(SYNTH):
+        order, gid, rep, ng, stats = assemble(got, ci, world)
+        want, f, lx, ly = reference(gpu_ctx, case)
+        assert ng == want.n_groups, case
+        assert np.array_equal(order, want.out_order), case
+        assert np.array_equal(gid, want.gid), case
+        assert np.array_equal(rep, want.repval), case
+        if f.n <= 20_000:  # the oracle directly
+            rc, ogid, orep, oorder, ong = ro.classify(f.x_start, f.y_start, f.length, f.strand,
+                                                      lx, ly, case.get("lr", 0.3),
+                                                      case.get("pr", 0.3))
+            assert rc == 0 and ong == ng
+            assert np.array_equal(order, oorder) and np.array_equal(gid, ogid)
+            assert np.array_equal(rep, orep)
+        if case.get("lead_in") == 0:
+            reruns += sum(s["x_reruns"] + s["y_reruns"] for s in stats)
+    # the dense no-lead-in sets must have exercised the fixed-halo path
+    assert reruns > 0
+
+
+def _edge_cases():
+    out = []
+    for name, case in edge_cases():
+        if case["expect"] == "error:RK_E_COUNT":
+            continue  # a parse error, before classification
+        out.append((name, dict(kind="csv", path=os.path.join(EDGE, name + ".in.csv"),
+                               lr=case["len_ratio"], pr=case["pos_ratio"],
+                               expect=case["expect"])))
+    return out
+
+
+ERR = {"error:RK_E_UB_BUCKET": -4, "error:RK_E_UB_CENTER": -5}
+
+
+def test_sharded_edge_fixtures(gpu_ctx, tmp_path):
+    named = _edge_cases()
+    cases = [c for _, c in named]
+    world = 2
+    got = run_ranks(world, cases)
+    for ci, (name, case) in enumerate(named):
+        if case["expect"] != "ref":
+            for r in range(world):
+                kind, code = got[(ci, r)]
+                assert kind == "error" and code == ERR[case["expect"]], (name, r, kind, code)
+            continue
+        order, gid, rep, ng, _ = assemble(got, ci, world)
+        db = rk.FragmentsDatabase(case["path"])
+        res = rk.ClassifyResult(gid, rep, order, ng)
+        out = tmp_path / f"{name}.csv"
+        db.save_all_frag_pairs(str(out), res)
+        with open(os.path.join(EDGE, name + ".out.csv"), "rb") as f:
+            assert out.read_bytes() == f.read(), name
+
+
+def test_sharded_rccl_single_rank(gpu_ctx):
+    cases = [dict(kind="synth", n=100_000, L=10_000_000, seed=31)]
+    got = run_ranks(1, cases, comm_kind="rccl")
+    order, gid, rep, ng, _ = assemble(got, 0, 1)
+    want, *_ = reference(gpu_ctx, cases[0])
+    assert ng == want.n_groups
+    assert np.array_equal(order, want.out_order) and np.array_equal(gid, want.gid)
+    assert np.array_equal(rep, want.repval)
