@@ -7,10 +7,16 @@ rk_classify_device call: SoA inputs already resident in HBM -> group id, repeat
 flag and output order in HBM (the reference's generate_fragment_groups +
 generate_diagonal_func + sort_groups + repeat flag, commonFunctions.cpp:41-177).
 
-Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one process per GPU,
-each classifying its OWN independent 50M-fragment set (weak scaling, no data-path
-collective -- DESIGN.md "Multi-GPU"); a gloo barrier brackets the timed region and
-the max time over ranks is reported.
+Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one process per GPU.
+`value` (default `--mode replicas`): every rank classifies its OWN independent
+50M-fragment set -- independent comparisons share nothing, so there is no
+data-path collective (weak scaling).  The same run then measures the `sharded`
+leg: ONE fragment set of 50M x N fragments over the 3 Gbp genome (rank r holds
+rows [r*50M, (r+1)*50M); at N=4 this is cfg4's 200M) classified by
+rk_classify_sharded with RCCL all-to-alls over xGMI (xStart/10 slices, X/Y
+halo exchange, cross-slice roots, gid-range member sort; DESIGN.md
+"Multi-GPU").  `--mode sharded` makes that leg the `value`.  A gloo barrier
+brackets every timed region and the max time over ranks is reported.
 
 Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the kernel with the
 most device time per step (algorithmic bytes per launch / HIP-event launch time
@@ -61,7 +67,14 @@ def dist_setup():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        sys.stdout.flush()  # gloo prints its connection banner on stdout: keep it off
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     return rank, world, local
 
 
@@ -146,78 +159,15 @@ def load_traffic(kernel: str):
         return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--len-ratio", type=float, default=0.3)
-    ap.add_argument("--pos-ratio", type=float, default=0.3)
-    args = ap.parse_args()
-
-    rank, world, local = dist_setup()
-    cfg = CONFIGS[args.config]
-    n, L = cfg["n"], cfg["genome_len"]
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    ctx = rk.Context(local)
-
-    f = rk.synth(n, L, seed=rank_seed(rank))  # independent fragment set per rank
-    x = torch.from_numpy(f.x_start.view(np.int64)).to(dev)
-    y = torch.from_numpy(f.y_start.view(np.int64)).to(dev)
-    ln = torch.from_numpy(f.length.view(np.int64)).to(dev)
-    s = torch.from_numpy(f.strand).to(dev)
-    gid = torch.empty(n, dtype=torch.int32, device=dev)
-    rep = torch.empty(n, dtype=torch.uint8, device=dev)
-    order = torch.empty(n, dtype=torch.int32, device=dev)
-    del f
-    torch.cuda.synchronize()
-
-    def step():
-        return ctx.classify_device(x, y, ln, s, gid, rep, order, L, L, args.len_ratio,
-                                   args.pos_ratio)
-
-    for _ in range(args.warmup):
-        step()
-    ctx.set_profiling(True)
-    ctx.reset_phases()
-    torch.cuda.synchronize()
-    barrier(world)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        n_out, n_groups = step()
-    torch.cuda.synchronize()
-    barrier(world)
-    dt = time.perf_counter() - t0
-    ctx.set_profiling(False)
-    frags_total, dt_max = aggregate(world, n, dt)
-    phases = ctx.phases()
-    st = ctx.stats()
-
-    # PCIe-inclusive rate (host buffers in and out), reported beside value, never as it
-    pcie = None
-    if rank == 0 and args.config != "cfg1":
-        fh = rk.Frags(x.cpu().numpy().view(np.uint64), y.cpu().numpy().view(np.uint64),
-                      ln.cpu().numpy().view(np.uint64), s.cpu().numpy())
-        ctx.classify(fh, L, L, args.len_ratio, args.pos_ratio)
-        t1 = time.perf_counter()
-        ctx.classify(fh, L, L, args.len_ratio, args.pos_ratio)
-        pcie = n / (time.perf_counter() - t1)
-
-    if rank != 0:
-        return
-    per_step = {k: v[0] / max(1, v[1]) for k, v in phases.items()}
-    # per-kernel HIP-event timing inside the timed steps (on the library's
-    # stream); the roofline is reported for the kernel with the most device
-    # time per step, whatever it is
-    kt = ctx.kernel_timing()
+def roofline_of(kt: dict, steps: int):
+    """Per-kernel HIP-event timing (inside the timed steps, on the library's
+    stream) -> the `kernels` table and the roofline of the kernel with the most
+    device time per step."""
     kernels = {}
     for name, k in kt.items():
         gbps = k["algo_bytes"] / (k["total_ms"] * 1e-3) / 1e9 if k["total_ms"] and k["algo_bytes"] else None
-        kernels[name] = {"ms_per_step": round(k["total_ms"] / args.steps, 3),
-                         "launches_per_step": round(k["launches"] / args.steps, 2),
+        kernels[name] = {"ms_per_step": round(k["total_ms"] / steps, 3),
+                         "launches_per_step": round(k["launches"] / steps, 2),
                          "algo_GBps": round(gbps, 1) if gbps else None}
     dom = max(kt, key=lambda n: kt[n]["total_ms"])
     d = kt[dom]
@@ -229,10 +179,105 @@ def main():
                 "traffic": load_traffic(dom), "kernel": dom,
                 "algorithmic_bytes_per_launch": round(bytes_per_launch),
                 "launch_ms": round(launch_ms, 4),
-                "launches_per_step": round(d["launches"] / args.steps, 2),
-                "kernel_ms_per_step": round(d["total_ms"] / args.steps, 3)}
+                "launches_per_step": round(d["launches"] / steps, 2),
+                "kernel_ms_per_step": round(d["total_ms"] / steps, 3)}
+    return kernels, roofline
+
+
+def timed(step, args, world, ctx):
+    """W untimed steps, then K timed steps (launch-level profiling on) between
+    barriers + device syncs."""
+    for _ in range(args.warmup):
+        step()
+    ctx.set_profiling(True)
+    ctx.reset_phases()
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    return out, dt
+
+
+def upload(f, dev):
+    return (torch.from_numpy(f.x_start.view(np.int64)).to(dev),
+            torch.from_numpy(f.y_start.view(np.int64)).to(dev),
+            torch.from_numpy(f.length.view(np.int64)).to(dev),
+            torch.from_numpy(f.strand).to(dev))
+
+
+def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
+    """ONE fragment set of n x world rows, rank r holding rows [r*n, (r+1)*n)."""
+    n, L = cfg["n"], cfg["genome_len"]
+    f = rk.synth(n, L, seed=rank_seed(rank))  # this rank's block of the one set
+    x, y, ln, s = upload(f, dev)
+    del f
+    comm = (rk.Comm.rccl(rank, world, local) if args.comm == "rccl"
+            else rk.Comm.torch_host(rank, world))
+
+    def step():
+        return rk.classify_sharded(ctx, comm, x, y, ln, s, L, L, args.len_ratio, args.pos_ratio,
+                                   copy=False)
+
+    out, dt = timed(step, args, world, ctx)
+    frags_total, dt_max = aggregate(world, n, dt)
+    st = rk.shard_stats(ctx)
+    sent = allsum(world, float(st["bytes_sent"]))
+    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps)
+    comm.close()
     value = frags_total * args.steps / dt_max
-    line = {
+    return {
+        "value": round(value, 1), "unit": "fragments/s", "n_gpus": world,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "scaling": "weak",
+        "workload": f"ONE {n * world}-fragment set over a {L} bp genome, sharded "
+                    f"({n} fragments per GPU; N=4 is cfg4's 200M)",
+        "fragments_total": n * world, "comm": args.comm,
+        "hbm_algorithmic_GBps": round(50 * value / 1e9, 3),
+        "roofline": roofline, "kernels": kernels,
+        "shard_rank0": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
+        "exchange_bytes_per_step": round(sent),
+        "groups": out.n_groups, "grouped_fragments": out.n_out_total,
+    }
+
+
+def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
+    """rk_classify_device on this rank's own fragment set (inputs resident in HBM)."""
+    n, L = cfg["n"], cfg["genome_len"]
+    f = rk.synth(n, L, seed=rank_seed(rank))  # independent fragment set per rank
+    x, y, ln, s = upload(f, dev)
+    gid = torch.empty(n, dtype=torch.int32, device=dev)
+    rep = torch.empty(n, dtype=torch.uint8, device=dev)
+    order = torch.empty(n, dtype=torch.int32, device=dev)
+    del f
+
+    def step():
+        return ctx.classify_device(x, y, ln, s, gid, rep, order, L, L, args.len_ratio,
+                                   args.pos_ratio)
+
+    (n_out, n_groups), dt = timed(step, args, world, ctx)
+    frags_total, dt_max = aggregate(world, n, dt)
+    phases = ctx.phases()
+    st = ctx.stats()
+    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps)
+
+    # PCIe-inclusive rate (host buffers in and out), reported beside value, never as it
+    pcie = None
+    if rank == 0 and args.config != "cfg1":
+        fh = rk.Frags(x.cpu().numpy().view(np.uint64), y.cpu().numpy().view(np.uint64),
+                      ln.cpu().numpy().view(np.uint64), s.cpu().numpy())
+        ctx.classify(fh, L, L, args.len_ratio, args.pos_ratio)
+        t1 = time.perf_counter()
+        ctx.classify(fh, L, L, args.len_ratio, args.pos_ratio)
+        pcie = n / (time.perf_counter() - t1)
+
+    per_step = {k: v[0] / max(1, v[1]) for k, v in phases.items()}
+    value = frags_total * args.steps / dt_max
+    return {
         "metric": METRIC,
         "value": round(value, 1),
         "unit": "fragments/s",
@@ -247,7 +292,8 @@ def main():
         "data": f"synthetic (SURVEY.md §8d generator, seed 3+rank, {n} fragments per GPU)",
         "config": {"workload": cfg["desc"], "fragments_per_gpu": n, "genome_bp": L,
                    "len_ratio": args.len_ratio, "pos_ratio": args.pos_ratio,
-                   "parallelism": f"independent fragment sets x{world} (weak)"},
+                   "parallelism": (f"independent fragment sets x{world} (weak)" if world > 1
+                                   else "single GPU")},
         "hbm_algorithmic_GBps": round(50 * value / 1e9, 3),  # 50 B/fragment
         "roofline": roofline,
         "phases_ms": {k: round(v, 3) for k, v in per_step.items()},
@@ -257,8 +303,74 @@ def main():
         "sweeps": {"x": st["x_sweeps"], "y": st["y_sweeps"], "jump_rounds": st["jump_rounds"]},
         "pcie_inclusive_fragments_per_s": round(pcie, 1) if pcie else None,
     }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--len-ratio", type=float, default=0.3)
+    ap.add_argument("--pos-ratio", type=float, default=0.3)
+    ap.add_argument("--mode", default="replicas", choices=["replicas", "sharded"],
+                    help="what `value` measures at N>1 (N=1 is always the single-GPU path "
+                         "unless --mode sharded)")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the sharded leg at N>1")
+    ap.add_argument("--sharded-timeout", type=float, default=240.0,
+                    help="seconds the sharded leg may take before the line is printed without it")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="sharded collectives: RCCL, or gloo host callbacks")
+    args = ap.parse_args()
+
+    rank, world, local = dist_setup()
+    cfg = CONFIGS[args.config]
+    if os.environ.get("RK_BENCH_SAME_GPU"):  # rehearsal: every rank on device 0
+        local = 0
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    ctx = rk.Context(local)
+
+    if args.mode == "sharded":
+        sh = bench_sharded(args, cfg, rank, world, local, dev, ctx)
+        line = {"metric": METRIC, "value": sh["value"], "unit": "fragments/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": sh["ms_per_step"],
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "u64/f64",
+                "data": f"synthetic (SURVEY.md §8d generator; rank r's block seeded 3+r), ONE "
+                        f"fragment set of {sh['fragments_total']} fragments",
+                "config": {"workload": sh["workload"], "fragments_per_gpu": cfg["n"],
+                           "genome_bp": cfg["genome_len"], "len_ratio": args.len_ratio,
+                           "pos_ratio": args.pos_ratio,
+                           "parallelism": f"sharded x{world} ({args.comm})"},
+                "hbm_algorithmic_GBps": sh["hbm_algorithmic_GBps"],
+                "roofline": sh["roofline"], "sharded": sh}
+    else:
+        line = bench_single(args, cfg, rank, world, dev, ctx)
+        if world > 1 and not args.no_sharded:
+            # every rank arms the same watchdog: a stuck collective must not cost the
+            # contract line measured above
+            import threading
+
+            def give_up():
+                if rank == 0:
+                    line["sharded"] = {"error": f"timeout after {args.sharded_timeout} s"}
+                    line["cpu_baseline"] = None
+                    print(json.dumps(line), flush=True)
+                os._exit(0)
+            dog = threading.Timer(args.sharded_timeout, give_up)
+            dog.daemon = True
+            dog.start()
+            try:
+                line["sharded"] = bench_sharded(args, cfg, rank, world, local, dev, ctx)
+            except Exception as e:  # noqa: BLE001 -- reported, the contract line stands
+                line["sharded"] = {"error": repr(e)}
+            dog.cancel()
+    if rank != 0:
+        return
     if not args.no_cpu and world == 1:
-        line["cpu_baseline"] = cpu_baseline(cfg, dt_max)
+        line["cpu_baseline"] = cpu_baseline(cfg, line["ms_per_step"] / 1e3 * args.steps)
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)

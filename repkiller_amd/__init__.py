@@ -505,8 +505,17 @@ class Comm:
             dist.broadcast(t, src=0)
         ident = (ctypes.c_uint8 * 128)(*t.tolist())
         h = ctypes.c_void_p()
-        _check(lib.rk_comm_create_rccl(rank, size, device, ident, ctypes.byref(h)),
-               "rk_comm_create_rccl")
+        # RCCL prints an init banner on stdout: keep stdout for the caller's output
+        import sys
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            rc = lib.rk_comm_create_rccl(rank, size, device, ident, ctypes.byref(h))
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+        _check(rc, "rk_comm_create_rccl")
         return cls(h, rank, size)
 
     @classmethod

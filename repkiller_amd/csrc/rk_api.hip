@@ -41,6 +41,21 @@ const char *const kKernelNames[KID_COUNT] = {
 
 namespace rk {
 
+void collect_kernel_timing(rk_ctx *ctx) {
+  g_ktimer = nullptr;
+  if (ctx->kt.n) (void)hipEventSynchronize(ctx->kt.ev[2 * ctx->kt.n - 1]);
+  for (int i = 0; i < ctx->kt.n; ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, ctx->kt.ev[2 * i], ctx->kt.ev[2 * i + 1]) == hipSuccess) {
+      const int k = ctx->kt.kid[i];
+      ctx->kt_ms[k] += ms;
+      ctx->kt_bytes[k] += ctx->kt.bytes[i];
+      ctx->kt_launches[k]++;
+    }
+  }
+  ctx->kt.n = 0;
+}
+
 int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count) {
   HIPCHK(ctx, hipMemcpyAsync(ctx->host, dev, count * sizeof(uint32_t), hipMemcpyDeviceToHost,
                              ctx->stream));
@@ -216,18 +231,7 @@ void mark(rk_ctx *ctx, int ph) {
 
 void collect_phases(rk_ctx *ctx) {
   if (!ctx->profiling) return;
-  rk::g_ktimer = nullptr;
-  if (ctx->kt.n) (void)hipEventSynchronize(ctx->kt.ev[2 * ctx->kt.n - 1]);
-  for (int i = 0; i < ctx->kt.n; ++i) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, ctx->kt.ev[2 * i], ctx->kt.ev[2 * i + 1]) == hipSuccess) {
-      const int k = ctx->kt.kid[i];
-      ctx->kt_ms[k] += ms;
-      ctx->kt_bytes[k] += ctx->kt.bytes[i];
-      ctx->kt_launches[k]++;
-    }
-  }
-  ctx->kt.n = 0;
+  rk::collect_kernel_timing(ctx);
   (void)hipEventSynchronize(ctx->pev[RK_N_PHASES]);
   for (int ph = 0; ph < RK_N_PHASES; ++ph) {
     if (!ctx->pev_used[ph]) continue;

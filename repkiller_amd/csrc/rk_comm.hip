@@ -13,6 +13,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 
@@ -227,7 +228,9 @@ extern "C" int rk_comm_create_rccl(int rank, int size, int device,
   c->device = device;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
-  if (api.CommInitRank(&c->comm, size, u, rank) != ncclSuccess) {
+  const ncclResult_t r = api.CommInitRank(&c->comm, size, u, rank);
+  std::fflush(stdout);  // RCCL's init banner, while the caller may redirect stdout
+  if (r != ncclSuccess) {
     c->comm = nullptr;
     delete c;
     return RK_E_HIP;

@@ -74,6 +74,8 @@ struct Carve {
 
 // copy `count` device words into ctx->host and wait
 int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count);
+// fold the launches timed during the current call into the per-kernel totals
+void collect_kernel_timing(rk_ctx *ctx);
 // device error bits (ERRB_*) -> status + message
 int err_status(rk_ctx *ctx, uint32_t bits);
 

@@ -179,17 +179,19 @@ struct RowOp {  // input rows -> slice owners (by xStart/10)
   }
 };
 
-// own entries in processing order -> later slices whose lead-in they fall in
+// own entries in processing order -> later slices whose lead-in they fall in.
+// Only a suffix of the slice can reach a later slice (centre <= xStart +
+// longest/2), so the op runs over entries base .. m-1.
 struct GhostOp {
   const uint32_t *row;
   const ulonglong2 *rec;
   uint64_t thr[MAXP];  // lead-in start bucket of every slice (~0: none)
-  uint32_t P, me, poff;
+  uint32_t P, me, poff, base;
   GhostX *out;          // records, or
   uint8_t *sout;        // the entries' X states (1 = ACTIVE), same order
   const uint32_t *xg;
-  __device__ uint32_t mask(uint32_t k) const {
-    const uint32_t r = row[k];
+  __device__ uint32_t mask(uint32_t i) const {
+    const uint32_t r = row[base + i];
     const uint64_t xc = rec[2 * (size_t)r].x + rec[2 * (size_t)r + 1].x / 2;
     const uint64_t bk = xc / 100;
     uint32_t m = 0;
@@ -197,7 +199,8 @@ struct GhostOp {
       if (bk >= thr[g]) m |= 1u << g;
     return m;
   }
-  __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
+  __device__ void emit(uint32_t i, uint32_t, uint32_t pos) const {
+    const uint32_t k = base + i;
     if (sout) {
       sout[pos] = xg[k] == NONE ? 1 : 0;
       return;
@@ -220,39 +223,27 @@ struct SelXOp {
   __device__ void emit(uint32_t j, uint32_t, uint32_t pos) const { out[pos] = gh[j]; }
 };
 
-struct YOp {  // own entries -> Y-range owners (+ their halos)
-  const uint32_t *row;
-  const ulonglong2 *rec;
+struct YOp {  // own entries -> Y-range owners (+ their halos), processing order
+  const ulonglong2 *yrec;  // {centre, length low 32 | ...} (gather_proc)
+  const uint32_t *ylenhi;  // length high 32 bits (null: all lengths < 2^31)
+  const uint32_t *keyy;    // strand * nby + bucket
   const uint32_t *xg;
   int64_t lo[MAXP], hi[MAXP];  // halo-extended ranges
-  uint32_t P, poff, shift;
+  uint32_t P, poff, shift, nby;
   YRec *out;
-  __device__ uint64_t yc(uint32_t k, uint64_t *len, uint32_t *s) const {
-    const uint32_t r = row[k];
-    const ulonglong2 a = rec[2 * (size_t)r], b = rec[2 * (size_t)r + 1];
-    *len = b.x;
-    *s = strand_code(b.y);
-    return a.y + b.x / 2;
-  }
-  __device__ uint32_t bin(uint32_t k) const {
-    uint64_t L;
-    uint32_t s;
-    return (uint32_t)((yc(k, &L, &s) / 100) >> shift);
-  }
+  __device__ uint32_t bin(uint32_t k) const { return (uint32_t)((yrec[k].x / 100) >> shift); }
   __device__ uint32_t mask(uint32_t k) const {
-    uint64_t L;
-    uint32_t s;
-    const int64_t bk = (int64_t)(yc(k, &L, &s) / 100);
+    const int64_t bk = (int64_t)(yrec[k].x / 100);
     uint32_t m = 0;
     for (uint32_t q = 0; q < P; ++q)
       if (bk >= lo[q] && bk < hi[q]) m |= 1u << q;
     return m;
   }
   __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
-    uint64_t L;
-    uint32_t s;
-    const uint64_t c = yc(k, &L, &s);
-    out[pos] = YRec{c, L, poff + k, s | (xg[k] != NONE ? 2u : 0u)};
+    const ulonglong2 a = yrec[k];
+    const uint64_t L = (a.y & 0xFFFFFFFFull) | (ylenhi ? (uint64_t)ylenhi[k] << 32 : 0ull);
+    const uint32_t s = keyy[k] >= nby ? 1u : 0u;
+    out[pos] = YRec{a.x, L, poff + k, s | (xg[k] != NONE ? 2u : 0u)};
   }
 };
 
@@ -352,14 +343,32 @@ struct MemOp {  // (in-group key, file row, gid) -> gid-range owners
 
 // ---------------------------------------------------------- small kernels --
 __global__ void k_unpack_rows(const ShardRow *in, uint32_t m, ulonglong2 *rec, uint32_t *pkey,
-                              uint32_t *grow) {
+                              uint32_t *grow, unsigned long long *maxlen) {
+  uint64_t lmax = 0;
   GRID_STRIDE(k, m) {
     const ShardRow r = in[k];
     rec[2 * (size_t)k] = make_ulonglong2(r.x, r.y);
     rec[2 * (size_t)k + 1] = make_ulonglong2(r.len, r.strand);
     pkey[k] = (uint32_t)(r.x / 10);
     grow[k] = r.row;
+    lmax = r.len > lmax ? r.len : lmax;
   }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(lmax, off);
+    lmax = o > lmax ? o : lmax;
+  }
+  if ((threadIdx.x & 63) == 0 && lmax) atomicMax(maxlen, (unsigned long long)lmax);
+}
+
+// first k with key[k] >= v (key ascending)
+__global__ void k_lower_bound(const uint32_t *key, uint32_t m, uint64_t v, uint32_t *out) {
+  uint32_t lo = 0, hi = m;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (key[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  *out = lo;
 }
 
 __global__ void k_fill_ghost_x(const GhostX *gh, uint32_t G, ulonglong2 *xrec, uint32_t *keyx,
@@ -797,6 +806,10 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   const uint32_t nbx = (uint32_t)(max_x + 1), nby = (uint32_t)(max_y + 1);
   const uint32_t drop = (uint32_t)(vsize - 1);  // the never-iterated last bucket
 
+  if (ctx->profiling) {  // launch-level timing of the pipeline kernels (rk_get_kernel_timing)
+    ctx->kt.n = 0;
+    g_ktimer = &ctx->kt;
+  }
   S.ctrl = S.take<uint32_t>(SL_CTRL, 256);
   S.zero(S.ctrl, 256 * 4);
 
@@ -837,7 +850,8 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   pr.pkey = S.take<uint32_t>(SL_PKEY, m + 1);
   pr.row = S.take<uint32_t>(SL_ROW, m + 1);
   if (m) {
-    k_unpack_rows<<<grid_for(m, 256), 256, 0, S.st>>>(rows, m, rec, pkey2, grow);
+    k_unpack_rows<<<grid_for(m, 256), 256, 0, S.st>>>(
+        rows, m, rec, pkey2, grow, reinterpret_cast<unsigned long long *>(S.ctrl + 10));
     S.launched("k_unpack_rows");
     const size_t rw = radix_scratch_words(m);
     radix_sort_pairs(pkey2, nullptr, pr.pkey, pr.row, S.take<uint32_t>(SL_TK, m),
@@ -872,9 +886,25 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
       gop.thr[g] = bmin >= 1 + H ? bmin - 1 - H : 0;
     }
   }
+  {  // the suffix of the slice whose centres can reach a later slice's lead-in
+    uint64_t thr_min = ~0ull;
+    for (uint32_t g = me + 1; g < P; ++g) thr_min = gop.thr[g] < thr_min ? gop.thr[g] : thr_min;
+    uint32_t k0 = m;
+    if (thr_min != ~0ull && m) {
+      const std::vector<uint32_t> lw = S.d2h(S.ctrl + 10, 2);
+      const uint64_t half = ((uint64_t)lw[0] | ((uint64_t)lw[1] << 32)) / 2;
+      const uint64_t reach = thr_min * 100;  // centre >= reach is needed
+      const uint64_t key0 = reach > half + 10 ? (reach - half) / 10 - 1 : 0;
+      k_lower_bound<<<1, 1, 0, S.st>>>(pr.pkey, m, key0, S.ctrl + 12);
+      S.launched("k_lower_bound");
+      k0 = S.read1(S.ctrl + 12);
+    }
+    gop.base = k0;
+  }
+  const uint32_t nsuf = m - gop.base;
   const uint64_t bmin_me = slice_keys.b[me] / 10;
   const uint64_t rel_x = bmin_me >= 1 ? bmin_me - 1 : 0;  // relevant: probed by own queries
-  S.plan(gop, m, pp);
+  S.plan(gop, nsuf, pp);
   gop.out = S.take<GhostX>(SL_SEND, pp.total + 1);
   S.emit(gop, pp);
   uint32_t G = 0;
@@ -887,6 +917,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   pr.ys = S.take<uint64_t>(SL_YS, m + 1);
   pr.keyy = S.take<uint32_t>(SL_KEYY, m + 1);
   pr.ylenhi = fast32 ? nullptr : S.take<uint32_t>(SL_YLENHI, m + 1);
+  const ulonglong2 *yrec_own = nullptr;  // own Y records of the last X problem
   auto solve_x = [&](const GhostX *halo, uint32_t Gc) {
     const uint32_t n = Gc + m;
     ulonglong2 *xrec = S.take<ulonglong2>(SL_XREC, n + 1);
@@ -900,6 +931,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
     Proc q = pr;
     q.xrec = xrec + Gc;
     q.yrec = yrec + Gc;
+    yrec_own = q.yrec;
     q.keyx = keyx + Gc;
     gather_proc(f, q, m, nbx, nby, S.st);
     S.launched("gather_proc");
@@ -928,7 +960,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
     GhostOp sop = gop;
     sop.out = nullptr;
     sop.xg = xg;
-    S.plan(sop, m, pp);
+    S.plan(sop, nsuf, pp);
     sop.sout = S.take<uint8_t>(SL_SEND, pp.total + 1);
     S.emit(sop, pp);
     uint32_t G2 = 0;
@@ -964,8 +996,10 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   // ---- 4: Y axis: entries -> Y-centre-bucket ranges (+ halos)
   const auto ty = std::chrono::steady_clock::now();
   YOp yop{};
-  yop.row = pr.row;
-  yop.rec = rec;
+  yop.yrec = yrec_own;
+  yop.ylenhi = pr.ylenhi;
+  yop.keyy = pr.keyy;
+  yop.nby = nby;
   yop.xg = xg;
   yop.P = P;
   yop.poff = poff;
@@ -1200,6 +1234,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   out->out_offset = ooff;
   out->n_out_total = otot;
   out->n_groups = Gtot;
+  if (ctx->profiling) collect_kernel_timing(ctx);
   ss.bytes_sent = S.bytes_sent;
   ss.ms_total = ms_since(t0);
   ctx->stats = rk_stats{};
@@ -1227,6 +1262,7 @@ extern "C" int rk_classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_so
     ctx->err = "unexpected C++ exception";
     rc = RK_E_INTERNAL;
   }
+  rk::g_ktimer = nullptr;
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   return rc;
 }

@@ -60,3 +60,45 @@ def test_single_rank_is_local():
     import bench
     assert bench.aggregate(1, 7, 0.25) == (7.0, 0.25)
     assert bench.rank_seed(0) != bench.rank_seed(1)
+
+
+def _comm_worker(rank, world, port, q):
+    """The gloo host-callback collectives behind rk.Comm.torch_host (the comm the
+    multi-rank GPU tests run rk_classify_sharded on), called as the C side does."""
+    import ctypes
+    import torch.distributed as dist
+    import repkiller_amd as rk
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = rk.Comm.torch_host(rank, world)
+    allgather, alltoallv = comm._keep[0], comm._keep[1]
+    mine = (ctypes.c_uint8 * 3)(*[10 * rank + i for i in range(3)])
+    allg = (ctypes.c_uint8 * (3 * world))()
+    assert allgather(None, ctypes.addressof(mine), ctypes.addressof(allg), 3) == 0
+    # rank r sends r+1+q bytes of value 16*r+q to rank q
+    sb = (ctypes.c_uint64 * world)(*[rank + 1 + q for q in range(world)])
+    rb = (ctypes.c_uint64 * world)(*[q + 1 + rank for q in range(world)])
+    send = bytes(b for q in range(world) for b in [16 * rank + q] * (rank + 1 + q))
+    sbuf = (ctypes.c_uint8 * len(send)).from_buffer_copy(send)
+    rbuf = (ctypes.c_uint8 * sum(rb))()
+    assert alltoallv(None, ctypes.addressof(sbuf), sb, ctypes.addressof(rbuf), rb) == 0
+    q.put((rank, list(allg), list(rbuf)))
+    comm.close()
+    dist.destroy_process_group()
+
+
+def test_host_comm_callbacks_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    for rank, allg, recv in res:
+        assert allg == [0, 1, 2, 10, 11, 12]
+        want = [16 * src + rank for src in range(2) for _ in range(src + 1 + rank)]
+        assert recv == want
