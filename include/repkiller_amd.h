@@ -147,6 +147,11 @@ typedef struct {
 } rk_comm_host_ops;
 
 int rk_comm_create_host(int rank, int size, const rk_comm_host_ops *ops, rk_comm **comm);
+/* An in-process group of `size` comms (comms[r] for rank r), for one thread per
+ * rank: exchanges are direct device copies between the ranks' buffers (peer
+ * copies over xGMI when the ranks use different GPUs).  Destroy each with
+ * rk_comm_destroy. */
+int rk_comm_create_local(int size, rk_comm **comms);
 /* RCCL communicator (librccl.so.1 is loaded on first use): rank 0 makes the
  * id, the caller distributes it (e.g. a torch.distributed broadcast), every
  * rank then creates its comm on its device. */
@@ -187,6 +192,9 @@ typedef struct {
  * halos only make re-resolution rounds rarer. */
 int rk_classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in_dev,
                         const rk_params *p, int32_t lead_in, rk_shard_result *out);
+/* The same with this rank's rows in HOST memory (copied to the device first). */
+int rk_classify_sharded_host(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in_host,
+                             const rk_params *p, int32_t lead_in, rk_shard_result *out);
 int rk_get_shard_stats(const rk_ctx *ctx, rk_shard_stats *st);
 /* Copy a rank's share (n_out rows) into caller buffers (host or device). */
 int rk_shard_copy_result(rk_ctx *ctx, const rk_shard_result *res, uint32_t *out_order,

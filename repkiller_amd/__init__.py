@@ -48,7 +48,7 @@ EXPORTS = (
     "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
     "rk_synth_write_csv", "rk_comm_create_host", "rk_comm_rccl_id", "rk_comm_create_rccl",
     "rk_comm_destroy", "rk_comm_last_error", "rk_classify_sharded", "rk_get_shard_stats",
-    "rk_shard_copy_result",
+    "rk_shard_copy_result", "rk_comm_create_local", "rk_classify_sharded_host",
 )
 
 
@@ -191,6 +191,10 @@ def load_library() -> ctypes.CDLL:
                                                ctypes.POINTER(Params), ctypes.c_int32,
                                                ctypes.POINTER(ShardResult)]),
         "rk_get_shard_stats": (ctypes.c_int, [vp, ctypes.POINTER(ShardStats)]),
+        "rk_comm_create_local": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+        "rk_classify_sharded_host": (ctypes.c_int, [vp, vp, ctypes.POINTER(FragsSoA),
+                                                    ctypes.POINTER(Params), ctypes.c_int32,
+                                                    ctypes.POINTER(ShardResult)]),
         "rk_shard_copy_result": (ctypes.c_int, [vp, ctypes.POINTER(ShardResult), vp, vp, vp]),
     }
     for name, (res, args) in sig.items():

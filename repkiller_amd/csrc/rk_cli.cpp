@@ -13,8 +13,13 @@
 // exits non-zero with a message instead of std::terminate.
 //
 // Options (before the positional arguments): --device N, --timing (phase
-// times as one JSON line on stderr).
+// times as one JSON line on stderr), --gpus P (one fragment set sharded over
+// P GPUs, devices N..N+P-1, one thread each: rk_classify_sharded over RCCL),
+// --same-device (all P ranks on device N -- a rehearsal of the sharded path
+// on one GPU), --comm rccl|local (collectives: RCCL, or in-process device
+// copies; default rccl, local with --same-device).
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -26,7 +31,8 @@
 
 static void print_help() {
   std::printf("Repkiller (MI355X) v0.9.b-compatible\n");
-  std::printf("Usage: ./rk_repkiller [--device N] [--timing] <input_file_path> <output_file_path> "
+  std::printf("Usage: ./rk_repkiller [--device N] [--gpus P [--same-device] [--comm rccl|local]] "
+              "[--timing] <input_file_path> <output_file_path> "
               "<length_ratio> <position_ratio> [<length_ratio> <position_ratio>]...\n");
   std::fflush(stdout);
 }
@@ -42,15 +48,84 @@ static bool parse_ratio(const char *s, double *v) {
   return end != s;
 }
 
+// One fragment set over `gpus` ranks, one thread each; every pair in turn.
+// The ranks hold consecutive blocks of rows; each copies its output share into
+// the full result arrays at its offset.
+static int classify_sharded_threads(const rk_frags_soa &soa, int device, int gpus,
+                                    bool same_device, bool local, const std::vector<rk_params> &ps,
+                                    std::vector<rk_result> &rs, std::string &err) {
+  std::vector<rk_comm *> comms(gpus, nullptr);
+  uint8_t id[RK_COMM_ID_BYTES];
+  if (local) {
+    if (rk_comm_create_local(gpus, comms.data())) {
+      err = "rk_comm_create_local failed";
+      return 1;
+    }
+  } else if (rk_comm_rccl_id(id)) {
+    err = "RCCL is not available";
+    return 1;
+  }
+  std::vector<int> status(gpus, 0);
+  std::vector<std::string> msgs(gpus);
+  std::vector<std::thread> th;
+  for (int r = 0; r < gpus; ++r)
+    th.emplace_back([&, r] {
+      const int dev = same_device ? device : device + r;
+      if (!local && rk_comm_create_rccl(r, gpus, dev, id, &comms[r])) {
+        status[r] = RK_E_HIP;
+        msgs[r] = "rk_comm_create_rccl failed";
+        return;
+      }
+      rk_ctx *ctx = nullptr;
+      if ((status[r] = rk_create(&ctx, dev))) {
+        msgs[r] = "no usable gfx950 device " + std::to_string(dev);
+        return;
+      }
+      const uint64_t a = soa.n * (uint64_t)r / gpus, b = soa.n * (uint64_t)(r + 1) / gpus;
+      const rk_frags_soa mine{soa.x_start + a, soa.y_start + a, soa.length + a,
+                              soa.strand + a, b - a};
+      for (size_t i = 0; i < ps.size() && !status[r]; ++i) {
+        rk_shard_result res;
+        status[r] = rk_classify_sharded_host(ctx, comms[r], &mine, &ps[i], -1, &res);
+        if (!status[r])
+          status[r] = rk_shard_copy_result(ctx, &res, rs[i].out_order + res.out_offset,
+                                           rs[i].gid + res.out_offset,
+                                           rs[i].repval + res.out_offset);
+        if (status[r]) msgs[r] = rk_last_error(ctx);
+        if (r == 0 && !status[r]) rs[i].n_out = res.n_out_total, rs[i].n_groups = res.n_groups;
+      }
+      rk_destroy(ctx);
+    });
+  for (auto &t : th) t.join();
+  for (rk_comm *c : comms) rk_comm_destroy(c);
+  for (int r = 0; r < gpus; ++r)
+    if (status[r]) {
+      err = "rank " + std::to_string(r) + ": " + msgs[r] + " (" + std::to_string(status[r]) + ")";
+      return status[r];
+    }
+  return 0;
+}
+
 int main(int argc, char **argv) {
-  int device = 0;
-  bool timing = false;
+  int device = 0, gpus = 1;
+  bool timing = false, same_device = false;
+  const char *comm_kind = nullptr;
   std::vector<const char *> pos;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) gpus = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--comm") && i + 1 < argc) comm_kind = argv[++i];
+    else if (!std::strcmp(argv[i], "--same-device")) same_device = true;
     else if (!std::strcmp(argv[i], "--timing")) timing = true;
     else pos.push_back(argv[i]);
   }
+  if (gpus < 1 || gpus > 32 ||
+      (comm_kind && std::strcmp(comm_kind, "rccl") && std::strcmp(comm_kind, "local"))) {
+    std::fprintf(stderr, "Invalid --gpus / --comm.\n");
+    print_help();
+    return 1;
+  }
+  const bool local = comm_kind ? !std::strcmp(comm_kind, "local") : same_device;
   // init_args (commonFunctions.cpp:14-29)
   if (pos.size() < 4 || (pos.size() - 2) % 2 != 0) {
     std::fprintf(stderr, "Invalid number of arguments.\n");
@@ -106,11 +181,13 @@ int main(int argc, char **argv) {
   rk_db_view(db, &soa, &lx, &ly, &total);
 
   rk_ctx *ctx = nullptr;
-  rc = rk_create(&ctx, device);
-  if (rc) {
-    std::fprintf(stderr, "no usable gfx950 device %d (%d)\n", device, rc);
-    rk_db_free(db);
-    return 1;
+  if (gpus == 1) {
+    rc = rk_create(&ctx, device);
+    if (rc) {
+      std::fprintf(stderr, "no usable gfx950 device %d (%d)\n", device, rc);
+      rk_db_free(db);
+      return 1;
+    }
   }
   rk_saver *sq = nullptr;
   rk_saver_start(db, &sq);
@@ -127,17 +204,23 @@ int main(int argc, char **argv) {
                       0, 0};
   }
   double a = now_s();
-  rc = rk_classify_pairs(ctx, &soa, ps.data(), (uint32_t)q, rs.data());
+  std::string err;
+  if (gpus == 1) {
+    rc = rk_classify_pairs(ctx, &soa, ps.data(), (uint32_t)q, rs.data());
+    if (rc) err = rk_last_error(ctx);
+  } else {
+    rc = classify_sharded_threads(soa, device, gpus, same_device, local, ps, rs, err);
+  }
   const double t_class = now_s() - a;
   if (rc) {
-    std::fprintf(stderr, "classification failed (%d): %s\n", rc, rk_last_error(ctx));
+    std::fprintf(stderr, "classification failed (%d): %s\n", rc, err.c_str());
     rk_saver_stop(sq);
     rk_destroy(ctx);
     rk_db_free(db);
     return 1;
   }
-  rk_stats stt;
-  rk_get_stats(ctx, &stt);
+  rk_stats stt{};
+  if (ctx) rk_get_stats(ctx, &stt);
   const double dev_ms = stt.device_ms;
   for (size_t i = 0; i < q; ++i) rk_saver_add(sq, out_path.c_str(), &rs[i], soa.n);
   double t2 = now_s();
@@ -147,8 +230,8 @@ int main(int argc, char **argv) {
   if (timing)
     std::fprintf(stderr,
                  "{\"frags\": %llu, \"pairs\": %zu, \"load_s\": %.6f, \"classify_s\": %.6f, "
-                 "\"device_ms\": %.3f, \"save_s\": %.6f}\n",
-                 (unsigned long long)soa.n, params.size(), t1 - t0, t_class, dev_ms, t3 - t2);
+                 "\"device_ms\": %.3f, \"save_s\": %.6f, \"gpus\": %d}\n",
+                 (unsigned long long)soa.n, params.size(), t1 - t0, t_class, dev_ms, t3 - t2, gpus);
   rk_db_free(db);
   if (rc) {
     std::fprintf(stderr, "writing output failed (%d)\n", rc);

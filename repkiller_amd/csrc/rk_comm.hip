@@ -13,8 +13,10 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 
 #include "rk_comm.h"
@@ -187,7 +189,93 @@ struct HostComm final : rk_comm {
   }
 };
 
+// ------------------------------------------------------ in-process group --
+// P threads of one process, one GPU each (or all on one GPU): every rank
+// publishes its buffer, a barrier, every rank copies what it needs from the
+// others' buffers (device blocks: hipMemcpyDefault, peer copies over xGMI when
+// the ranks sit on different GPUs), a second barrier frees the buffers.
+struct LocalShared {
+  int size;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  std::vector<const void *> ptr;
+  std::vector<const uint64_t *> counts;
+  explicit LocalShared(int p) : size(p), ptr(p), counts(p) {}
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t g = generation;
+    if (++arrived == size) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != g; });
+    }
+  }
+};
+
+struct LocalComm final : rk_comm {
+  std::shared_ptr<LocalShared> sh;
+
+  int allgather(const void *send, void *recv, size_t bytes, hipStream_t) override {
+    sh->ptr[rank] = send;
+    sh->barrier();
+    for (int q = 0; q < size; ++q)
+      if (bytes) std::memcpy((char *)recv + (size_t)q * bytes, sh->ptr[q], bytes);
+    sh->barrier();
+    return RK_OK;
+  }
+
+  int alltoallv(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb,
+                hipStream_t st) override {
+    sh->ptr[rank] = send;
+    sh->counts[rank] = sb;
+    sh->barrier();
+    size_t ro = 0;
+    hipError_t e = hipSuccess;
+    for (int q = 0; q < size && e == hipSuccess; ++q) {
+      const uint64_t *qsb = sh->counts[q];
+      size_t so = 0;
+      for (int r = 0; r < rank; ++r) so += qsb[r];
+      if (qsb[rank] != rb[q]) {
+        e = hipErrorInvalidValue;
+        break;
+      }
+      if (rb[q])
+        e = hipMemcpyAsync((char *)recv + ro, (const char *)sh->ptr[q] + so, rb[q],
+                           hipMemcpyDefault, st);
+      ro += rb[q];
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    sh->barrier();  // every rank has copied out of every send buffer
+    if (e != hipSuccess) {
+      err = std::string("local alltoallv: ") + hipGetErrorString(e);
+      return RK_E_HIP;
+    }
+    return RK_OK;
+  }
+};
+
 }  // namespace
+
+extern "C" int rk_comm_create_local(int size, rk_comm **comms) {
+  if (!comms || size < 1 || size > 32) return RK_E_ARG;
+  auto sh = std::make_shared<LocalShared>(size);
+  for (int r = 0; r < size; ++r) {
+    auto c = new (std::nothrow) LocalComm;
+    if (!c) {
+      for (int q = 0; q < r; ++q) delete comms[q];
+      return RK_E_NOMEM;
+    }
+    c->rank = r;
+    c->size = size;
+    c->sh = sh;
+    comms[r] = c;
+  }
+  return RK_OK;
+}
 
 extern "C" int rk_comm_create_host(int rank, int size, const rk_comm_host_ops *ops,
                                    rk_comm **comm) {

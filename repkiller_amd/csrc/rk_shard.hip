@@ -1286,3 +1286,32 @@ extern "C" int rk_shard_copy_result(rk_ctx *ctx, const rk_shard_result *res, uin
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return RK_OK;
 }
+
+extern "C" int rk_classify_sharded_host(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in,
+                                        const rk_params *p, int32_t lead_in,
+                                        rk_shard_result *out) {
+  if (!ctx || !in) return RK_E_ARG;
+  ctx->err.clear();
+  const size_t n = in->n;
+  if (n && (!in->x_start || !in->y_start || !in->length || !in->strand)) return RK_E_ARG;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const size_t need = rk::align_up(n * 8 + 16) * 3 + rk::align_up(n + 16);
+  if (need > ctx->io_cap) {
+    if (ctx->io) (void)hipFree(ctx->io);
+    ctx->io = nullptr;
+    ctx->io_cap = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->io, need));
+    ctx->io_cap = need;
+  }
+  rk::Carve c{(char *)ctx->io};
+  uint64_t *dx = c.take<uint64_t>(n), *dy = c.take<uint64_t>(n), *dl = c.take<uint64_t>(n);
+  uint8_t *ds = c.take<uint8_t>(n);
+  if (n) {
+    HIPCHK(ctx, hipMemcpyAsync(dx, in->x_start, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(dy, in->y_start, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(dl, in->length, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ds, in->strand, n, hipMemcpyHostToDevice, ctx->stream));
+  }
+  rk_frags_soa din{dx, dy, dl, ds, n};
+  return rk_classify_sharded(ctx, comm, &din, p, lead_in, out);
+}

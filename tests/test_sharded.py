@@ -157,3 +157,34 @@ def test_sharded_rccl_single_rank(gpu_ctx):
     assert ng == want.n_groups
     assert np.array_equal(order, want.out_order) and np.array_equal(gid, want.gid)
     assert np.array_equal(rep, want.repval)
+
+
+def test_cli_sharded_threads(tmp_path):
+    """rk_repkiller --gpus P: one fragment set over P ranks (one thread each,
+    in-process device-copy comm, all ranks on the test box's one GPU), CSV in,
+    CSV out, byte-identical to the reference's output; several ratio pairs."""
+    import gzip
+    import shutil
+    import subprocess
+    from conftest import GOLDEN
+    inp, out = tmp_path / "in.csv", tmp_path / "out.csv"
+    with gzip.open(os.path.join(GOLDEN, "corpus10k.in.csv.gz"), "rb") as fi, open(inp, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    with gzip.open(os.path.join(GOLDEN, "corpus10k.out.csv.gz"), "rb") as f:
+        want = f.read()
+    for gpus in (2, 3, 5):
+        p = subprocess.run([rk.CLI_PATH, "--gpus", str(gpus), "--same-device", str(inp), str(out),
+                            "0.05", "0.05", "0.3", "0.3"], capture_output=True, text=True,
+                           timeout=300)
+        assert p.returncode == 0, p.stderr
+        assert out.read_bytes() == want, gpus  # last pair wins (E10)
+    # a larger synthetic set against the single-GPU CLI
+    f = rk.synth(300_000, 30_000_000, seed=51)
+    big = tmp_path / "big.csv"
+    rk.write_input_csv(str(big), f, 30_000_000, 30_000_000)
+    one, four = tmp_path / "one.csv", tmp_path / "four.csv"
+    for args, dst in (([], one), (["--gpus", "4", "--same-device"], four)):
+        p = subprocess.run([rk.CLI_PATH, *args, str(big), str(dst), "0.3", "0.3"],
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr
+    assert one.read_bytes() == four.read_bytes()
