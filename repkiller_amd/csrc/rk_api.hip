@@ -35,7 +35,9 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_sweep_fast",    "k_sweep_fast_more", "k_sweep_wave",    "k_csr_fill_y",    "k_jump",
     "k_assign_gid",    "k_group_offsets",   "k_build_records",
     "k_sort_small",    "k_sort_groups_reg", "k_sort_groups_lds", "k_sort_groups_global",
-    "k_emit",
+    "k_emit",          "k_part (sharded)", "exchange (sharded)", "k_aux (sharded)",
+    "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
+    "k_merge_yx (sharded)",
 };
 }  // namespace rk
 
@@ -165,6 +167,7 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.p.keyy = c.take<uint32_t>(n);
   w.p.par = c.take<uint32_t>(n);
   w.p.gid = c.take<uint32_t>(n);
+  w.p.grow = nullptr;  // the sharded driver's global rows; unused here
   for (rk::Csr *cs : {&w.cx, &w.cy}) {
     cs->key = c.take<uint32_t>(n);
     cs->ent = c.take<uint32_t>(n);
@@ -287,7 +290,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   }
   pl.nbx = (uint32_t)(pl.max_x + 1);
   pl.nby = (uint32_t)(pl.max_y + 1);
-  Work w;
+  Work w{};  // value-initialised: optional Proc columns (grow, ...) stay null
   int rc = ensure_ws(ctx, pl, w);
   if (rc) return rc;
   const uint32_t n = (uint32_t)pl.n;

@@ -44,9 +44,12 @@ __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t ma
     wide |= f.len[i] >= 0x80000000ull;
     const uint64_t pk = x / 10;
     // pack the row once, coalesced, so the processing-order gather is one
-    // 32-B read per row instead of four scattered reads
-    rec[2 * (size_t)i] = make_ulonglong2(x, f.y[i]);
-    rec[2 * (size_t)i + 1] = make_ulonglong2(f.len[i], f.strand[i]);
+    // 32-B read per row instead of four scattered reads (the sharded driver
+    // packs its rows elsewhere: rec null)
+    if (rec) {
+      rec[2 * (size_t)i] = make_ulonglong2(x, f.y[i]);
+      rec[2 * (size_t)i + 1] = make_ulonglong2(f.len[i], f.strand[i]);
+    }
     uint32_t key = (uint32_t)(vsize - 1);  // the never-iterated last bucket sorts last
     if (pk >= vsize) {
       atomicOr(err, ERRB_UB_BUCKET);
@@ -78,11 +81,12 @@ __global__ void k_gather_proc(Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
     const ulonglong2 a = p.rec[2 * (size_t)r], b = p.rec[2 * (size_t)r + 1];
     const uint64_t x = a.x, y = a.y, L = b.x;
     const uint64_t xc = x + L / 2;
-    const uint32_t s = b.y == 'f' ? 0u : 1u;
+    const uint32_t s = (uint8_t)b.y == 'f' ? 0u : 1u;  // strand: the low byte
     p.ys[k] = y;
     p.xrec[k] = make_ulonglong2(xc, L);
     p.yrec[k] = make_ulonglong2(y + L / 2, L & 0xFFFFFFFFull);  // X result merged later
     if (p.ylenhi) p.ylenhi[k] = (uint32_t)(L >> 32);
+    if (p.grow) p.grow[k] = (uint32_t)(b.y >> 32);
     p.keyx[k] = s * nbx + (uint32_t)(xc / 100);
     p.keyy[k] = s * nby + (uint32_t)((y + L / 2) / 100);
   }
@@ -218,7 +222,7 @@ void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, u
     kt_begin(st);
     k_prep_keys<<<grid_for(f.n, 256, 2048), 256, 0, st>>>(f, vsize, max_x, max_y, pkey, rec, kept,
                                                            err);
-    kt_end(st, KID_PREP, 61.0 * f.n);  // x, y, len, strand in; key + 32-B record out
+    kt_end(st, KID_PREP, (rec ? 61.0 : 29.0) * f.n);  // x, y, len, strand in; key (+ 32-B record) out
   }
 }
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st) {

@@ -55,7 +55,8 @@ enum KernelId : int {
   KID_PREP, KID_HIST, KID_SCATTER, KID_GATHER, KID_SORT_KEYS, KID_CSR_FILL_X, KID_RUN_BOUNDS,
   KID_SWEEP_TILE, KID_SWEEP_FAST, KID_SWEEP_MORE, KID_SWEEP_WAVE, KID_CSR_FILL_Y, KID_JUMP,
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
-  KID_SORT_GLOBAL, KID_EMIT, KID_COUNT
+  KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
+  KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 struct KernelTimer {
@@ -146,6 +147,7 @@ struct Proc {  // processing-order working set
   ulonglong2 *hrec;  // {in-group sort key, file row}: one gather per member
   uint32_t *keyx, *keyy;
   uint32_t *par, *gid;
+  uint32_t *grow;  // optional (sharded driver): global file row, from rec's high word
 };
 struct Csr {  // one axis in CSR order (see Axis)
   uint32_t *key, *ent;

@@ -76,9 +76,11 @@ __device__ __forceinline__ uint32_t owner_of(const Bounds &B, uint64_t key) {
 }
 
 // ---------------------------------------------------------------- records --
-struct ShardRow {  // an input row on its way to its slice owner (32 B)
-  uint64_t x, y, len;
-  uint32_t row, strand;
+// An input row on its way to its slice owner (32 B).  Received rows are used
+// in place as the processing-order gather's records ({x, y}, {len, sr}):
+// sr = strand byte | global file row << 32 (gather_proc reads the low byte).
+struct ShardRow {
+  uint64_t x, y, len, sr;
 };
 struct GhostX {  // an X-axis halo entry (24 B)
   uint64_t xc, len;
@@ -96,12 +98,18 @@ struct ParRec {
 // An Op describes, per element i < n, the set of destination ranks (mask) and
 // writes the record bound for rank d at send position pos (emit).  Positions
 // are stable: rank-d records keep element order.
+// mcache: masks of an earlier plan over the same elements (mread), or where
+// this plan stores them (the scatter then reads them back)
 template <class Op>
 __global__ void __launch_bounds__(256) k_part_count(Op op, uint32_t n, uint32_t P, uint32_t nblk,
-                                                    uint32_t *cnt) {
+                                                    uint32_t *cnt, uint32_t *mcache, bool mread) {
   __shared__ uint32_t wc[4][MAXP];
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t mask = i < n ? op.mask(i) : 0u;
+  uint32_t mask = 0u;
+  if (i < n) {
+    mask = mread ? mcache[i] : op.mask(i);
+    if (mcache && !mread) mcache[i] = mask;
+  }
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint32_t d = 0; d < P; ++d) {
     const uint64_t b = __ballot((mask >> d) & 1u);
@@ -116,10 +124,11 @@ __global__ void __launch_bounds__(256) k_part_count(Op op, uint32_t n, uint32_t 
 
 template <class Op>
 __global__ void __launch_bounds__(256) k_part_scatter(Op op, uint32_t n, uint32_t P,
-                                                      uint32_t nblk, const uint32_t *off) {
+                                                      uint32_t nblk, const uint32_t *off,
+                                                      const uint32_t *mcache) {
   __shared__ uint32_t wc[4][MAXP];
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t mask = i < n ? op.mask(i) : 0u;
+  const uint32_t mask = i < n ? (mcache ? mcache[i] : op.mask(i)) : 0u;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
   for (uint32_t d = 0; d < P; ++d) {
@@ -157,11 +166,11 @@ __global__ void __launch_bounds__(256) k_hist(Op op, uint32_t n, uint32_t *hist)
 }
 
 // -------------------------------------------------------------------- ops --
-__device__ __forceinline__ uint32_t strand_code(uint64_t s) { return s == 'f' ? 0u : 1u; }
+__device__ __forceinline__ uint32_t strand_code(uint64_t s) { return (uint8_t)s == 'f' ? 0u : 1u; }
 
 struct RowOp {  // input rows -> slice owners (by xStart/10)
   const uint32_t *pkey;
-  const ulonglong2 *rec;
+  Frags f;  // this rank's rows (SoA, file order)
   Bounds B;
   uint32_t drop, shift, row_base;
   ShardRow *out;
@@ -174,8 +183,8 @@ struct RowOp {  // input rows -> slice owners (by xStart/10)
     return k < drop ? 1u << owner_of(B, k) : 0u;
   }
   __device__ void emit(uint32_t i, uint32_t, uint32_t pos) const {
-    const ulonglong2 a = rec[2 * (size_t)i], b = rec[2 * (size_t)i + 1];
-    out[pos] = ShardRow{a.x, a.y, b.x, row_base + i, (uint32_t)b.y};
+    out[pos] = ShardRow{f.x[i], f.y[i], f.len[i],
+                        (uint64_t)f.strand[i] | ((uint64_t)(row_base + i) << 32)};
   }
 };
 
@@ -227,10 +236,11 @@ struct YOp {  // own entries -> Y-range owners (+ their halos), processing order
   const ulonglong2 *yrec;  // {centre, length low 32 | ...} (gather_proc)
   const uint32_t *ylenhi;  // length high 32 bits (null: all lengths < 2^31)
   const uint32_t *keyy;    // strand * nby + bucket
-  const uint32_t *xg;
+  const uint32_t *xg;      // with xout: the X results, sent after X in the same order
   int64_t lo[MAXP], hi[MAXP];  // halo-extended ranges
   uint32_t P, poff, shift, nby;
   YRec *out;
+  uint8_t *xout;
   __device__ uint32_t bin(uint32_t k) const { return (uint32_t)((yrec[k].x / 100) >> shift); }
   __device__ uint32_t mask(uint32_t k) const {
     const int64_t bk = (int64_t)(yrec[k].x / 100);
@@ -242,74 +252,77 @@ struct YOp {  // own entries -> Y-range owners (+ their halos), processing order
   __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
     const ulonglong2 a = yrec[k];
     const uint64_t L = (a.y & 0xFFFFFFFFull) | (ylenhi ? (uint64_t)ylenhi[k] << 32 : 0ull);
+    if (xout) {
+      xout[pos] = xg[k] != NONE ? 1 : 0;
+      return;
+    }
     const uint32_t s = keyy[k] >= nby ? 1u : 0u;
-    out[pos] = YRec{a.x, L, poff + k, s | (xg[k] != NONE ? 2u : 0u)};
+    out[pos] = YRec{a.x, L, poff + k, s};  // the X-hit bit follows after X
   }
 };
 
-// Y records held here: own range [lo, hi); relevant halo = buckets lo-1 and hi
-struct YView {
-  const YRec *yr;
-  uint64_t lo, hi;
-  __device__ uint64_t bk(uint32_t r) const { return yr[r].yc / 100; }
-  __device__ bool own(uint32_t r) const {
-    const uint64_t b = bk(r);
-    return b >= lo && b < hi;
-  }
-  __device__ bool rel(uint32_t r) const {
-    const uint64_t b = bk(r);
-    return b + 1 == lo || b == hi;
-  }
+// One code byte per Y record held here (own range [lo, hi), relevant halo =
+// buckets lo-1 and hi), written with the records' first fill; the verification
+// and parent ops then read one byte per record instead of the 24-B record.
+enum : uint8_t {
+  YC_OWN = 0, YC_REL_LO = 1, YC_REL_HI = 2, YC_GHOST = 3,  // bits 0-1: class
+  YC_FIRST = 4,   // own entry in bucket lo (a lower neighbour's relevant halo)
+  YC_LAST = 8,    // own entry in bucket hi-1 (an upper neighbour's relevant halo)
+  YC_XHIT = 16,   // the entry hit on X (set once X is final)
 };
+__device__ __forceinline__ uint8_t y_code(uint64_t b, uint64_t lo, uint64_t hi) {
+  if (b >= lo && b < hi) return (b == lo ? YC_FIRST : 0) | (b + 1 == hi ? YC_LAST : 0);
+  return b + 1 == lo ? YC_REL_LO : b == hi ? YC_REL_HI : YC_GHOST;
+}
 
 struct YStateOp {  // owner side: own entries in a neighbour's relevant halo
-  YView v;
-  uint64_t lo[MAXP], hi[MAXP];  // every rank's own range
-  uint32_t P, me;
+  const uint8_t *code;
+  uint32_t first_mask, last_mask;  // ranks whose relevant halo holds my first / last bucket
   const uint8_t *ystate;
   uint8_t *out;
   __device__ uint32_t mask(uint32_t r) const {
-    if (!v.own(r)) return 0u;
-    const uint64_t b = v.bk(r);
-    uint32_t m = 0;
-    for (uint32_t q = 0; q < P; ++q)
-      if (q != me && (b + 1 == lo[q] || b == hi[q])) m |= 1u << q;
-    return m;
+    const uint8_t c = code[r];
+    if (c & 3) return 0u;
+    return (c & YC_FIRST ? first_mask : 0u) | (c & YC_LAST ? last_mask : 0u);
   }
   __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const { out[pos] = ystate[r]; }
 };
 
 struct RelOp {  // receiver side: relevant halo entries grouped by owner
-  YView v;
-  Bounds B;
+  const uint8_t *code;
+  uint32_t lo_owner, hi_owner;  // owners of buckets lo-1 and hi
   uint32_t *out;
   __device__ uint32_t mask(uint32_t r) const {
-    return v.rel(r) ? 1u << owner_of(B, v.bk(r)) : 0u;
+    const uint8_t c = code[r] & 3;
+    return c == YC_REL_LO ? 1u << lo_owner : c == YC_REL_HI ? 1u << hi_owner : 0u;
   }
   __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const { out[pos] = r; }
 };
 
 struct SelYOp {  // the fixed-halo Y problem: own + relevant halo the owner calls ACTIVE
-  YView v;
+  const uint8_t *code;
   const uint8_t *used;
   uint32_t *out;
   __device__ uint32_t mask(uint32_t r) const {
-    if (v.own(r)) return 1u;
-    return v.rel(r) && ((v.yr[r].flags & 2u) || used[r]) ? 1u : 0u;
+    const uint8_t c = code[r], k = c & 3;
+    if (k == YC_OWN) return 1u;
+    return (k == YC_REL_LO || k == YC_REL_HI) && ((c & YC_XHIT) || used[r]) ? 1u : 0u;
   }
   __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const { out[pos] = r; }
 };
 
 struct ParOp {  // Y decisions of own X misses -> slice owners
-  YView v;
+  const YRec *yr;
+  const uint8_t *code;
   Bounds slices;
   const uint32_t *ywin;
   ParRec *out;
   __device__ uint32_t mask(uint32_t r) const {
-    return v.own(r) && !(v.yr[r].flags & 2u) ? 1u << owner_of(slices, v.yr[r].gidx) : 0u;
+    const uint8_t c = code[r];
+    return !(c & 3) && !(c & YC_XHIT) ? 1u << owner_of(slices, yr[r].gidx) : 0u;
   }
   __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const {
-    out[pos] = ParRec{v.yr[r].gidx, ywin[r]};
+    out[pos] = ParRec{yr[r].gidx, ywin[r]};
   }
 };
 
@@ -328,8 +341,7 @@ struct ReqOp {  // unresolved cross-slice roots -> the owner of their current ta
 
 struct MemOp {  // (in-group key, file row, gid) -> gid-range owners
   const uint32_t *gid;
-  const ulonglong2 *hrec;
-  const uint32_t *grow;
+  const ulonglong2 *hrec;  // {in-group key, GLOBAL file row}
   Bounds B;
   uint32_t shift;
   ulonglong2 *out;
@@ -337,27 +349,45 @@ struct MemOp {  // (in-group key, file row, gid) -> gid-range owners
   __device__ uint32_t mask(uint32_t k) const { return 1u << owner_of(B, gid[k]); }
   __device__ void emit(uint32_t k, uint32_t, uint32_t pos) const {
     const ulonglong2 h = hrec[k];
-    out[pos] = make_ulonglong2(h.x, (uint64_t)grow[(uint32_t)h.y] | ((uint64_t)gid[k] << 32));
+    out[pos] = make_ulonglong2(h.x, (h.y & 0xFFFFFFFFull) | ((uint64_t)gid[k] << 32));
   }
 };
 
 // ---------------------------------------------------------- small kernels --
-__global__ void k_unpack_rows(const ShardRow *in, uint32_t m, ulonglong2 *rec, uint32_t *pkey,
-                              uint32_t *grow, unsigned long long *maxlen) {
+// processing keys of the received rows (used in place as records) and the
+// longest length
+__global__ void k_row_keys(const ulonglong2 *rec, uint32_t m, uint32_t *pkey,
+                           unsigned long long *maxlen) {
   uint64_t lmax = 0;
   GRID_STRIDE(k, m) {
-    const ShardRow r = in[k];
-    rec[2 * (size_t)k] = make_ulonglong2(r.x, r.y);
-    rec[2 * (size_t)k + 1] = make_ulonglong2(r.len, r.strand);
-    pkey[k] = (uint32_t)(r.x / 10);
-    grow[k] = r.row;
-    lmax = r.len > lmax ? r.len : lmax;
+    pkey[k] = (uint32_t)(rec[2 * (size_t)k].x / 10);
+    const uint64_t L = rec[2 * (size_t)k + 1].x;
+    lmax = L > lmax ? L : lmax;
   }
   for (int off = 32; off > 0; off >>= 1) {
     const uint64_t o = __shfl_xor(lmax, off);
     lmax = o > lmax ? o : lmax;
   }
-  if ((threadIdx.x & 63) == 0 && lmax) atomicMax(maxlen, (unsigned long long)lmax);
+  // one atomic per block (the grid is capped): a per-wave atomic on one
+  // address serialises ~m/64 updates
+  __shared__ uint64_t wmax[4];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = lmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t b = wmax[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) b = wmax[w] > b ? wmax[w] : b;
+    if (b) atomicMax(maxlen, (unsigned long long)b);
+  }
+}
+
+// Y records get their X-hit bit once X is final: the code byte and the Y
+// problem's X-result word (which csr_fill_y turns into the initial state)
+__global__ void k_merge_yx(uint8_t *code, const uint8_t *xh, uint32_t n, ulonglong2 *yrec) {
+  GRID_STRIDE(r, n) {
+    const bool h = xh[r] != 0;
+    if (h) code[r] |= YC_XHIT;
+    yrec[r].y = (yrec[r].y & 0xFFFFFFFFull) | ((uint64_t)(h ? 0u : NONE) << 32);
+  }
 }
 
 // first k with key[k] >= v (key ascending)
@@ -406,22 +436,27 @@ __global__ void k_cmp_x(const GhostX *gh, uint32_t G, uint64_t rel, const uint8_
   }
 }
 
+// the Y problem's records (all held records, or the selection ymap); the
+// first fill (ymap null) also writes the code bytes
 __global__ void k_fill_y(const YRec *yr, const uint32_t *ymap, uint32_t c, ulonglong2 *yrec,
-                         uint32_t *ylenhi, uint32_t *keyy, uint32_t nby) {
+                         uint32_t *ylenhi, uint32_t *keyy, uint32_t nby, uint8_t *code,
+                         uint64_t lo, uint64_t hi_b) {
   GRID_STRIDE(k, c) {
-    const YRec R = yr[ymap ? ymap[k] : k];
-    const uint64_t hi = (R.flags & 2u) ? 0ull : (uint64_t)NONE;
+    const uint32_t r = ymap ? ymap[k] : k;
+    const YRec R = yr[r];
+    if (!ymap) code[r] = y_code(R.yc / 100, lo, hi_b);
+    const uint64_t hi = ymap && (code[r] & YC_XHIT) ? 0ull : (uint64_t)NONE;
     yrec[k] = make_ulonglong2(R.yc, (R.len & 0xFFFFFFFFull) | (hi << 32));
     if (ylenhi) ylenhi[k] = (uint32_t)(R.len >> 32);
     keyy[k] = (R.flags & 1u) * nby + (uint32_t)(R.yc / 100);
   }
 }
 
-__global__ void k_y_results(const YRec *yr, const uint32_t *ymap, uint32_t c,
+__global__ void k_y_results(const YRec *yr, const uint8_t *code, const uint32_t *ymap, uint32_t c,
                             const uint32_t *par, uint8_t *ystate, uint32_t *ywin) {
   GRID_STRIDE(k, c) {
     const uint32_t r = ymap ? ymap[k] : k;
-    if (yr[r].flags & 2u) {
+    if (code[r] & YC_XHIT) {
       ystate[r] = 1;
       ywin[r] = NONE;
     } else {
@@ -541,12 +576,16 @@ enum Slot : int {
   SL_RBEG, SL_YR, SL_YMAP, SL_YRECL, SL_YLENHIL, SL_KEYYL, SL_PARL, SL_YSTATE, SL_YWIN,
   SL_YUSED, SL_RELIDX, SL_RYS, SL_PR, SL_PARG, SL_LPAR, SL_EXT, SL_ISROOT, SL_LRANK, SL_JUNK,
   SL_LAB, SL_CUR, SL_REQ, SL_SRC, SL_RQ, SL_RESP, SL_BACK, SL_HREC, SL_MEM, SL_LG, SL_SGID,
-  SL_GMEM, SL_GOFF, SL_RECKEY, SL_TAG, SL_OTAG, SL_GSORT, SL_OGID, SL_OREP, SL_OORD, SL_COUNT
+  SL_GMEM, SL_GOFF, SL_RECKEY, SL_TAG, SL_OTAG, SL_GSORT, SL_OGID, SL_OREP, SL_OORD, SL_CKEY_Y,
+  SL_CENT_Y, SL_CSTATE_Y, SL_CPK_Y, SL_CNBD_Y, SL_CCEN_Y, SL_CLEN_Y, SL_TK2, SL_TV2, SL_RADIX2,
+  SL_YXH, SL_YMASK, SL_YCODE, SL_COUNT
 };
 
 struct PartPlan {
   uint32_t n = 0, nblk = 1;
   uint32_t *off = nullptr;
+  uint32_t *mcache = nullptr;  // set before plan(): masks cached there (mread: read)
+  bool mread = false;
   uint64_t cnt[MAXP] = {};
   uint64_t total = 0;
 };
@@ -554,7 +593,8 @@ struct PartPlan {
 struct Shard {
   rk_ctx *ctx;
   rk_comm *comm;
-  hipStream_t st;
+  hipStream_t st;   // compute + exchanges
+  hipStream_t st2;  // overlapped work (Y bucket order, in-group sort keys)
   uint32_t P, me;
   uint32_t *ctrl = nullptr;  // [0] err bits, [1] kept, [2] mismatches, [3] jump flag,
                             // [4] long-run count, [6] wide keys, [64..128) sweep
@@ -633,7 +673,9 @@ struct Shard {
     uint32_t *cnt = take<uint32_t>(SL_PCNT, len);
     pp.off = take<uint32_t>(SL_POFF, len);
     zero(cnt + len - 1, 4);
-    k_part_count<<<pp.nblk, 256, 0, st>>>(op, n, P, pp.nblk, cnt);
+    kt_begin(st);
+    k_part_count<<<pp.nblk, 256, 0, st>>>(op, n, P, pp.nblk, cnt, pp.mcache, pp.mread);
+    kt_end(st, KID_PART, 0.0);
     launched("k_part_count");
     exclusive_scan_u32(cnt, pp.off, len, scan_scratch(SL_PSCAN, len), st);
     k_totals<<<1, 64, 0, st>>>(pp.off, pp.nblk, P, ctrl + 128);
@@ -644,7 +686,9 @@ struct Shard {
   }
   template <class Op>
   void emit(const Op &op, const PartPlan &pp) {
-    k_part_scatter<<<pp.nblk, 256, 0, st>>>(op, pp.n, P, pp.nblk, pp.off);
+    kt_begin(st);
+    k_part_scatter<<<pp.nblk, 256, 0, st>>>(op, pp.n, P, pp.nblk, pp.off, pp.mcache);
+    kt_end(st, KID_PART, 0.0);
     launched("k_part_scatter");
   }
 
@@ -674,7 +718,12 @@ struct Shard {
   void run_a2a(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb) {
     for (uint32_t q = 0; q < P; ++q)
       if (q != me) bytes_sent += sb[q];
-    if (comm->alltoallv(send, sb, recv, rb, st)) {
+    double moved = 0;
+    for (uint32_t q = 0; q < P; ++q) moved += (double)sb[q] + (double)rb[q];
+    kt_begin(st);
+    const int rc = comm->alltoallv(send, sb, recv, rb, st);
+    kt_end(st, KID_EXCHANGE, moved);  // bytes read + written (device time of the a2a)
+    if (rc) {
       ctx->err = "alltoallv: " + comm->err;
       throw RK_E_HIP;
     }
@@ -688,6 +737,12 @@ struct Shard {
     check(err_status(ctx, any & ~(uint32_t)ERRB_WIDE_LENGTH));
   }
 };
+
+uint32_t owner_of_host(const Bounds &B, uint64_t key) {
+  uint32_t q = 0;
+  while (q + 1 < B.P && B.b[q + 1] <= key) ++q;
+  return q;
+}
 
 uint32_t bin_shift(uint64_t keys) {  // keys in [0, keys) -> < NBINS bins
   uint32_t s = 0;
@@ -750,21 +805,39 @@ struct AxisIn {
   bool is_x, fast32;
 };
 
-uint32_t resolve(Shard &S, const AxisIn &a, const rk_params &p) {
+// device buffers of one axis' CSR and its radix sort (X and Y own separate
+// sets: the Y axis is sorted on the second stream while X resolves)
+struct AxisSlots {
+  int key, ent, state, pk, nbd, cen, len, tk, tv, radix;
+};
+constexpr AxisSlots kXSlots{SL_CKEY, SL_CENT, SL_CSTATE, SL_CPK, SL_CNBD,
+                           SL_CCEN, SL_CLEN, SL_TK, SL_TV, SL_RADIX};
+constexpr AxisSlots kYSlots{SL_CKEY_Y, SL_CENT_Y, SL_CSTATE_Y, SL_CPK_Y, SL_CNBD_Y,
+                           SL_CCEN_Y, SL_CLEN_Y, SL_TK2, SL_TV2, SL_RADIX2};
+
+// the axis' bucket order (stable radix sort of the keys) on stream st
+Csr sort_axis(Shard &S, const AxisIn &a, const AxisSlots &sl, hipStream_t st) {
+  const uint32_t n = a.n;
+  Csr c{};
+  c.key = S.take<uint32_t>(sl.key, n + 1);
+  c.ent = S.take<uint32_t>(sl.ent, n + 1);
+  c.state = S.take<uint8_t>(sl.state, n + 1);
+  c.pk = S.take<uint2>(sl.pk, n + 1);
+  c.nbd = S.take<uint8_t>(sl.nbd, n + 1);
+  c.cen = a.fast32 ? nullptr : S.take<uint64_t>(sl.cen, n + 1);
+  c.len = a.fast32 ? nullptr : S.take<uint64_t>(sl.len, n + 1);
+  const size_t rw = radix_scratch_words(n + 1);
+  uint32_t *tk = S.take<uint32_t>(sl.tk, n + 1), *tv = S.take<uint32_t>(sl.tv, n + 1);
+  uint32_t *rs = S.take<uint32_t>(sl.radix, rw);
+  if (n) radix_sort_pairs(a.key, nullptr, c.key, c.ent, tk, tv, n, a.bits, rs, rw, st);
+  return c;
+}
+
+// CSR columns (centre, length, neighbour code, states) and the sweeps, on the
+// context stream
+uint32_t sweep_axis(Shard &S, const AxisIn &a, const Csr &c, const rk_params &p) {
   const uint32_t n = a.n;
   if (!n) return 0;
-  Csr c{};
-  c.key = S.take<uint32_t>(SL_CKEY, n);
-  c.ent = S.take<uint32_t>(SL_CENT, n);
-  c.state = S.take<uint8_t>(SL_CSTATE, n);
-  c.pk = S.take<uint2>(SL_CPK, n);
-  c.nbd = S.take<uint8_t>(SL_CNBD, n);
-  c.cen = a.fast32 ? nullptr : S.take<uint64_t>(SL_CCEN, n);
-  c.len = a.fast32 ? nullptr : S.take<uint64_t>(SL_CLEN, n);
-  const size_t rw = radix_scratch_words(n);
-  radix_sort_pairs(a.key, nullptr, c.key, c.ent, S.take<uint32_t>(SL_TK, n),
-                   S.take<uint32_t>(SL_TV, n), n, a.bits, S.take<uint32_t>(SL_RADIX, rw), rw,
-                   S.st);
   if (a.is_x) csr_fill_x(c, a.rec, n, a.max_index, S.st);
   else csr_fill_y(c, a.rec, a.ylenhi, n, a.max_index, S.st);
   S.launched("axis csr");
@@ -779,6 +852,12 @@ uint32_t resolve(Shard &S, const AxisIn &a, const rk_params &p) {
   return sweeps;
 }
 
+uint32_t resolve(Shard &S, const AxisIn &a, const AxisSlots &sl, const rk_params &p) {
+  if (!a.n) return 0;
+  const Csr c = sort_axis(S, a, sl, S.st);
+  return sweep_axis(S, a, c, p);
+}
+
 int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const rk_params *prm,
                      int32_t lead_in, rk_shard_result *out) {
   if (!ctx || !comm || !in || !prm || !out) return RK_E_ARG;
@@ -788,7 +867,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   const auto t0 = std::chrono::steady_clock::now();
   rk_shard_stats &ss = ctx->shard_stats;
   std::memset(&ss, 0, sizeof ss);
-  Shard S{ctx, comm, ctx->stream, (uint32_t)comm->size, (uint32_t)comm->rank};
+  Shard S{ctx, comm, ctx->stream, ctx->stream2, (uint32_t)comm->size, (uint32_t)comm->rank};
   const uint32_t P = S.P, me = S.me;
   const uint64_t H = lead_in < 0 ? 2 : (uint64_t)lead_in;
   const rk_params p = *prm;
@@ -825,13 +904,12 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   // ---- 1: processing keys, slice bounds from the global xStart/10 histogram
   Frags f{in->x_start, in->y_start, in->length, in->strand, nl};
   uint32_t *pkey_in = S.take<uint32_t>(SL_PKEY_IN, nl + 1);
-  ulonglong2 *rec_in = S.take<ulonglong2>(SL_REC_IN, 2 * (size_t)nl + 2);
-  prep_keys(f, vsize, max_x, max_y, pkey_in, rec_in, S.ctrl + 1, S.ctrl, S.st);
+  prep_keys(f, vsize, max_x, max_y, pkey_in, nullptr, S.ctrl + 1, S.ctrl, S.st);
   S.launched("prep_keys");
   S.agree_errors();
   bool fast32 = true;
   for (uint32_t b : S.gather1<uint32_t>(S.read1(S.ctrl))) fast32 &= !(b & ERRB_WIDE_LENGTH);
-  RowOp rop{pkey_in, rec_in, {}, drop, bin_shift(drop), (uint32_t)row_base, nullptr};
+  RowOp rop{pkey_in, f, {}, drop, bin_shift(drop), (uint32_t)row_base, nullptr};
   const Bounds slice_keys = split_bounds(global_hist(S, rop, nl), rop.shift, drop, P);
   rop.B = slice_keys;
 
@@ -841,18 +919,19 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   rop.out = S.take<ShardRow>(SL_SEND, pp.total + 1);
   S.emit(rop, pp);
   uint32_t m = 0;
-  const ShardRow *rows = S.exchange<ShardRow>(rop.out, pp, SL_ROWS, &m);
-  ulonglong2 *rec = S.take<ulonglong2>(SL_REC, 2 * (size_t)m + 2);
+  ShardRow *rows = S.exchange<ShardRow>(rop.out, pp, SL_ROWS, &m);
+  ulonglong2 *rec = reinterpret_cast<ulonglong2 *>(rows);  // the records, in place
   uint32_t *pkey2 = S.take<uint32_t>(SL_PKEY2, m + 1);
-  uint32_t *grow = S.take<uint32_t>(SL_GROW, m + 1);
   Proc pr{};
   pr.rec = rec;
   pr.pkey = S.take<uint32_t>(SL_PKEY, m + 1);
   pr.row = S.take<uint32_t>(SL_ROW, m + 1);
   if (m) {
-    k_unpack_rows<<<grid_for(m, 256), 256, 0, S.st>>>(
-        rows, m, rec, pkey2, grow, reinterpret_cast<unsigned long long *>(S.ctrl + 10));
-    S.launched("k_unpack_rows");
+    kt_begin(S.st);
+    k_row_keys<<<grid_for(m, 256, 1024), 256, 0, S.st>>>(
+        rec, m, pkey2, reinterpret_cast<unsigned long long *>(S.ctrl + 10));
+    kt_end(S.st, KID_SH_ROWKEYS, 0.0);
+    S.launched("k_row_keys");
     const size_t rw = radix_scratch_words(m);
     radix_sort_pairs(pkey2, nullptr, pr.pkey, pr.row, S.take<uint32_t>(SL_TK, m),
                      S.take<uint32_t>(SL_TV, m), m, bit_length(vsize - 1),
@@ -911,45 +990,115 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   GhostX *gh = S.exchange<GhostX>(gop.out, pp, SL_GH, &G);
   ss.x_ghosts = G;
 
-  // X problem = [halo (global order)] + own slice; own arrays sit after the halo
+  // X problem = [halo (global order)] + own slice.  The own arrays sit at
+  // offset G (the whole lead-in); a fixed-halo re-resolution with Gc <= G
+  // halo entries uses the window [G - Gc, G + m).
   uint32_t *xg = S.take<uint32_t>(SL_XG, m + 1);
   uint8_t *xused = S.take<uint8_t>(SL_XUSED, G + 1);
   pr.ys = S.take<uint64_t>(SL_YS, m + 1);
   pr.keyy = S.take<uint32_t>(SL_KEYY, m + 1);
   pr.ylenhi = fast32 ? nullptr : S.take<uint32_t>(SL_YLENHI, m + 1);
-  const ulonglong2 *yrec_own = nullptr;  // own Y records of the last X problem
-  auto solve_x = [&](const GhostX *halo, uint32_t Gc) {
-    const uint32_t n = Gc + m;
-    ulonglong2 *xrec = S.take<ulonglong2>(SL_XREC, n + 1);
-    ulonglong2 *yrec = S.take<ulonglong2>(SL_YRECF, n + 1);
-    uint32_t *keyx = S.take<uint32_t>(SL_KEYX, n + 1);
-    uint32_t *par = S.take<uint32_t>(SL_PARF, n + 1);
-    if (Gc) {
-      k_fill_ghost_x<<<grid_for(Gc, 256), 256, 0, S.st>>>(halo, Gc, xrec, keyx, nbx);
-      S.launched("k_fill_ghost_x");
-    }
+  uint32_t *grow_proc = S.take<uint32_t>(SL_GROW, m + 1);  // global file row by processing index
+  ulonglong2 *xrec_f = S.take<ulonglong2>(SL_XREC, G + m + 1);
+  ulonglong2 *yrec_f = S.take<ulonglong2>(SL_YRECF, G + m + 1);
+  uint32_t *keyx_f = S.take<uint32_t>(SL_KEYX, G + m + 1);
+  uint32_t *par_f = S.take<uint32_t>(SL_PARF, G + m + 1);
+  {
     Proc q = pr;
-    q.xrec = xrec + Gc;
-    q.yrec = yrec + Gc;
-    yrec_own = q.yrec;
-    q.keyx = keyx + Gc;
+    q.xrec = xrec_f + G;
+    q.yrec = yrec_f + G;
+    q.keyx = keyx_f + G;
+    q.grow = grow_proc;
     gather_proc(f, q, m, nbx, nby, S.st);
     S.launched("gather_proc");
-    AxisIn a{xrec, nullptr, keyx, par, reinterpret_cast<uint32_t *>(yrec), n,
+  }
+  const ulonglong2 *yrec_own = yrec_f + G;
+  ss.ms_x = ms_since(tx);
+
+  // ---- 4a: Y records -> Y-centre-bucket ranges (+ halos).  They do not depend
+  // on X (the X-hit bit follows later in the same order), so the Y axis'
+  // bucket order and the in-group sort keys are built on the second stream
+  // while X resolves.
+  const auto ty = std::chrono::steady_clock::now();
+  YOp yop{};
+  yop.yrec = yrec_own;
+  yop.ylenhi = pr.ylenhi;
+  yop.keyy = pr.keyy;
+  yop.nby = nby;
+  yop.xg = xg;
+  yop.P = P;
+  yop.poff = poff;
+  yop.shift = bin_shift(nby);
+  const Bounds yb = split_bounds(global_hist(S, yop, m), yop.shift, nby, P);
+  for (uint32_t q = 0; q < MAXP; ++q) {
+    yop.lo[q] = q < P ? (int64_t)yb.b[q] - 1 - (int64_t)H : 0;
+    yop.hi[q] = q < P ? (int64_t)yb.b[q + 1] + 1 + (int64_t)H : 0;
+  }
+  PartPlan ypp;
+  ypp.mcache = S.take<uint32_t>(SL_YMASK, m + 1);  // the X-hit bits follow the same masks
+  S.plan(yop, m, ypp);
+  yop.out = S.take<YRec>(SL_SEND, ypp.total + 1);
+  S.emit(yop, ypp);
+  uint32_t ny = 0;
+  YRec *yr = S.exchange<YRec>(yop.out, ypp, SL_YR, &ny);
+  ss.y_entries = ny;
+  uint8_t *ycode = S.take<uint8_t>(SL_YCODE, ny + 1);
+  uint8_t *ystate = S.take<uint8_t>(SL_YSTATE, ny + 1);
+  uint32_t *ywin = S.take<uint32_t>(SL_YWIN, ny + 1);
+  uint8_t *yused = S.take<uint8_t>(SL_YUSED, ny + 1);
+  ulonglong2 *yrec_l = S.take<ulonglong2>(SL_YRECL, ny + 1);
+  uint32_t *ylh_l = fast32 ? nullptr : S.take<uint32_t>(SL_YLENHIL, ny + 1);
+  uint32_t *keyy_l = S.take<uint32_t>(SL_KEYYL, ny + 1);
+  uint32_t *par_l = S.take<uint32_t>(SL_PARL, ny + 1);
+  pr.hrec = S.take<ulonglong2>(SL_HREC, m + 1);
+  const uint32_t ybits = (uint32_t)bit_length(2ull * nby - 1);
+  const AxisIn ya{yrec_l, ylh_l, keyy_l, par_l, nullptr, ny, ybits, max_y, false, fast32};
+  S.zero(S.ctrl + 6, 4);
+  S.hip(hipEventRecord(ctx->fork, S.st), "fork");
+  S.hip(hipStreamWaitEvent(S.st2, ctx->fork, 0), "fork wait");
+  if (ny) {
+    kt_begin(S.st2);
+    k_fill_y<<<grid_for(ny, 256), 256, 0, S.st2>>>(yr, nullptr, ny, yrec_l, ylh_l, keyy_l, nby,
+                                                   ycode, yb.b[me], yb.b[me + 1]);
+    kt_end(S.st2, KID_SH_FILLY, 0.0);
+    S.launched("k_fill_y");
+  }
+  const Csr ycsr = sort_axis(S, ya, kYSlots, S.st2);
+  {
+    Proc q = pr;
+    q.row = grow_proc;  // the member records carry global file rows
+    sort_keys(q, m, S.ctrl + 6, S.st2);  // in-group keys, for the member stage
+  }
+  S.launched("stream-2 work");
+  S.hip(hipEventRecord(ctx->join, S.st2), "join");
+  ss.ms_y = ms_since(ty);
+
+  // ---- 4b: X axis
+  const auto tx2 = std::chrono::steady_clock::now();
+  auto solve_x = [&](const GhostX *halo, uint32_t Gc) {
+    const uint32_t base = G - Gc, n = Gc + m;
+    if (Gc) {
+      kt_begin(S.st);
+      k_fill_ghost_x<<<grid_for(Gc, 256), 256, 0, S.st>>>(halo, Gc, xrec_f + base,
+                                                         keyx_f + base, nbx);
+      kt_end(S.st, KID_SHARD_AUX, 0.0);
+      S.launched("k_fill_ghost_x");
+    }
+    AxisIn a{xrec_f + base, nullptr, keyx_f + base, par_f + base,
+             reinterpret_cast<uint32_t *>(yrec_f + base), n,
              (uint32_t)bit_length(2ull * nbx - 1), max_x, true, fast32};
-    resolve(S, a, p);
+    resolve(S, a, kXSlots, p);
     if (m) {
-      k_x_own<<<grid_for(m, 256), 256, 0, S.st>>>(yrec + Gc, halo, Gc, poff, m, xg);
+      kt_begin(S.st);
+      k_x_own<<<grid_for(m, 256), 256, 0, S.st>>>(yrec_f + G, halo, Gc, poff, m, xg);
+      kt_end(S.st, KID_SH_XOWN, 0.0);
       S.launched("k_x_own");
     }
-    return yrec;
   };
-  {
-    const ulonglong2 *yrec = solve_x(gh, G);
-    if (G) {
-      k_x_used<<<grid_for(G, 256), 256, 0, S.st>>>(yrec, G, xused);
-      S.launched("k_x_used");
-    }
+  solve_x(gh, G);
+  if (G) {
+    k_x_used<<<grid_for(G, 256), 256, 0, S.st>>>(yrec_f, G, xused);
+    S.launched("k_x_used");
   }
   for (;;) {  // verify the relevant halo against its owners' decisions
     ++ss.x_rounds;
@@ -991,51 +1140,59 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
       S.hip(e, "xused copy");
     }
   }
-  ss.ms_x = ms_since(tx);
+  ss.ms_x += ms_since(tx2);
 
-  // ---- 4: Y axis: entries -> Y-centre-bucket ranges (+ halos)
-  const auto ty = std::chrono::steady_clock::now();
-  YOp yop{};
-  yop.yrec = yrec_own;
-  yop.ylenhi = pr.ylenhi;
-  yop.keyy = pr.keyy;
-  yop.nby = nby;
-  yop.xg = xg;
-  yop.P = P;
-  yop.poff = poff;
-  yop.shift = bin_shift(nby);
-  const Bounds yb = split_bounds(global_hist(S, yop, m), yop.shift, nby, P);
-  for (uint32_t q = 0; q < MAXP; ++q) {
-    yop.lo[q] = q < P ? (int64_t)yb.b[q] - 1 - (int64_t)H : 0;
-    yop.hi[q] = q < P ? (int64_t)yb.b[q + 1] + 1 + (int64_t)H : 0;
+  // ---- 4c: the X-hit bits follow the Y records (same plan, same order); the
+  // Y axis resolves on the bucket order stream 2 built
+  const auto ty2 = std::chrono::steady_clock::now();
+  {
+    YOp xop = yop;
+    xop.out = nullptr;
+    PartPlan xpp;
+    xpp.mcache = ypp.mcache;
+    xpp.mread = true;
+    S.plan(xop, m, xpp);
+    xop.xout = S.take<uint8_t>(SL_SEND, xpp.total + 1);
+    S.emit(xop, xpp);
+    uint32_t n2 = 0;
+    const uint8_t *xh = S.exchange<uint8_t>(xop.xout, xpp, SL_YXH, &n2);
+    if (n2 != ny) {
+      ctx->err = "Y X-hit count mismatch";
+      throw RK_E_INTERNAL;
+    }
+    S.hip(hipStreamWaitEvent(S.st, ctx->join, 0), "join wait");
+    if (ny) {
+      kt_begin(S.st);
+      k_merge_yx<<<grid_for(ny, 256), 256, 0, S.st>>>(ycode, xh, ny, yrec_l);
+      kt_end(S.st, KID_SH_MERGE, 0.0);
+      S.launched("k_merge_yx");
+    }
   }
-  S.plan(yop, m, pp);
-  yop.out = S.take<YRec>(SL_SEND, pp.total + 1);
-  S.emit(yop, pp);
-  uint32_t ny = 0;
-  const YRec *yr = S.exchange<YRec>(yop.out, pp, SL_YR, &ny);
-  ss.y_entries = ny;
-  const YView yv{yr, yb.b[me], yb.b[me + 1]};
-  uint8_t *ystate = S.take<uint8_t>(SL_YSTATE, ny + 1);
-  uint32_t *ywin = S.take<uint32_t>(SL_YWIN, ny + 1);
-  uint8_t *yused = S.take<uint8_t>(SL_YUSED, ny + 1);
-  auto solve_y = [&](const uint32_t *ymap, uint32_t c) {
-    ulonglong2 *yrec = S.take<ulonglong2>(SL_YRECL, c + 1);
-    uint32_t *ylh = fast32 ? nullptr : S.take<uint32_t>(SL_YLENHIL, c + 1);
-    uint32_t *keyy = S.take<uint32_t>(SL_KEYYL, c + 1);
-    uint32_t *par = S.take<uint32_t>(SL_PARL, c + 1);
+  auto y_results = [&](const uint32_t *ymap, uint32_t c, const uint32_t *par) {
     if (!c) return;
-    k_fill_y<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ymap, c, yrec, ylh, keyy, nby);
-    S.launched("k_fill_y");
-    AxisIn a{yrec, ylh, keyy, par, nullptr, c, (uint32_t)bit_length(2ull * nby - 1), max_y, false,
-             fast32};
-    resolve(S, a, p);
-    k_y_results<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ymap, c, par, ystate, ywin);
+    kt_begin(S.st);
+    k_y_results<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ycode, ymap, c, par, ystate, ywin);
+    kt_end(S.st, KID_SH_YRES, 0.0);
     S.launched("k_y_results");
   };
-  solve_y(nullptr, ny);
+  sweep_axis(S, ya, ycsr, p);
+  y_results(nullptr, ny, par_l);
+  // a fixed-halo re-resolution: the selected records, sorted again on stream 1
+  auto solve_y = [&](const uint32_t *ymap, uint32_t c) {
+    if (!c) return;
+    kt_begin(S.st);
+    k_fill_y<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ymap, c, yrec_l, ylh_l, keyy_l, nby,
+                                                  ycode, 0, 0);
+    kt_end(S.st, KID_SH_FILLY, 0.0);
+    S.launched("k_fill_y");
+    AxisIn a{yrec_l, ylh_l, keyy_l, par_l, nullptr, c, ybits, max_y, false, fast32};
+    resolve(S, a, kYSlots, p);
+    y_results(ymap, c, par_l);
+  };
   // relevant halo entries grouped by owner (the order owners send their states in)
-  RelOp relop{yv, yb, nullptr};
+  const uint64_t ylo = yb.b[me], yhi = yb.b[me + 1];
+  RelOp relop{ycode, ylo ? owner_of_host(yb, ylo - 1) : 0u,
+              yhi < nby ? owner_of_host(yb, yhi) : 0u, nullptr};
   S.plan(relop, ny, pp);
   const uint32_t nrel = (uint32_t)pp.total;
   uint32_t *relidx = S.take<uint32_t>(SL_RELIDX, nrel + 1);
@@ -1046,13 +1203,12 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
     S.launched("k_set_used");
   }
   YStateOp yso{};
-  yso.v = yv;
-  yso.P = P;
-  yso.me = me;
+  yso.code = ycode;
   yso.ystate = ystate;
-  for (uint32_t q = 0; q < MAXP; ++q) {
-    yso.lo[q] = q < P ? yb.b[q] : 0;
-    yso.hi[q] = q < P ? yb.b[q + 1] : 0;
+  for (uint32_t q = 0; q < P; ++q) {  // whose relevant halo holds my first / last bucket
+    if (q == me) continue;
+    if (yb.b[q + 1] == ylo) yso.first_mask |= 1u << q;
+    if (yb.b[q] == yhi) yso.last_mask |= 1u << q;
   }
   for (;;) {
     ++ss.y_rounds;
@@ -1081,7 +1237,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
       ++ss.y_reruns;
       k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, rys, nullptr, yused);
       S.launched("k_set_used");
-      SelYOp sel{yv, yused, nullptr};
+      SelYOp sel{ycode, yused, nullptr};
       Shard S1 = S;
       S1.P = 1;
       S1.me = 0;
@@ -1092,11 +1248,12 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
       solve_y(sel.out, (uint32_t)sp.total);
     }
   }
-  ss.ms_y = ms_since(ty);
+  ss.ms_y += ms_since(ty2);
+
 
   // ---- 5: parents back to the slice owners; roots; gids
   const auto tr = std::chrono::steady_clock::now();
-  ParOp pop{yv, slices, ywin, nullptr};
+  ParOp pop{yr, ycode, slices, ywin, nullptr};
   S.plan(pop, ny, pp);
   pop.out = S.take<ParRec>(SL_SEND, pp.total + 1);
   S.emit(pop, pp);
@@ -1111,10 +1268,17 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   uint32_t *lab = S.take<uint32_t>(SL_LAB, m + 1);
   uint32_t *cur = S.take<uint32_t>(SL_CUR, m + 1);
   if (m) {
+    kt_begin(S.st);
     k_par_init<<<grid_for(m, 256), 256, 0, S.st>>>(xg, m, parg);
-    if (npar)
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
+    if (npar) {
+      kt_begin(S.st);
       k_par_scatter<<<grid_for(npar, 256), 256, 0, S.st>>>(prr, npar, poff, m, parg, S.ctrl);
+      kt_end(S.st, KID_SHARD_AUX, 0.0);
+    }
+    kt_begin(S.st);
     k_local_par<<<grid_for(m, 256), 256, 0, S.st>>>(parg, m, poff, lpar, ext, isroot, S.ctrl);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
     S.launched("parents");
     Proc jp{};
     jp.par = lpar;
@@ -1136,8 +1300,10 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   uint64_t goff = 0, Gtot = 0;
   for (uint32_t q = 0; q < P; ++q) Gtot += rall[q], goff += q < me ? rall[q] : 0;
   if (m) {
+    kt_begin(S.st);
     k_init_labels<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, ext, lrank, (uint32_t)goff, m, lab,
                                                         cur);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
     S.launched("k_init_labels");
   }
   for (;;) {  // cross-slice links: request/response rounds (the owner answers
@@ -1171,7 +1337,9 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   }
   uint32_t *gid_own = junk;  // the jump's scratch is free again
   if (m) {
+    kt_begin(S.st);
     k_final_gid<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, lab, m, gid_own, S.ctrl);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
     S.launched("k_final_gid");
   }
   S.agree_errors();
@@ -1179,13 +1347,9 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
 
   // ---- 6: members -> gid-range owners; exact in-group order; emit
   const auto tm = std::chrono::steady_clock::now();
-  pr.hrec = S.take<ulonglong2>(SL_HREC, m + 1);
-  S.zero(S.ctrl + 6, 4);
-  sort_keys(pr, m, S.ctrl + 6, S.st);
-  S.launched("sort_keys");
-  bool narrow = true;
+  bool narrow = true;  // the sort keys came from stream 2 (joined before the Y sweeps)
   for (uint32_t w : S.gather1<uint32_t>(S.read1(S.ctrl + 6))) narrow &= w == 0;
-  MemOp mop{gid_own, pr.hrec, grow, {}, bin_shift(Gtot), nullptr};
+  MemOp mop{gid_own, pr.hrec, {}, bin_shift(Gtot), nullptr};
   const Bounds gb = split_bounds(global_hist(S, mop, m), mop.shift, Gtot, P);
   mop.B = gb;
   S.plan(mop, m, pp);
@@ -1206,7 +1370,9 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
     uint32_t *tag = S.take<uint32_t>(SL_TAG, mr + 1);
     uint32_t *otag = S.take<uint32_t>(SL_OTAG, mr + 1);
     void *gsort = S.take<uint8_t>(SL_GSORT, groupsort_scratch_bytes(mr));
+    kt_begin(S.st);
     k_mem_keys<<<grid_for(mr, 256), 256, 0, S.st>>>(mem, mr, g0, lg);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
     S.launched("k_mem_keys");
     const size_t rw = radix_scratch_words(mr);
     radix_sort_pairs(lg, nullptr, sgid, gmem, S.take<uint32_t>(SL_TK, mr),
