@@ -440,6 +440,7 @@ extern "C" int rk_create(rk_ctx **out, int device) {
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->aux, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void **)&ctx->host, 256 * sizeof(uint32_t), hipHostMallocDefault) !=
           hipSuccess) {
     rk_destroy(ctx);
@@ -477,6 +478,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
     if (e) (void)hipEventDestroy(e);
   if (ctx->fork) (void)hipEventDestroy(ctx->fork);
   if (ctx->join) (void)hipEventDestroy(ctx->join);
+  if (ctx->aux) (void)hipEventDestroy(ctx->aux);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

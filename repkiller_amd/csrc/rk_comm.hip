@@ -230,11 +230,13 @@ struct LocalComm final : rk_comm {
 
   int alltoallv(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb,
                 hipStream_t st) override {
+    // the send blocks were written by kernels on this rank's stream: complete
+    // them before another rank copies out of them
+    hipError_t e = hipStreamSynchronize(st);
     sh->ptr[rank] = send;
     sh->counts[rank] = sb;
     sh->barrier();
     size_t ro = 0;
-    hipError_t e = hipSuccess;
     for (int q = 0; q < size && e == hipSuccess; ++q) {
       const uint64_t *qsb = sh->counts[q];
       size_t so = 0;

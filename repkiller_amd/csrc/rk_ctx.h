@@ -24,6 +24,7 @@ struct rk_ctx {
   hipStream_t stream2 = nullptr;             // Y-axis sort, overlapped with the X sweeps
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t aux = nullptr;  // sharded driver: the X bucket order is ready (stream 2)
   void *ws = nullptr;  // device workspace
   size_t ws_cap = 0;
   uint32_t *host = nullptr;  // pinned readback words

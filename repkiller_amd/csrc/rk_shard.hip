@@ -1013,6 +1013,21 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
     S.launched("gather_proc");
   }
   const ulonglong2 *yrec_own = yrec_f + G;
+  // the X problem's bucket order (lead-in + own) is sorted on stream 2 while
+  // stream 1 exchanges the Y records
+  const uint32_t xbits = (uint32_t)bit_length(2ull * nbx - 1);
+  const AxisIn xa{xrec_f, nullptr, keyx_f, par_f, reinterpret_cast<uint32_t *>(yrec_f), G + m,
+                  xbits, max_x, true, fast32};
+  S.hip(hipEventRecord(ctx->fork, S.st), "fork");
+  S.hip(hipStreamWaitEvent(S.st2, ctx->fork, 0), "fork wait");
+  if (G) {
+    kt_begin(S.st2);
+    k_fill_ghost_x<<<grid_for(G, 256), 256, 0, S.st2>>>(gh, G, xrec_f, keyx_f, nbx);
+    kt_end(S.st2, KID_SHARD_AUX, 0.0);
+    S.launched("k_fill_ghost_x");
+  }
+  const Csr xcsr = sort_axis(S, xa, kXSlots, S.st2);
+  S.hip(hipEventRecord(ctx->aux, S.st2), "x sorted");
   ss.ms_x = ms_since(tx);
 
   // ---- 4a: Y records -> Y-centre-bucket ranges (+ halos).  They do not depend
@@ -1075,6 +1090,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
 
   // ---- 4b: X axis
   const auto tx2 = std::chrono::steady_clock::now();
+  // a fixed-halo re-resolution: the selected halo in [G - Gc, G), all on stream 1
   auto solve_x = [&](const GhostX *halo, uint32_t Gc) {
     const uint32_t base = G - Gc, n = Gc + m;
     if (Gc) {
@@ -1095,7 +1111,14 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
       S.launched("k_x_own");
     }
   };
-  solve_x(gh, G);
+  S.hip(hipStreamWaitEvent(S.st, ctx->aux, 0), "x sorted wait");
+  sweep_axis(S, xa, xcsr, p);
+  if (m) {
+    kt_begin(S.st);
+    k_x_own<<<grid_for(m, 256), 256, 0, S.st>>>(yrec_f + G, gh, G, poff, m, xg);
+    kt_end(S.st, KID_SH_XOWN, 0.0);
+    S.launched("k_x_own");
+  }
   if (G) {
     k_x_used<<<grid_for(G, 256), 256, 0, S.st>>>(yrec_f, G, xused);
     S.launched("k_x_used");

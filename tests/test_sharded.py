@@ -172,7 +172,7 @@ def test_cli_sharded_threads(tmp_path):
         shutil.copyfileobj(fi, fo)
     with gzip.open(os.path.join(GOLDEN, "corpus10k.out.csv.gz"), "rb") as f:
         want = f.read()
-    for gpus in (2, 3, 5):
+    for gpus in (2, 3, 5, 8):
         p = subprocess.run([rk.CLI_PATH, "--gpus", str(gpus), "--same-device", str(inp), str(out),
                             "0.05", "0.05", "0.3", "0.3"], capture_output=True, text=True,
                            timeout=300)
