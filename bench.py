@@ -169,6 +169,8 @@ def roofline_of(kt: dict, steps: int):
         kernels[name] = {"ms_per_step": round(k["total_ms"] / steps, 3),
                          "launches_per_step": round(k["launches"] / steps, 2),
                          "algo_GBps": round(gbps, 1) if gbps else None}
+    if not kt:  # profiling off (RK_BENCH_NOPROF)
+        return kernels, None
     dom = max(kt, key=lambda n: kt[n]["total_ms"])
     d = kt[dom]
     launch_ms = d["total_ms"] / max(1, d["launches"])
@@ -189,7 +191,7 @@ def timed(step, args, world, ctx):
     barriers + device syncs."""
     for _ in range(args.warmup):
         step()
-    ctx.set_profiling(True)
+    ctx.set_profiling(not os.environ.get("RK_BENCH_NOPROF"))  # A/B of the timers' own cost
     ctx.reset_phases()
     torch.cuda.synchronize()
     barrier(world)

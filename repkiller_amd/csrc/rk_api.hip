@@ -46,6 +46,20 @@ namespace rk {
 void collect_kernel_timing(rk_ctx *ctx) {
   g_ktimer = nullptr;
   if (ctx->kt.n) (void)hipEventSynchronize(ctx->kt.ev[2 * ctx->kt.n - 1]);
+  if (ctx->kt.tier_counts) {  // the group-sort tiers' algorithmic bytes
+    const uint32_t nb = ctx->kt.tier_nblk;
+    std::vector<uint32_t> h((size_t)KernelTimer::TIERS * nb);
+    if (hipMemcpy(h.data(), ctx->kt.tier_counts, (size_t)7 * nb * 4, hipMemcpyDeviceToHost) ==
+        hipSuccess) {
+      for (int u = 0; u < 7; ++u) {
+        double mem = 0;
+        for (uint32_t b = 0; b < nb; ++b) mem += h[(size_t)u * nb + b];
+        const int sl = ctx->kt.tier_slot[u];
+        if (sl >= 0 && sl < ctx->kt.n) ctx->kt.bytes[sl] = 16.0 * mem;
+      }
+    }
+    ctx->kt.tier_counts = nullptr;
+  }
   for (int i = 0; i < ctx->kt.n; ++i) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, ctx->kt.ev[2 * i], ctx->kt.ev[2 * i + 1]) == hipSuccess) {
@@ -446,13 +460,15 @@ extern "C" int rk_create(rk_ctx **out, int device) {
     rk_destroy(ctx);
     return RK_E_HIP;
   }
+  // timing-only events: no system-scope fence at record (HIP's recommendation
+  // for pure timing events; it keeps the instrumentation's own cost low)
   for (auto &e : ctx->kt.ev)
-    if (hipEventCreate(&e) != hipSuccess) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
       rk_destroy(ctx);
       return RK_E_HIP;
     }
   for (auto &e : ctx->pev)
-    if (hipEventCreate(&e) != hipSuccess) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
     rk_destroy(ctx);
     return RK_E_HIP;
   }

@@ -655,24 +655,24 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   }
   kt_begin(s2);
   k_sort_small<<<grid_for(m, 256), 256, 0, s2>>>(gid_sorted, goff, m, key, tag, otag);
-  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in below from the tier sizes
-  const int small_slot = timing ? g_ktimer->n - 1 : -1;
+  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
+  if (timing) {
+    g_ktimer->tier_nblk = nblk;
+    for (int u = 0; u < KernelTimer::TIERS; ++u) g_ktimer->tier_slot[u] = -1;
+    g_ktimer->tier_slot[0] = g_ktimer->n - 1;
+  }
   k_tier_count<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, bc, timing ? bm : nullptr);
   (void)hipMemsetAsync(bc + (size_t)NL * nblk, 0, 4, st);
   exclusive_scan_u32(bc, boff, (size_t)NL * nblk + 1, ss, st);
   k_tier_lists<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, boff, list);
   const TierLists tl{list, boff, nblk};
   // algorithmic bytes of every tier (timing only): each member's (key, tag)
-  // read, its tag written once at its final slot
-  double members[NTIER] = {};
-  if (timing) {
-    std::vector<uint32_t> h((size_t)NTIER * nblk);
-    (void)hipMemcpyAsync(h.data(), bm, h.size() * 4, hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
-    for (int u = 0; u < NTIER; ++u)
-      for (uint32_t b2 = 0; b2 < nblk; ++b2) members[u] += h[(size_t)u * nblk + b2];
-    g_ktimer->bytes[small_slot] = 16.0 * members[0];
-  }
+  // read, its tag written once at its final slot -- 16 B x the tier's members,
+  // filled in from bm when the timings are collected
+  if (timing) g_ktimer->tier_counts = bm;
+  auto tier_slot = [&](int u) {
+    if (timing && g_ktimer->n > 0) g_ktimer->tier_slot[u] = g_ktimer->n - 1;
+  };
   (void)host_words;
   // fixed grids: every kernel reads its list range on the device
   if (side) {
@@ -681,7 +681,8 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   }
   kt_begin(s2);
   k_sort_groups_reg<<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
-  kt_end(s2, KID_SORT_REG, 16.0 * members[1]);
+  kt_end(s2, KID_SORT_REG, 0.0);
+  tier_slot(1);
   if (side) (void)hipEventRecord(ev_join, s2);
   for (int j = 0; j < NLDS; ++j) {
     const uint32_t cap = caps.c[j];
@@ -693,12 +694,14 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     else
       k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), st>>>(tl, 2 + j, goff, key, tag,
                                                                        otag, cap);
-    kt_end(st, KID_SORT_LDS, 16.0 * members[2 + j]);
+    kt_end(st, KID_SORT_LDS, 0.0);
+    tier_slot(2 + j);
   }
   kt_begin(st);
   k_sort_groups_global<<<1024, 64, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
                                             frames);
-  kt_end(st, KID_SORT_GLOBAL, 16.0 * members[NTIER - 1]);
+  kt_end(st, KID_SORT_GLOBAL, 0.0);
+  tier_slot(NTIER - 1);
   if (side) (void)hipStreamWaitEvent(st, ev_join, 0);
 }
 

@@ -65,6 +65,12 @@ struct KernelTimer {
   int kid[MAX];
   double bytes[MAX];
   int n;
+  // group-sort tiers: their member counts exist on the device only; they are
+  // read back when the call's timings are collected (no sync inside the call)
+  static constexpr int TIERS = 8;
+  const uint32_t *tier_counts;  // [tier][nblk] members per block, or null
+  uint32_t tier_nblk;
+  int tier_slot[TIERS];         // timer slot of each tier's launch (-1: none)
 };
 extern thread_local KernelTimer *g_ktimer;
 inline void kt_begin(hipStream_t st) {
