@@ -83,6 +83,8 @@ SYNTH = [
     dict(kind="synth", n=200_000, L=20_000_000, seed=21),
     dict(kind="synth", n=200_000, L=20_000_000, seed=22, lr=0.05, pr=0.05),
     dict(kind="synth", n=100_000, L=10_000_000, seed=23, ff=0.95, copies=(100, 600)),
+    # cfg5's shape (repeat-rich, long bucket runs, groups of thousands) at 1M
+    dict(kind="synth", n=1_000_000, L=150_000_000, seed=28, ff=0.95, copies=(100, 600)),
     # dense: ~40 entries per 100-bp bucket and strand, no lead-in -> reruns
     dict(kind="synth", n=20_000, L=60_000, seed=24, lead_in=0),
     dict(kind="synth", n=20_000, L=60_000, seed=25, lead_in=0, lr=1.5, pr=0.7),
