@@ -56,6 +56,11 @@ CONFIGS = {
     # one MI355X (~62 GB of HBM), so it runs here as a single-GPU stress case
     "cfg4": dict(n=200_000_000, genome_len=3_000_000_000,
                  desc="cfg4: 200M fragments, 3 Gbp x 3 Gbp"),
+    # BASELINE.json configs[4] is quoted for 8 GPUs ("streaming / HBM-spill");
+    # its 1B fragments fit one MI355X's HBM too (run it with --no-cpu)
+    "cfg5": dict(n=1_000_000_000, genome_len=15_000_000_000,
+                 synth=dict(family_frac=0.95, copies=(100, 600)),
+                 desc="cfg5: 1B fragments, 15 Gbp repeat-rich self-comparison"),
 }
 
 
@@ -216,7 +221,7 @@ def upload(f, dev):
 def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
     """ONE fragment set of n x world rows, rank r holding rows [r*n, (r+1)*n)."""
     n, L = cfg["n"], cfg["genome_len"]
-    f = rk.synth(n, L, seed=rank_seed(rank))  # this rank's block of the one set
+    f = rk.synth(n, L, seed=rank_seed(rank), **cfg.get("synth", {}))  # this rank's block
     x, y, ln, s = upload(f, dev)
     del f
     comm = (rk.Comm.rccl(rank, world, local) if args.comm == "rccl"
@@ -250,7 +255,7 @@ def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
 def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
     """rk_classify_device on this rank's own fragment set (inputs resident in HBM)."""
     n, L = cfg["n"], cfg["genome_len"]
-    f = rk.synth(n, L, seed=rank_seed(rank))  # independent fragment set per rank
+    f = rk.synth(n, L, seed=rank_seed(rank), **cfg.get("synth", {}))  # own set per rank
     x, y, ln, s = upload(f, dev)
     gid = torch.empty(n, dtype=torch.int32, device=dev)
     rep = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -269,7 +274,7 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
 
     # PCIe-inclusive rate (host buffers in and out), reported beside value, never as it
     pcie = None
-    if rank == 0 and args.config != "cfg1":
+    if rank == 0 and args.config in ("cfg2", "cfg3", "cfg4"):  # cfg5: no HBM for a 2nd copy
         fh = rk.Frags(x.cpu().numpy().view(np.uint64), y.cpu().numpy().view(np.uint64),
                       ln.cpu().numpy().view(np.uint64), s.cpu().numpy())
         ctx.classify(fh, L, L, args.len_ratio, args.pos_ratio)

@@ -169,14 +169,24 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.radix_words = rk::radix_scratch_words((uint32_t)n);
   w.radix = c.take<uint32_t>(w.radix_words);
   w.radix2 = c.take<uint32_t>(w.radix_words);
-  w.p.rec = c.take<ulonglong2>(2 * n);
+  // the file-order records are dead once gather_proc has read them: the
+  // in-group sort keys and the member stage's arrays reuse their 32 B / entry
+  w.p.rec = c.take<ulonglong2>(2 * n + 64);
+  {
+    char *r = reinterpret_cast<char *>(w.p.rec);
+    const size_t o1 = rk::align_up(16 * n + 64), o2 = o1 + rk::align_up(8 * n + 64),
+                 o3 = o2 + rk::align_up(4 * n + 64);  // + slack, like every take()
+    w.p.hrec = reinterpret_cast<ulonglong2 *>(r);
+    w.reckey = reinterpret_cast<uint64_t *>(r + o1);
+    w.tag = reinterpret_cast<uint32_t *>(r + o2);
+    w.otag = reinterpret_cast<uint32_t *>(r + o3);
+  }
   w.p.ys = c.take<uint64_t>(n);
   w.p.pkey = c.take<uint32_t>(n);
   w.p.row = c.take<uint32_t>(n);
   w.p.xrec = c.take<ulonglong2>(n);
   w.p.yrec = c.take<ulonglong2>(n);
-  w.p.ylenhi = c.take<uint32_t>(n);
-  w.p.hrec = c.take<ulonglong2>(n);
+  w.p.ylenhi = nullptr;  // 64-bit lengths only: ensure_wide
   w.p.keyx = c.take<uint32_t>(n);
   w.p.keyy = c.take<uint32_t>(n);
   w.p.par = c.take<uint32_t>(n);
@@ -185,8 +195,7 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   for (rk::Csr *cs : {&w.cx, &w.cy}) {
     cs->key = c.take<uint32_t>(n);
     cs->ent = c.take<uint32_t>(n);
-    cs->cen = c.take<uint64_t>(n);
-    cs->len = c.take<uint64_t>(n);
+    cs->cen = cs->len = nullptr;  // 64-bit lengths only: ensure_wide
     cs->state = c.take<uint8_t>(n);
     cs->pk = c.take<uint2>(n);
     cs->nbd = c.take<uint8_t>(n);
@@ -196,10 +205,7 @@ size_t carve(Carve &c, const Plan &pl, Work &w) {
   w.sgid = c.take<uint32_t>(n);
   w.gmem = c.take<uint32_t>(n);
   w.goff = c.take<uint32_t>(n);
-  w.tag = c.take<uint32_t>(n);
-  w.otag = c.take<uint32_t>(n);
   w.gsort = c.take<uint8_t>(rk::groupsort_scratch_bytes((uint32_t)n));
-  w.reckey = c.take<uint64_t>(n);
   w.rpend = c.take<uint32_t>(n / 4 + 1);
   w.wpend = c.take<uint8_t>(n / 64 + 1);
   w.runs = c.take<uint32_t>(rk::runs_scratch_words((uint32_t)n));
@@ -233,6 +239,32 @@ int ensure_ws(rk_ctx *ctx, const Plan &pl, Work &w) {
 rk::SweepScratch sweep_scratch(const Work &w) {
   return rk::SweepScratch{w.runs, w.wpend, reinterpret_cast<uint8_t *>(w.rpend), w.ctrl + 64,
                           w.ctrl + 2};
+}
+
+// The 64-bit centre/length copies of both axes and the Y lengths' high words,
+// needed only when some length is >= 2^31 (the generic sweep kernel): a
+// second grow-only buffer, so the common case does not carry 36 B per entry.
+int ensure_wide(rk_ctx *ctx, size_t n1, Work &w) {
+  const size_t n = n1 + 1;
+  const size_t need = rk::align_up(4 * n) + 4 * rk::align_up(8 * n);
+  if (need > ctx->ws_wide_cap) {
+    if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
+    ctx->ws_wide = nullptr;
+    ctx->ws_wide_cap = 0;
+    hipError_t e = hipMalloc(&ctx->ws_wide, need);
+    if (e != hipSuccess) {
+      ctx->err = std::string("64-bit workspace hipMalloc: ") + hipGetErrorString(e);
+      return e == hipErrorOutOfMemory ? RK_E_NOMEM : RK_E_HIP;
+    }
+    ctx->ws_wide_cap = need;
+  }
+  Carve c{(char *)ctx->ws_wide};
+  w.p.ylenhi = c.take<uint32_t>(n);
+  w.cx.cen = c.take<uint64_t>(n);
+  w.cx.len = c.take<uint64_t>(n);
+  w.cy.cen = c.take<uint64_t>(n);
+  w.cy.len = c.take<uint64_t>(n);
+  return RK_OK;
 }
 
 // mark the START of phase `ph` (ph == RK_N_PHASES marks the end of the last)
@@ -338,10 +370,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
 
   // 3: processing-order SoA, bucket keys, in-group sort keys
   mark(ctx, RK_PH_GATHER);
-  if (fast32) {  // every length fits 32 bits: the 64-bit centre/length copies are unused
-    w.p.ylenhi = nullptr;
-    w.cx.cen = w.cx.len = w.cy.cen = w.cy.len = nullptr;
-  }
+  if (!fast32 && (rc = ensure_wide(ctx, pl.n, w))) return rc;  // some length >= 2^31
   rk::gather_proc(f, w.p, m, pl.nbx, pl.nby, st);
 
   // 4: the two occupancy axes as bucket runs (stable: processing order inside).
@@ -483,6 +512,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->io) (void)hipFree(ctx->io);
+  if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
   for (void *p : ctx->pool.ptr)
     if (p) (void)hipFree(p);
   if (ctx->host) (void)hipHostFree(ctx->host);

@@ -27,6 +27,8 @@ struct rk_ctx {
   hipEvent_t aux = nullptr;  // sharded driver: the X bucket order is ready (stream 2)
   void *ws = nullptr;  // device workspace
   size_t ws_cap = 0;
+  void *ws_wide = nullptr;  // 64-bit length columns, only when a length is >= 2^31
+  size_t ws_wide_cap = 0;
   uint32_t *host = nullptr;  // pinned readback words
   // device copies for rk_classify (host-buffer entry point)
   void *io = nullptr;
