@@ -899,6 +899,257 @@ __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big
   }
 }
 
+// ---- long runs on the 32-bit records: 64 entries at a time -----------------
+// k_sweep_wave decides a long run's entries one after another, each with a
+// wave-wide scan of every earlier entry: O(run^2 / 64) dependent steps, which
+// dominates repeat-rich sets (cfg5: ~93 % of the entries sit in runs of
+// 100-800).  Here lane l owns entry cb + l of the chunk [cb, cb + 64), and the
+// chunk is decided like a short-run window (sweep_window32): each open entry
+// gathers its candidates as
+//   * a bit mask over the earlier lanes of its chunk,
+//   * a summary of the run's earlier chunks, read from an LDS list that keeps
+//     only their ACTIVE and UNKNOWN entries (a HIT or HIT_PENDING entry is
+//     never in the reference's list again; a run's states change only in this
+//     walk, so the list is exact),
+//   * a summary of the neighbour run's entries inserted before it, read from
+//     an LDS list of that run's ACTIVE / UNKNOWN entries made once per run
+//     (states only leave that set; they are re-read at every chunk),
+// then rounds of ballots decide the chunk.  Scan order and tie rule are the
+// reference's: own run newest first (this chunk, then the list, newest
+// first), then the neighbour run newest first; the first strict maximum wins.
+// A list that would overflow hands the rest of the run to the entry-by-entry
+// walk (own list) or to a per-entry global scan (neighbour list).
+__device__ __forceinline__ int below_count(uint64_t m) {  // set bits below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+constexpr int LCAP = 128;  // own-run list
+constexpr int NCAP = 64;   // neighbour-run list, per side
+
+struct LongLds {
+  uint2 cpk[64 + OWN_U];
+  uint32_t cent[64];
+  uint2 lpk[LCAP];
+  uint32_t lpos[LCAP], lent[LCAP];
+  uint8_t lst[LCAP];
+  uint2 npk[2][NCAP];
+  uint32_t npos[2][NCAP], nent[2][NCAP];
+  uint8_t nst[2][NCAP];
+};
+
+// the entry-by-entry walk of k_sweep_wave<true> over [from, end) of run [beg, end)
+__device__ bool walk_entries32(const Axis &ax, uint32_t beg, uint32_t from, uint32_t end,
+                               bool has_lo, uint32_t lo_b, uint32_t lo_e, bool has_hi,
+                               uint32_t hi_b, uint32_t hi_e, uint32_t lane) {
+  bool pending = false;
+  for (uint32_t t = from; t < end; ++t) {
+    const uint8_t st = load_state(&ax.state[t]);
+    if (st == ST_ACTIVE || st == ST_HIT) continue;
+    const uint32_t i = ax.ent[t];
+    const uint2 me = ax.pk[t];
+    const Q32 q32 = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
+    const int dir = ax.nbd[t] == 1 ? -1 : ax.nbd[t] == 2 ? 1 : 0;
+    Scan s{0.0, NONE, 0xFFFFFFFFu, false, false};
+    for (uint32_t q0 = beg; q0 < t; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      if (q < t) consider_ranked32(ax, s, q, t - 1 - q, q32);
+    }
+    if ((dir < 0 && has_lo) || (dir > 0 && has_hi)) {
+      const uint32_t nb = dir < 0 ? lo_b : hi_b, ne = dir < 0 ? lo_e : hi_e;
+      const uint32_t own = t - beg;
+      for (uint32_t q0 = nb; q0 < ne; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        if (q < ne && ax.ent[q] < i) consider_ranked32(ax, s, q, own + (ne - 1 - q), q32);
+      }
+    }
+    wave_combine(s);
+    const uint8_t ns = decide(s);
+    if (lane == 0) {
+      if (ns != st && (ns == ST_HIT || ns == ST_ACTIVE))
+        record_decision(ax, i, ns, ns == ST_HIT ? ax.ent[s.win] : NONE);
+      if (ns != st) store_state(&ax.state[t], ns);
+    }
+    pending |= ns == ST_UNKNOWN || ns == ST_HIT_PENDING;
+  }
+  return pending;
+}
+
+// the neighbour run [nb, ne)'s ACTIVE / UNKNOWN entries into side `sd` of the
+// LDS lists; returns their count, or -1 when they do not fit
+__device__ int neighbour_list(const Axis &ax, uint32_t nb, uint32_t ne, LongLds &L, int sd,
+                              uint32_t lane) {
+  int n = 0;
+  for (uint32_t q0 = nb; q0 < ne; q0 += 64) {
+    const uint32_t q = q0 + lane;
+    const uint8_t s = q < ne ? load_state(&ax.state[q]) : ST_HIT;
+    const bool keep = s < ST_HIT_PENDING;
+    const uint64_t b = __ballot(keep);
+    const int at = n + below_count(b);
+    if (n + __popcll(b) > NCAP) return -1;
+    if (keep) {
+      L.npk[sd][at] = ax.pk[q];
+      L.npos[sd][at] = q;
+      L.nent[sd][at] = ax.ent[q];
+      L.nst[sd][at] = s;
+    }
+    n += __popcll(b);
+  }
+  return n;
+}
+
+__global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint32_t *big,
+                                                      const uint32_t *nbig_dev, uint8_t *rpend,
+                                                      uint32_t *counters) {
+  __shared__ LongLds s_l[4];
+  const uint32_t lane = threadIdx.x & 63;
+  LongLds &L = s_l[threadIdx.x >> 6];
+  const uint32_t count = *nbig_dev;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < count;
+       w += (gridDim.x * blockDim.x) >> 6) {
+    const uint32_t beg = big[w];
+    if (!rpend[beg]) continue;
+    const uint32_t key = ax.key[beg];
+    const uint32_t end = wave_scan_end(ax, beg + LONG_RUN, key, lane);
+    uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
+    const bool has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
+    if (has_lo) lo_e = beg, lo_b = wave_scan_begin(ax, beg, key - 1, lane);
+    const bool has_hi = end < ax.m && ax.key[end] == key + 1;
+    if (has_hi) hi_b = end, hi_e = wave_scan_end(ax, end + 1, key + 1, lane);
+    wave_sync_lds();  // the previous run's LDS reads are done
+    const int nn0 = has_lo ? neighbour_list(ax, lo_b, lo_e, L, 0, lane) : 0;
+    const int nn1 = has_hi ? neighbour_list(ax, hi_b, hi_e, L, 1, lane) : 0;
+    int nl = 0;
+    bool pending = false;
+    uint32_t cb = beg;
+    for (; cb < end; cb += 64) {
+      const uint32_t t = cb + lane;
+      const bool in = t < end;
+      uint2 me = make_uint2(0, 0);
+      uint32_t i = 0;
+      uint8_t st = ST_HIT, nd = 0;
+      if (in) me = ax.pk[t], i = ax.ent[t], st = load_state(&ax.state[t]), nd = ax.nbd[t];
+      wave_sync_lds();  // the previous chunk's LDS reads are done
+      L.cpk[lane] = me;
+      L.cent[lane] = i;
+      if ((int)lane < nn0) L.nst[0][lane] = load_state(&ax.state[L.npos[0][lane]]);
+      if ((int)lane < nn1) L.nst[1][lane] = load_state(&ax.state[L.npos[1][lane]]);
+      wave_sync_lds();
+      const uint8_t st0 = st;
+      const bool open = in && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
+      uint64_t rown = 0;
+      Scan fl{0.0, NONE, 0, false, false}, fn{0.0, NONE, 0, false, false};
+      Q32 q{};
+      if (open) {
+        q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
+        for (int j = 0; j < (int)lane; j += OWN_U) {
+          uint64_t b4 = 0;
+#pragma unroll
+          for (int u = 0; u < OWN_U; ++u) b4 |= (uint64_t)m32(q, L.cpk[j + u]) << u;
+          if ((int)lane - j < OWN_U) b4 &= (1ull << ((int)lane - j)) - 1ull;
+          rown |= b4 << j;
+        }
+        for (int k = nl - 1; k >= 0; --k) {  // earlier chunks, newest first
+          const uint8_t sk = L.lst[k];
+          const uint2 o = L.lpk[k];
+          if (!m32(q, o)) continue;
+          if (sk != ST_ACTIVE) {
+            fl.any_unknown = true;
+            continue;
+          }
+          const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
+          if (d > fl.best) fl.best = d, fl.win = L.lent[k];
+          fl.any_active = true;
+        }
+        const int dir = nd == 1 ? -1 : nd == 2 ? 1 : 0;
+        const int sd = dir < 0 ? 0 : 1;
+        const int nn = dir < 0 ? nn0 : nn1;
+        if (dir != 0 && (dir < 0 ? has_lo : has_hi)) {
+          if (nn >= 0) {
+            for (int k = nn - 1; k >= 0; --k) {  // newest first
+              if (L.nent[sd][k] >= i) continue;
+              const uint8_t sk = L.nst[sd][k];
+              if (sk >= ST_HIT_PENDING) continue;
+              const uint2 o = L.npk[sd][k];
+              if (!m32(q, o)) continue;
+              if (sk != ST_ACTIVE) {
+                fn.any_unknown = true;
+                continue;
+              }
+              const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
+              if (d > fn.best) fn.best = d, fn.win = L.nent[sd][k];
+              fn.any_active = true;
+            }
+          } else {  // list overflow: the global scan of the short-run kernel
+            foreign_scan32(ax, dir < 0 ? beg - 1 : end, dir, key + dir, i, q, fn);
+          }
+        }
+      }
+      const bool out_act = fl.any_active || fn.any_active;
+      const bool out_unk = fl.any_unknown || fn.any_unknown;
+      for (;;) {
+        const uint64_t A = __ballot(in && st == ST_ACTIVE);
+        const uint64_t U = __ballot(in && st == ST_UNKNOWN);
+        bool changed = false;
+        if (open && st == ST_UNKNOWN) {
+          if ((A & rown) || out_act) st = ST_HIT_PENDING, changed = true;
+          else if (!(U & rown) && !out_unk) st = ST_ACTIVE, changed = true;
+        }
+        const uint64_t V = __ballot(in && st == ST_UNKNOWN);
+        if (open && st == ST_HIT_PENDING && !(V & rown) && !out_unk) st = ST_HIT, changed = true;
+        const bool left = open && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
+        if (!__ballot(changed) || !__ballot(left)) break;
+      }
+      const uint64_t A = __ballot(in && st == ST_ACTIVE);
+      pending |= open && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
+      if (open && st != st0) {
+        if (st == ST_HIT) {
+          double best = 0.0;
+          uint32_t win = NONE;
+          uint64_t b = A & rown;
+          while (b) {  // this chunk, newest first
+            const int v = 63 - __clzll(b);
+            b &= ~(1ull << v);
+            const double d = dev32(q, L.cpk[v], ax.len_ratio, ax.pos_ratio);
+            if (d > best) best = d, win = L.cent[v];
+          }
+          if (fl.any_active && fl.best > best) best = fl.best, win = fl.win;
+          if (fn.any_active && fn.best > best) win = fn.win;
+          record_decision(ax, i, ST_HIT, win);
+        } else if (st == ST_ACTIVE) {
+          record_decision(ax, i, ST_ACTIVE, NONE);
+        }
+        store_state(&ax.state[t], st);
+      }
+      // this chunk's ACTIVE / UNKNOWN entries join the list
+      const bool keep = in && (st == ST_ACTIVE || st == ST_UNKNOWN);
+      const uint64_t kb = __ballot(keep);
+      if (nl + __popcll(kb) > LCAP) {
+        cb += 64;
+        break;
+      }
+      wave_sync_lds();  // the list reads of this chunk are done
+      if (keep) {
+        const int at = nl + below_count(kb);
+        L.lpk[at] = me;
+        L.lpos[at] = t;
+        L.lent[at] = i;
+        L.lst[at] = st;
+      }
+      nl += __popcll(kb);
+    }
+    if (cb < end) {  // own list overflow: the rest entry by entry
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      pending |= walk_entries32(ax, beg, cb, end, has_lo, lo_b, lo_e, has_hi, hi_b, hi_e, lane);
+    }
+    const bool pend = __ballot(pending) != 0;
+    if (lane == 0) {
+      rpend[beg] = pend;
+      if (pend) atomicAdd(&counters[w % PEND_SLOTS], 1u);
+    }
+  }
+}
+
 // Run bounds of every bucket run, one wavefront per 64 positions: rlen_at at
 // each run start, rbeg_at at each run end, and the starts of the runs longer
 // than LONG_RUN appended to `big` (one atomic per wave).  A run crossing the
@@ -1013,7 +1264,7 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   }
   if (rl.fast32) {  // the long-run count lives on the device: a fixed grid reads it
     kt_begin(st);
-    k_sweep_wave<true><<<256, 256, 0, st>>>(ax, rl.big, 0, rl.nbig_dev, rpend, counters);
+    k_sweep_long32<<<2048, 256, 0, st>>>(ax, rl.big, rl.nbig_dev, rpend, counters);
     kt_end(st, KID_SWEEP_WAVE, 0.0);
   } else if (rl.nbig) {
     kt_begin(st);

@@ -94,6 +94,43 @@ with open(os.path.join(GOLDEN, "boundary_hashes.json")) as _f:
     BOUNDARY = json.load(_f)
 
 
+def long_run_set(runs_len: int, seed: int) -> rk.Frags:
+    """Consecutive 100-bp buckets, each holding `runs_len` entries on both axes:
+    centres anywhere in the bucket (4 % of them at the edges, which probe the
+    neighbour bucket), lengths on a x1.5 ladder (8 .. 2.3e6) so few entries
+    match each other -- with tight ratios a run keeps more than 128 ACTIVE
+    entries and its neighbour more than 64 (the LDS lists of k_sweep_long32
+    overflow), with wide ratios the lists hold -- and repeated (centre,
+    length) pairs, which hit."""
+    rng = np.random.default_rng(seed)
+    nb = 24
+    b0 = 20_000  # centres >= 2 Mbp: every ladder length fits before its centre
+    n = nb * runs_len
+    bucket = np.repeat(np.arange(nb), runs_len) + b0
+    off = rng.integers(0, 100, n)
+    L = np.round(8 * 1.5 ** rng.integers(0, 32, n)).astype(np.int64)
+    dup = rng.random(n) < 0.3  # copy an earlier entry of the same bucket
+    src = np.maximum(np.arange(n) - rng.integers(1, runs_len, n), 0)
+    same = (bucket[src] == bucket) & dup
+    off[same], L[same] = off[src[same]], L[src[same]]
+    c = bucket * 100 + off
+    x = c - L // 2
+    y = x + rng.choice([0, 3_000_000], n)
+    strand = np.where(rng.random(n) < 0.5, ord("f"), ord("r")).astype(np.uint8)
+    perm = rng.permutation(n)  # file order is not processing order
+    return rk.Frags(x[perm].astype(np.uint64), y[perm].astype(np.uint64),
+                    L[perm].astype(np.uint64), strand[perm])
+
+
+@pytest.mark.parametrize("runs_len", [70, 300, 2500])
+@pytest.mark.parametrize("lr,pr", [(0.05, 0.05), (0.3, 0.3), (1.5, 0.7)])
+def test_long_runs_vs_oracle(gpu_ctx, runs_len, lr, pr):
+    """Bucket runs longer than 64 entries (the long-run sweep), including runs
+    whose ACTIVE entries overflow its LDS lists."""
+    f = long_run_set(runs_len, seed=runs_len)
+    gpu_vs_oracle(gpu_ctx, f, 10_000_000, 10_000_000, lr, pr)
+
+
 @pytest.mark.parametrize("lr,pr", bc.RATIOS)
 def test_deviation_boundaries(gpu_ctx, tmp_path, lr, pr):
     """sl == 0 / sp == 0 boundaries and NaN/inf/extreme ratios: bit-exact with
