@@ -34,10 +34,10 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_sort_keys",     "k_csr_fill_x",      "k_run_bounds",    "k_sweep_tile",
     "k_sweep_fast",    "k_sweep_fast_more", "k_sweep_wave",    "k_csr_fill_y",    "k_jump",
     "k_assign_gid",    "k_group_offsets",   "k_build_records",
-    "k_sort_small",    "k_sort_groups_reg", "k_sort_groups_lds", "k_sort_groups_global",
+    "k_sort_small",    "k_sort_groups_reg", "k_sort_groups_lds", "k_sort_groups_split",
     "k_emit",          "k_part (sharded)", "exchange (sharded)", "k_aux (sharded)",
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
-    "k_merge_yx (sharded)",
+    "k_merge_yx (sharded)", "k_sort_segments",
 };
 }  // namespace rk
 
@@ -56,6 +56,8 @@ void collect_kernel_timing(rk_ctx *ctx) {
         for (uint32_t b = 0; b < nb; ++b) mem += h[(size_t)u * nb + b];
         const int sl = ctx->kt.tier_slot[u];
         if (sl >= 0 && sl < ctx->kt.n) ctx->kt.bytes[sl] = 16.0 * mem;
+        const int s2 = u == 6 ? ctx->kt.tier_slot[7] : -1;  // the large tier's phase B
+        if (s2 >= 0 && s2 < ctx->kt.n) ctx->kt.bytes[s2] = 16.0 * mem;
       }
     }
     ctx->kt.tier_counts = nullptr;

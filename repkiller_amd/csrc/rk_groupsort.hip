@@ -346,10 +346,10 @@ struct Frame {
 // leaf ranks written to out[0..n) (tags only)
 template <bool GLOBAL, class V>
 __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stack,
-                              Frame *smallq, Frame *heapq, uint32_t lane) {
+                              Frame *smallq, Frame *heapq, uint32_t lane, int d0) {
   for (uint32_t x = lane; x < n; x += 64) v.B[x] = 0;
   int sp = 0, nsmall = 0, nheap = 0;
-  if (lane == 0) stack[0] = {0u, n, 2 * (31 - __clz((int)n))};
+  if (lane == 0) stack[0] = {0u, n, d0};
   sp = 1;
   sync_mem<GLOBAL>();
   while (sp) {
@@ -481,31 +481,225 @@ __global__ void __launch_bounds__(64) k_sort_groups_lds(TierLists tl, int tier,
       T[x] = tag[b + x];
     }
     wave_sync();
-    wave_std_sort<false>(v, n, otag + b, stack, smallq, heapq, lane);
+    wave_std_sort<false>(v, n, otag + b, stack, smallq, heapq, lane, 2 * (31 - __clz((int)n)));
     wave_sync();
   }
 }
 
-// global tier: same code on the group's own slices of global scratch.  Frame
-// storage of the w-th listed group starts at (b >> 3) + 80 * w: regions of
-// consecutive listed groups never overlap (a group of n members needs at most
-// 72 + 2 * (n / 17 + 2) frames).
-__global__ void __launch_bounds__(64) k_sort_groups_global(TierLists tl, int tier,
+// Groups above the largest LDS cap (repeat families: 10^4 - 10^6 members)
+// run in two phases.
+//
+// Phase A, one 256-thread block per group: the introsort loop on the group's
+// slice of global memory, but only segments of more than SPLIT_T members are
+// partitioned here, each by the whole block -- stopper lists from two
+// ballot passes (counts, then ranked writes; each wave owns a quarter of the
+// segment), K by a 256-ary search (the stop predicate Lpos[k] >= Rpos[k] is
+// monotone in k), the K swaps in parallel.  A segment that reaches SPLIT_T
+// members or less is final for this phase: its start gets bnd = 1 and
+// head = length | depth << 16.  (A segment above SPLIT_T whose depth budget
+// is spent is heap-sorted here by one thread -- libstdc++'s own fallback --
+// and written out directly.)  Stopper lists of a segment [f, l) live in
+// pl/pr[f, l), so final segments' heads are never overwritten.
+//
+// Phase B, one wavefront per final segment (found by scanning bnd over 64
+// positions per step): the LDS introsort of the other tiers, started with the
+// segment's remaining depth budget, writing the segment's final order.
+// Together the two phases are the libstdc++ recursion exactly: sibling
+// segments are independent, and every segment keeps its own depth budget.
+constexpr uint32_t SPLIT_T = 2048;
+constexpr int SPLIT_STACK = 72;  // one frame per level: 2 * log2(2^32) + slack
+
+__device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint32_t *PR,
+                                    uint32_t f, uint32_t l, uint32_t *s_w) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) median_to_first(GView{K, T, nullptr, nullptr, nullptr}, f, l);
+  __syncthreads();
+  const uint64_t p = K[f];
+  const uint32_t len = l - f;
+  const uint32_t per = ((len + 3) / 4 + 255) & ~255u;  // a wave's share, 4 x 64 aligned
+  const uint32_t a = f + wv * per;
+  const uint32_t e = a + per < l ? a + per : l;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  // pass 1: stopper counts of this wave's share
+  uint32_t cl = 0, cr = 0;
+  for (uint32_t c = a; c < e; c += 256) {
+    uint64_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t x = c + 64 * u + lane;
+      k[u] = x < e ? K[x] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t x = c + 64 * u + lane;
+      cl += __popcll(__ballot(x < e && x > f && !(k[u] < p)));
+      cr += __popcll(__ballot(x < e && !(p < k[u])));
+    }
+  }
+  if (lane == 0) s_w[wv] = cl, s_w[4 + wv] = cr;
+  __syncthreads();
+  uint32_t nL = 0, nR = 0, oL = 0, oR = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u) {
+    if (u < wv) oL += s_w[u], oR += s_w[4 + u];
+    nL += s_w[u], nR += s_w[4 + u];
+  }
+  // pass 2: ranked writes (PL ascending, PR ascending; PR is read from the right)
+  for (uint32_t c = a; c < e; c += 256) {
+    uint64_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t x = c + 64 * u + lane;
+      k[u] = x < e ? K[x] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t x = c + 64 * u + lane;
+      const bool lf = x < e && x > f && !(k[u] < p);
+      const bool rf = x < e && !(p < k[u]);
+      const uint64_t bl = __ballot(lf), br = __ballot(rf);
+      if (lf) PL[f + oL + __popcll(bl & lt)] = x;
+      if (rf) PR[f + oR + __popcll(br & lt)] = x;
+      oL += __popcll(bl);
+      oR += __popcll(br);
+    }
+  }
+  __syncthreads();
+  // K = first k < lim with PL[k] >= PR[nR-1-k] (lim if none), 256 probes a round
+  const uint32_t lim = nL < nR ? nL : nR;
+  uint32_t lo = 0, hi = lim;  // K in [lo, hi]
+  while (lo < hi) {
+    const uint32_t span = hi - lo;
+    const uint32_t k = lo + (uint32_t)(((uint64_t)span * tid) / 256);
+    const bool probe = tid == 0 || k != lo + (uint32_t)(((uint64_t)span * (tid - 1)) / 256);
+    const bool stop = probe && PL[f + k] >= PR[f + nR - 1 - k];
+    if (tid == 0) s_w[8] = 0xFFFFFFFFu;
+    __syncthreads();
+    if (stop) atomicMin(&s_w[8], k);
+    __syncthreads();
+    const uint32_t first = s_w[8];
+    // the largest probed k below `first` (or below hi) is known false
+    uint32_t nlo = lo;
+    {
+      const uint32_t bound = first == 0xFFFFFFFFu ? hi : first;
+      // probes are increasing in tid: the false ones below bound
+      const bool f_ok = probe && !stop && k < bound;
+      if (tid == 0) s_w[9] = 0;
+      __syncthreads();
+      if (f_ok) atomicMax(&s_w[9], k + 1);
+      __syncthreads();
+      nlo = s_w[9] > lo ? s_w[9] : lo;
+      hi = bound;
+    }
+    lo = nlo;
+    __syncthreads();
+  }
+  const uint32_t Kc = lo;
+  for (uint32_t k = tid; k < Kc; k += 256) {
+    const uint32_t xa = PL[f + k], xb = PR[f + nR - 1 - k];
+    const uint64_t ka = K[xa];
+    K[xa] = K[xb];
+    K[xb] = ka;
+    const uint32_t ta = T[xa];
+    T[xa] = T[xb];
+    T[xb] = ta;
+  }
+  uint32_t cut;
+  if (Kc == 0) {
+    cut = PL[f];
+  } else {
+    cut = PR[f + nR - Kc];
+    if (Kc < nL && PL[f + Kc] < cut) cut = PL[f + Kc];
+  }
+  __syncthreads();
+  return cut;
+}
+
+__global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tier,
                                                            const uint32_t *goff, uint64_t *key,
                                                            uint32_t *tag, uint32_t *otag,
                                                            uint32_t *pl, uint32_t *pr,
-                                                           uint8_t *bnd, Frame *frames) {
-  const uint32_t lane = threadIdx.x;
+                                                           uint8_t *bnd) {
+  __shared__ Frame stack[SPLIT_STACK];
+  __shared__ uint32_t s_w[16];
+  const uint32_t tid = threadIdx.x;
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
   for (uint32_t w = lo + blockIdx.x; w < hi; w += gridDim.x) {
     const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
-    Frame *fr = frames + (b >> 3) + (size_t)80 * (w - lo);
-    const uint32_t nfr = n / (THRESH + 1) + 2;
-    const GView v{key + b, tag + b, pl + b, pr + b, bnd + b};
-    wave_std_sort<true>(v, n, otag + b, fr, fr + 72, fr + 72 + nfr, lane);
-    wave_sync_global();
+    uint64_t *K = key + b;
+    uint32_t *T = tag + b;
+    int sp = 1;
+    if (tid == 0) stack[0] = {0u, n, 2 * (31 - __clz((int)n))};
+    __syncthreads();
+    while (sp) {
+      const Frame fr = stack[--sp];
+      __syncthreads();  // every thread has read the frame before it is reused
+      uint32_t f = fr.f, l = fr.l;
+      int d = fr.d;
+      for (;;) {
+        if (l - f <= SPLIT_T) {
+          if (tid == 0) {
+            bnd[b + f] = 1;
+            pl[b + f] = (l - f) | (uint32_t)d << 16;
+          }
+          break;
+        }
+        if (d == 0) {  // __partial_sort fallback on a large segment
+          if (tid == 0) heap_sort_segment(GView{K, T, nullptr, nullptr, nullptr}, f, l);
+          __syncthreads();
+          for (uint32_t x = f + tid; x < l; x += 256) otag[b + x] = T[x];
+          break;
+        }
+        --d;
+        const uint32_t cut = block_partition(K, T, pl + b, pr + b, f, l, s_w);
+        if (tid == 0) stack[sp] = {cut, l, d};
+        ++sp;
+        l = cut;
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// phase B: LDS layout of k_sort_groups_lds with a stack for any depth budget
+__host__ __device__ constexpr size_t seg_lds_bytes(uint32_t cap, size_t key_bytes) {
+  return (size_t)cap * (key_bytes + 4 + 2 + 2 + 1) +
+         (SPLIT_STACK + 2 * (cap / (THRESH + 1) + 2)) * sizeof(Frame) + 16;
+}
+template <class KT>
+__global__ void __launch_bounds__(64) k_sort_segments(uint32_t m, const uint8_t *bnd,
+                                                      const uint32_t *head, const uint64_t *key,
+                                                      const uint32_t *tag, uint32_t *otag) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  constexpr uint32_t cap = SPLIT_T;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nfr = cap / (THRESH + 1) + 2;
+  KT *K = reinterpret_cast<KT *>(smem);
+  uint32_t *T = reinterpret_cast<uint32_t *>(K + cap);
+  Frame *stack = reinterpret_cast<Frame *>(T + cap);
+  Frame *smallq = stack + SPLIT_STACK;
+  Frame *heapq = smallq + nfr;
+  uint16_t *PL = reinterpret_cast<uint16_t *>(heapq + nfr);
+  uint16_t *PR = PL + cap;
+  uint8_t *B = reinterpret_cast<uint8_t *>(PR + cap);
+  const ViewT<KT, uint16_t> v{K, T, PL, PR, B};
+  for (uint32_t w0 = blockIdx.x * 64; w0 < m; w0 += gridDim.x * 64) {
+    uint64_t hb = __ballot(w0 + lane < m && bnd[w0 + lane] == 1);
+    while (hb) {
+      const uint32_t x = w0 + (uint32_t)__builtin_ctzll(hb);
+      hb &= hb - 1;
+      const uint32_t h = head[x], n = h & 0xFFFFu;
+      for (uint32_t y = lane; y < n; y += 64) {
+        K[y] = (KT)key[x + y];
+        T[y] = tag[x + y];
+      }
+      wave_sync();
+      wave_std_sort<false>(v, n, otag + x, stack, smallq, heapq, lane, (int)(h >> 16));
+      wave_sync();
+    }
   }
 }
 
@@ -619,12 +813,11 @@ size_t lds_bytes(uint32_t cap, size_t key_bytes) {
 }  // namespace
 
 size_t groupsort_scratch_bytes(uint32_t n) {
-  constexpr uint32_t cap = lds_caps().c[NLDS - 1];
   const size_t nblk = (size_t)n / TCH + 1;
-  const size_t frames = (size_t)n / 8 + 80 * ((size_t)n / (cap + 1) + 1) + 80;
-  // pl, pr; tier lists; bounds; block counts (+ scan), block members; frames
+  // pl, pr (stopper lists; segment heads); tier lists; bounds; block counts
+  // (+ scan), block members
   return (size_t)n * 4 * 2 + ((size_t)n + 1) * 4 + (size_t)n + 64 +
-         (nblk * (NTIER - 1) + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + frames * sizeof(Frame) + 256;
+         (nblk * (NTIER - 1) + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + 256;
 }
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
@@ -646,8 +839,6 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
       (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
   uint32_t *boff = bc + (size_t)NL * nblk + 1;
   uint32_t *bm = boff + (size_t)NL * nblk + 1;
-  Frame *frames = reinterpret_cast<Frame *>(
-      (reinterpret_cast<uintptr_t>(bm + (size_t)NTIER * nblk) + 63) & ~(uintptr_t)63);
   const bool timing = g_ktimer != nullptr;
   if (side) {
     (void)hipEventRecord(ev_fork, st);
@@ -697,11 +888,20 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     kt_end(st, KID_SORT_LDS, 0.0);
     tier_slot(2 + j);
   }
+  (void)hipMemsetAsync(bnd, 0, m, st);  // phase A marks the final segments' starts
   kt_begin(st);
-  k_sort_groups_global<<<1024, 64, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
-                                            frames);
+  k_sort_groups_split<<<2048, 256, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd);
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
+  kt_begin(st);
+  if (narrow_keys)
+    k_sort_segments<uint32_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 4), st>>>(m, bnd, pl, key, tag,
+                                                                          otag);
+  else
+    k_sort_segments<uint64_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 8), st>>>(m, bnd, pl, key, tag,
+                                                                          otag);
+  kt_end(st, KID_SORT_SEGS, 0.0);
+  tier_slot(NTIER);
   if (side) (void)hipStreamWaitEvent(st, ev_join, 0);
 }
 

@@ -302,6 +302,30 @@ def test_std_sort_segments_vs_restatement(gpu_ctx):
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
 
 
+def test_std_sort_large_segments_vs_restatement(gpu_ctx):
+    """Segments far above the LDS cap (block-partitioned top levels, then one
+    wavefront per final segment): ties, sorted, reversed, organ pipe, all
+    equal, wide random keys, and a median-of-3 killer whose depth-limit
+    heapsort falls on a segment above the split size."""
+    from sort_cases import heap_fallbacks, mcilroy_killer
+    rng = np.random.default_rng(12)
+    killer = mcilroy_killer(20000)
+    assert heap_fallbacks(killer) > 0
+    pipe = np.r_[np.arange(25000), np.arange(25000)[::-1]].astype(np.uint64)
+    segs = [rng.integers(0, 4, 300_000).astype(np.uint64),
+            np.arange(100_000, dtype=np.uint64), np.arange(100_000, dtype=np.uint64)[::-1].copy(),
+            pipe, np.full(70_000, 7, np.uint64), killer,
+            rng.integers(0, 1 << 40, 500_000).astype(np.uint64),
+            rng.integers(0, 300, 2049).astype(np.uint64),  # just past the split size
+            rng.integers(0, 1 << 20, 4097).astype(np.uint64)]
+    keys = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
+    perm = gpu_ctx.std_sort_segments(keys, off)
+    for a, b, s in zip(off[:-1], off[1:], segs):
+        want = ro.std_sort(s) + a
+        assert np.array_equal(perm[a:b], want), (int(a), s.size)
+
+
 def full_size_properties(gpu_ctx, f, L):
     """Size-independent properties of the reference's output on a set too
     large for the oracle -- determinism, output order a permutation of the
