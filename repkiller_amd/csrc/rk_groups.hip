@@ -95,7 +95,8 @@ __global__ void k_gather_proc(Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
 // In-group sort key |yStart - diag_func[xStart/10]|: diag_func[b] is the yStart
 // of the LAST fragment of processing bucket b, i.e. of the end of k's run of
 // equal processing keys.  Run ends inside the wavefront come from a ballot and
-// a shuffle; only runs that cross the wave's end read further.
+// a shuffle; the run that crosses the wave's end (always the one holding lane
+// 63) is followed by the whole wave, 64 keys per step.
 __global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m, uint32_t *wide) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; base < m;
@@ -108,10 +109,18 @@ __global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m, uint32_t 
     const uint64_t ends = __ballot(end) & ~((1ull << lane) - 1ull);
     const int src = ends ? __ffsll((unsigned long long)ends) - 1 : 63;
     uint64_t d = __shfl(y, src);
-    if (in && !ends) {  // the run continues past this wave
-      uint32_t e = base + 63;
-      while (e + 1 < m && p.pkey[e + 1] == key) ++e;
-      d = p.ys[e];
+    if (__ballot(in && !ends)) {  // the last run continues past this wave
+      const uint32_t klast = __shfl(key, 63);
+      uint32_t e = 0;
+      for (uint32_t b = base + 64;; b += 64) {
+        const uint32_t q = b + lane;
+        const uint64_t stop = __ballot(q >= m || p.pkey[q] != klast);
+        if (stop) {
+          e = b + __builtin_ctzll(stop) - 1;  // the run's last entry
+          break;
+        }
+      }
+      if (in && !ends) d = p.ys[e];
     }
     const uint64_t h = y > d ? y - d : d - y;
     if (in) p.hrec[k] = make_ulonglong2(h, p.row[k]);
