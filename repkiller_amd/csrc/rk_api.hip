@@ -479,9 +479,14 @@ extern "C" int rk_create(rk_ctx **out, int device) {
   auto ctx = new (std::nothrow) rk_ctx;
   if (!ctx) return RK_E_NOMEM;
   ctx->device = device;
+  // RK_ONE_STREAM=1 (profiling only): the overlapped work runs on the main
+  // stream too, so per-kernel times are not shared with a concurrent kernel
+  const char *one = std::getenv("RK_ONE_STREAM");
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+      (one && one[0] == '1' ? (ctx->stream2 = ctx->stream, hipSuccess)
+                            : hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking)) !=
+          hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming) != hipSuccess ||
@@ -527,7 +532,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->fork) (void)hipEventDestroy(ctx->fork);
   if (ctx->join) (void)hipEventDestroy(ctx->join);
   if (ctx->aux) (void)hipEventDestroy(ctx->aux);
-  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->stream2 && ctx->stream2 != ctx->stream) (void)hipStreamDestroy(ctx->stream2);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

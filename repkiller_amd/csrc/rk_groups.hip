@@ -99,6 +99,7 @@ __global__ void k_gather_proc(Proc p, uint32_t m, uint32_t nbx, uint32_t nby) {
 // 63) is followed by the whole wave, 64 keys per step.
 __global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m, uint32_t *wide) {
   const uint32_t lane = threadIdx.x & 63;
+  bool wd = false;
   for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; base < m;
        base += gridDim.x * blockDim.x) {
     const uint32_t k = base + lane;
@@ -124,8 +125,11 @@ __global__ void __launch_bounds__(256) k_sort_keys(Proc p, uint32_t m, uint32_t 
     }
     const uint64_t h = y > d ? y - d : d - y;
     if (in) p.hrec[k] = make_ulonglong2(h, p.row[k]);
-    if (__ballot(in && (h >> 32) != 0) && lane == 0) atomicOr(wide, 1u);
+    wd |= in && (h >> 32) != 0;
   }
+  // one flag per wave, and only while unset: a 15-Gbp set has wide keys in
+  // every wave, and one hot atomic address serialises (~90 per us)
+  if (__ballot(wd) && lane == 0 && *(volatile uint32_t *)wide == 0) atomicOr(wide, 1u);
 }
 
 __device__ __forceinline__ uint8_t nbd_code(uint64_t c, uint64_t max_index) {

@@ -468,8 +468,11 @@ __device__ __forceinline__ void foreign_scan32(const Axis &ax, uint32_t g0, int 
     if (kg != want) return;
     if (eg >= i || sg >= ST_HIT_PENDING || !m32(q, o)) continue;
     if (sg != ST_ACTIVE) {
+      // an undecided candidate: this query cannot be final in this sweep, and
+      // HIT_PENDING needs only one ACTIVE candidate, so the rest of the run
+      // (a long run of hundreds in the first sweep) need not be read now
       fs.any_unknown = true;
-      continue;
+      return;
     }
     const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
     if (!fs.any_active || d > fs.best || (d == fs.best && g > bestpos))
@@ -486,7 +489,7 @@ constexpr int OWN_U = RK_OWN_U;
 // wavefront in pk / ent / key.  Returns (wave-uniformly) whether the window
 // still owns undecided entries, and records that in wpend[w].
 __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8_t *wpend,
-                                               uint32_t *big, uint32_t *nbig, uint2 *pk,
+                                               uint8_t *lflag, uint2 *pk,
                                                uint32_t *ent, uint32_t *key, int lane) {
   bool pending = false;
   {
@@ -518,13 +521,10 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
       rs[s] = hs_le(S0, S1, P);
       const int re = ls_gt(S0, S1, P);
       own[s] = base + P < m && rs[s] >= 0 && rs[s] < 64 && re - rs[s] <= (int)LONG_RUN;
-      if (s == 0 && big) {  // first sweep: list the long runs that start here
+      if (s == 0 && lflag) {  // first sweep: flag a long run that starts here
         const bool lng = base + P < m && rs[0] == P && re - P > (int)LONG_RUN;
         const uint64_t bb = __ballot(lng);
-        uint32_t at = 0;
-        if (lane == 0 && bb) at = atomicAdd(nbig, (uint32_t)__popcll(bb));
-        at = __shfl(at, 0);
-        if (lng) big[at + __popcll(bb & ((1ull << lane) - 1ull))] = base + P;
+        if (lane == 0) lflag[w] = bb != 0;
       }
       st[s] = ST_HIT;
       nd[s] = 0;
@@ -706,15 +706,14 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
 
 // first sweep: one wavefront per window
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint32_t *big,
-             uint32_t *nbig) {
+k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint8_t *lflag) {
   __shared__ uint2 s_pk[4][128 + OWN_U];  // {centre low 32 bits, length}; read padding
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t w = blockIdx.x * 4 + wv;
   bool pending = false;
   if (w < nwin && wpend[w])
-    pending = sweep_window32(ax, w, wpend, big, nbig, s_pk[wv], s_ent[wv], s_key[wv], lane);
+    pending = sweep_window32(ax, w, wpend, lflag, s_pk[wv], s_ent[wv], s_key[wv], lane);
   count_pending(counters, pending && lane == 0);
 }
 
@@ -732,7 +731,7 @@ __global__ void __launch_bounds__(256) k_sweep_fast_more(Axis ax, uint8_t *wpend
       const int b = __builtin_ctzll(todo);
       todo &= todo - 1;
       wave_sync_lds();  // the previous window's LDS reads are done
-      pending |= sweep_window32(ax, w0 + b, wpend, nullptr, nullptr, s_pk[wv], s_ent[wv],
+      pending |= sweep_window32(ax, w0 + b, wpend, nullptr, s_pk[wv], s_ent[wv],
                                 s_key[wv], lane);
     }
   }
@@ -998,154 +997,168 @@ __device__ int neighbour_list(const Axis &ax, uint32_t nb, uint32_t ne, LongLds 
   return n;
 }
 
-__global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint32_t *big,
-                                                      const uint32_t *nbig_dev, uint8_t *rpend,
+// lflag[w] = 1: a run of more than LONG_RUN entries starts in window w (at
+// most one can); the first sweep's window kernel sets the flags, so no
+// shared list (and no hot atomic counter) is needed.  One wavefront takes 64
+// windows and walks their long runs in turn.
+__global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lflag,
+                                                      uint32_t nwin, uint8_t *rpend,
                                                       uint32_t *counters) {
   __shared__ LongLds s_l[4];
   const uint32_t lane = threadIdx.x & 63;
   LongLds &L = s_l[threadIdx.x >> 6];
-  const uint32_t count = *nbig_dev;
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < count;
-       w += (gridDim.x * blockDim.x) >> 6) {
-    const uint32_t beg = big[w];
-    if (!rpend[beg]) continue;
-    const uint32_t key = ax.key[beg];
-    const uint32_t end = wave_scan_end(ax, beg + LONG_RUN, key, lane);
-    uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
-    const bool has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
-    if (has_lo) lo_e = beg, lo_b = wave_scan_begin(ax, beg, key - 1, lane);
-    const bool has_hi = end < ax.m && ax.key[end] == key + 1;
-    if (has_hi) hi_b = end, hi_e = wave_scan_end(ax, end + 1, key + 1, lane);
-    wave_sync_lds();  // the previous run's LDS reads are done
-    const int nn0 = has_lo ? neighbour_list(ax, lo_b, lo_e, L, 0, lane) : 0;
-    const int nn1 = has_hi ? neighbour_list(ax, hi_b, hi_e, L, 1, lane) : 0;
-    int nl = 0;
-    bool pending = false;
-    uint32_t cb = beg;
-    for (; cb < end; cb += 64) {
-      const uint32_t t = cb + lane;
-      const bool in = t < end;
-      uint2 me = make_uint2(0, 0);
-      uint32_t i = 0;
-      uint8_t st = ST_HIT, nd = 0;
-      if (in) me = ax.pk[t], i = ax.ent[t], st = load_state(&ax.state[t]), nd = ax.nbd[t];
-      wave_sync_lds();  // the previous chunk's LDS reads are done
-      L.cpk[lane] = me;
-      L.cent[lane] = i;
-      if ((int)lane < nn0) L.nst[0][lane] = load_state(&ax.state[L.npos[0][lane]]);
-      if ((int)lane < nn1) L.nst[1][lane] = load_state(&ax.state[L.npos[1][lane]]);
-      wave_sync_lds();
-      const uint8_t st0 = st;
-      const bool open = in && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
-      uint64_t rown = 0;
-      Scan fl{0.0, NONE, 0, false, false}, fn{0.0, NONE, 0, false, false};
-      Q32 q{};
-      if (open) {
-        q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
-        for (int j = 0; j < (int)lane; j += OWN_U) {
-          uint64_t b4 = 0;
-#pragma unroll
-          for (int u = 0; u < OWN_U; ++u) b4 |= (uint64_t)m32(q, L.cpk[j + u]) << u;
-          if ((int)lane - j < OWN_U) b4 &= (1ull << ((int)lane - j)) - 1ull;
-          rown |= b4 << j;
-        }
-        for (int k = nl - 1; k >= 0; --k) {  // earlier chunks, newest first
-          const uint8_t sk = L.lst[k];
-          const uint2 o = L.lpk[k];
-          if (!m32(q, o)) continue;
-          if (sk != ST_ACTIVE) {
-            fl.any_unknown = true;
-            continue;
+  const uint32_t ngrp = (nwin + 63) / 64;
+  for (uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; gi < ngrp;
+       gi += (gridDim.x * blockDim.x) >> 6) {
+    uint64_t todo = __ballot(gi * 64 + lane < nwin && lflag[gi * 64 + lane]);
+    while (todo) {
+      const uint32_t w = gi * 64 + (uint32_t)__builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t pw = w * 64 + lane;
+      const uint32_t kp = pw < ax.m ? ax.key[pw] : NONE;
+      const uint64_t sb = __ballot(pw < ax.m && (pw == 0 || ax.key[pw - 1] != kp) &&
+                                   pw + LONG_RUN < ax.m && ax.key[pw + LONG_RUN] == kp);
+      if (!sb) continue;
+      const uint32_t beg = w * 64 + (uint32_t)__builtin_ctzll(sb);
+      if (!rpend[beg]) continue;
+      const uint32_t key = ax.key[beg];
+      const uint32_t end = wave_scan_end(ax, beg + LONG_RUN, key, lane);
+      uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
+      const bool has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
+      if (has_lo) lo_e = beg, lo_b = wave_scan_begin(ax, beg, key - 1, lane);
+      const bool has_hi = end < ax.m && ax.key[end] == key + 1;
+      if (has_hi) hi_b = end, hi_e = wave_scan_end(ax, end + 1, key + 1, lane);
+      wave_sync_lds();  // the previous run's LDS reads are done
+      const int nn0 = has_lo ? neighbour_list(ax, lo_b, lo_e, L, 0, lane) : 0;
+      const int nn1 = has_hi ? neighbour_list(ax, hi_b, hi_e, L, 1, lane) : 0;
+      int nl = 0;
+      bool pending = false;
+      uint32_t cb = beg;
+      for (; cb < end; cb += 64) {
+        const uint32_t t = cb + lane;
+        const bool in = t < end;
+        uint2 me = make_uint2(0, 0);
+        uint32_t i = 0;
+        uint8_t st = ST_HIT, nd = 0;
+        if (in) me = ax.pk[t], i = ax.ent[t], st = load_state(&ax.state[t]), nd = ax.nbd[t];
+        wave_sync_lds();  // the previous chunk's LDS reads are done
+        L.cpk[lane] = me;
+        L.cent[lane] = i;
+        if ((int)lane < nn0) L.nst[0][lane] = load_state(&ax.state[L.npos[0][lane]]);
+        if ((int)lane < nn1) L.nst[1][lane] = load_state(&ax.state[L.npos[1][lane]]);
+        wave_sync_lds();
+        const uint8_t st0 = st;
+        const bool open = in && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
+        uint64_t rown = 0;
+        Scan fl{0.0, NONE, 0, false, false}, fn{0.0, NONE, 0, false, false};
+        Q32 q{};
+        if (open) {
+          q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
+          for (int j = 0; j < (int)lane; j += OWN_U) {
+            uint64_t b4 = 0;
+  #pragma unroll
+            for (int u = 0; u < OWN_U; ++u) b4 |= (uint64_t)m32(q, L.cpk[j + u]) << u;
+            if ((int)lane - j < OWN_U) b4 &= (1ull << ((int)lane - j)) - 1ull;
+            rown |= b4 << j;
           }
-          const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
-          if (d > fl.best) fl.best = d, fl.win = L.lent[k];
-          fl.any_active = true;
-        }
-        const int dir = nd == 1 ? -1 : nd == 2 ? 1 : 0;
-        const int sd = dir < 0 ? 0 : 1;
-        const int nn = dir < 0 ? nn0 : nn1;
-        if (dir != 0 && (dir < 0 ? has_lo : has_hi)) {
-          if (nn >= 0) {
-            for (int k = nn - 1; k >= 0; --k) {  // newest first
-              if (L.nent[sd][k] >= i) continue;
-              const uint8_t sk = L.nst[sd][k];
-              if (sk >= ST_HIT_PENDING) continue;
-              const uint2 o = L.npk[sd][k];
-              if (!m32(q, o)) continue;
-              if (sk != ST_ACTIVE) {
-                fn.any_unknown = true;
-                continue;
-              }
-              const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
-              if (d > fn.best) fn.best = d, fn.win = L.nent[sd][k];
-              fn.any_active = true;
+          for (int k = nl - 1; k >= 0; --k) {  // earlier chunks, newest first
+            const uint8_t sk = L.lst[k];
+            const uint2 o = L.lpk[k];
+            if (!m32(q, o)) continue;
+            if (sk != ST_ACTIVE) {
+              fl.any_unknown = true;
+              continue;
             }
-          } else {  // list overflow: the global scan of the short-run kernel
-            foreign_scan32(ax, dir < 0 ? beg - 1 : end, dir, key + dir, i, q, fn);
+            const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
+            if (d > fl.best) fl.best = d, fl.win = L.lent[k];
+            fl.any_active = true;
+          }
+          const int dir = nd == 1 ? -1 : nd == 2 ? 1 : 0;
+          const int sd = dir < 0 ? 0 : 1;
+          const int nn = dir < 0 ? nn0 : nn1;
+          if (dir != 0 && (dir < 0 ? has_lo : has_hi)) {
+            if (nn >= 0) {
+              for (int k = nn - 1; k >= 0; --k) {  // newest first
+                if (L.nent[sd][k] >= i) continue;
+                const uint8_t sk = L.nst[sd][k];
+                if (sk >= ST_HIT_PENDING) continue;
+                const uint2 o = L.npk[sd][k];
+                if (!m32(q, o)) continue;
+                if (sk != ST_ACTIVE) {
+                  fn.any_unknown = true;
+                  continue;
+                }
+                const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
+                if (d > fn.best) fn.best = d, fn.win = L.nent[sd][k];
+                fn.any_active = true;
+              }
+            } else {  // list overflow: the global scan of the short-run kernel
+              foreign_scan32(ax, dir < 0 ? beg - 1 : end, dir, key + dir, i, q, fn);
+            }
           }
         }
-      }
-      const bool out_act = fl.any_active || fn.any_active;
-      const bool out_unk = fl.any_unknown || fn.any_unknown;
-      for (;;) {
+        const bool out_act = fl.any_active || fn.any_active;
+        const bool out_unk = fl.any_unknown || fn.any_unknown;
+        for (;;) {
+          const uint64_t A = __ballot(in && st == ST_ACTIVE);
+          const uint64_t U = __ballot(in && st == ST_UNKNOWN);
+          bool changed = false;
+          if (open && st == ST_UNKNOWN) {
+            if ((A & rown) || out_act) st = ST_HIT_PENDING, changed = true;
+            else if (!(U & rown) && !out_unk) st = ST_ACTIVE, changed = true;
+          }
+          const uint64_t V = __ballot(in && st == ST_UNKNOWN);
+          if (open && st == ST_HIT_PENDING && !(V & rown) && !out_unk) st = ST_HIT, changed = true;
+          const bool left = open && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
+          if (!__ballot(changed) || !__ballot(left)) break;
+        }
         const uint64_t A = __ballot(in && st == ST_ACTIVE);
-        const uint64_t U = __ballot(in && st == ST_UNKNOWN);
-        bool changed = false;
-        if (open && st == ST_UNKNOWN) {
-          if ((A & rown) || out_act) st = ST_HIT_PENDING, changed = true;
-          else if (!(U & rown) && !out_unk) st = ST_ACTIVE, changed = true;
-        }
-        const uint64_t V = __ballot(in && st == ST_UNKNOWN);
-        if (open && st == ST_HIT_PENDING && !(V & rown) && !out_unk) st = ST_HIT, changed = true;
-        const bool left = open && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
-        if (!__ballot(changed) || !__ballot(left)) break;
-      }
-      const uint64_t A = __ballot(in && st == ST_ACTIVE);
-      pending |= open && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
-      if (open && st != st0) {
-        if (st == ST_HIT) {
-          double best = 0.0;
-          uint32_t win = NONE;
-          uint64_t b = A & rown;
-          while (b) {  // this chunk, newest first
-            const int v = 63 - __clzll(b);
-            b &= ~(1ull << v);
-            const double d = dev32(q, L.cpk[v], ax.len_ratio, ax.pos_ratio);
-            if (d > best) best = d, win = L.cent[v];
+        pending |= open && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
+        if (open && st != st0) {
+          if (st == ST_HIT) {
+            double best = 0.0;
+            uint32_t win = NONE;
+            uint64_t b = A & rown;
+            while (b) {  // this chunk, newest first
+              const int v = 63 - __clzll(b);
+              b &= ~(1ull << v);
+              const double d = dev32(q, L.cpk[v], ax.len_ratio, ax.pos_ratio);
+              if (d > best) best = d, win = L.cent[v];
+            }
+            if (fl.any_active && fl.best > best) best = fl.best, win = fl.win;
+            if (fn.any_active && fn.best > best) win = fn.win;
+            record_decision(ax, i, ST_HIT, win);
+          } else if (st == ST_ACTIVE) {
+            record_decision(ax, i, ST_ACTIVE, NONE);
           }
-          if (fl.any_active && fl.best > best) best = fl.best, win = fl.win;
-          if (fn.any_active && fn.best > best) win = fn.win;
-          record_decision(ax, i, ST_HIT, win);
-        } else if (st == ST_ACTIVE) {
-          record_decision(ax, i, ST_ACTIVE, NONE);
+          store_state(&ax.state[t], st);
         }
-        store_state(&ax.state[t], st);
+        // this chunk's ACTIVE / UNKNOWN entries join the list
+        const bool keep = in && (st == ST_ACTIVE || st == ST_UNKNOWN);
+        const uint64_t kb = __ballot(keep);
+        if (nl + __popcll(kb) > LCAP) {
+          cb += 64;
+          break;
+        }
+        wave_sync_lds();  // the list reads of this chunk are done
+        if (keep) {
+          const int at = nl + below_count(kb);
+          L.lpk[at] = me;
+          L.lpos[at] = t;
+          L.lent[at] = i;
+          L.lst[at] = st;
+        }
+        nl += __popcll(kb);
       }
-      // this chunk's ACTIVE / UNKNOWN entries join the list
-      const bool keep = in && (st == ST_ACTIVE || st == ST_UNKNOWN);
-      const uint64_t kb = __ballot(keep);
-      if (nl + __popcll(kb) > LCAP) {
-        cb += 64;
-        break;
+      if (cb < end) {  // own list overflow: the rest entry by entry
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        pending |= walk_entries32(ax, beg, cb, end, has_lo, lo_b, lo_e, has_hi, hi_b, hi_e, lane);
       }
-      wave_sync_lds();  // the list reads of this chunk are done
-      if (keep) {
-        const int at = nl + below_count(kb);
-        L.lpk[at] = me;
-        L.lpos[at] = t;
-        L.lent[at] = i;
-        L.lst[at] = st;
+      const bool pend = __ballot(pending) != 0;
+      if (lane == 0) {
+        rpend[beg] = pend;
+        if (pend) atomicAdd(&counters[w % PEND_SLOTS], 1u);
       }
-      nl += __popcll(kb);
-    }
-    if (cb < end) {  // own list overflow: the rest entry by entry
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      pending |= walk_entries32(ax, beg, cb, end, has_lo, lo_b, lo_e, has_hi, hi_b, hi_e, lane);
-    }
-    const bool pend = __ballot(pending) != 0;
-    if (lane == 0) {
-      rpend[beg] = pend;
-      if (pend) atomicAdd(&counters[w % PEND_SLOTS], 1u);
     }
   }
 }
@@ -1252,8 +1265,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   if (rl.nwin) {
     kt_begin(st);
     if (rl.fast32 && first)
-      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters, rl.big,
-                                                      rl.nbig_dev);
+      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters,
+                                                      reinterpret_cast<uint8_t *>(rl.big));
     else if (rl.fast32)
       k_sweep_fast_more<<<((rl.nwin + 63) / 64 + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin,
                                                                        counters);
@@ -1264,7 +1277,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   }
   if (rl.fast32) {  // the long-run count lives on the device: a fixed grid reads it
     kt_begin(st);
-    k_sweep_long32<<<2048, 256, 0, st>>>(ax, rl.big, rl.nbig_dev, rpend, counters);
+    k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<const uint8_t *>(rl.big), rl.nwin,
+                                         rpend, counters);
     kt_end(st, KID_SWEEP_WAVE, 0.0);
   } else if (rl.nbig) {
     kt_begin(st);
