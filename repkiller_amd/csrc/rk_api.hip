@@ -37,7 +37,7 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_sort_small",    "k_sort_groups_reg", "k_sort_groups_lds", "k_sort_groups_split",
     "k_emit",          "k_part (sharded)", "exchange (sharded)", "k_aux (sharded)",
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
-    "k_merge_yx (sharded)", "k_sort_segments",
+    "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32",
 };
 }  // namespace rk
 

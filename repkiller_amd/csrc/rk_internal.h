@@ -56,7 +56,7 @@ enum KernelId : int {
   KID_SWEEP_TILE, KID_SWEEP_FAST, KID_SWEEP_MORE, KID_SWEEP_WAVE, KID_CSR_FILL_Y, KID_JUMP,
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
-  KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_COUNT
+  KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 struct KernelTimer {

@@ -979,22 +979,59 @@ __device__ bool walk_entries32(const Axis &ax, uint32_t beg, uint32_t from, uint
 __device__ int neighbour_list(const Axis &ax, uint32_t nb, uint32_t ne, LongLds &L, int sd,
                               uint32_t lane) {
   int n = 0;
-  for (uint32_t q0 = nb; q0 < ne; q0 += 64) {
-    const uint32_t q = q0 + lane;
-    const uint8_t s = q < ne ? load_state(&ax.state[q]) : ST_HIT;
-    const bool keep = s < ST_HIT_PENDING;
-    const uint64_t b = __ballot(keep);
-    const int at = n + below_count(b);
-    if (n + __popcll(b) > NCAP) return -1;
-    if (keep) {
-      L.npk[sd][at] = ax.pk[q];
-      L.npos[sd][at] = q;
-      L.nent[sd][at] = ax.ent[q];
-      L.nst[sd][at] = s;
+  for (uint32_t q0 = nb; q0 < ne; q0 += 128) {  // two chunks' loads in flight
+    uint8_t s[2];
+    uint2 pk[2];
+    uint32_t en[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t q = q0 + 64 * u + lane;
+      s[u] = ST_HIT, pk[u] = make_uint2(0, 0), en[u] = 0;
+      if (q < ne) s[u] = load_state(&ax.state[q]), pk[u] = ax.pk[q], en[u] = ax.ent[q];
     }
-    n += __popcll(b);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool keep = s[u] < ST_HIT_PENDING;
+      const uint64_t b = __ballot(keep);
+      const int at = n + below_count(b);
+      if (n + __popcll(b) > NCAP) return -1;
+      if (keep) {
+        L.npk[sd][at] = pk[u];
+        L.npos[sd][at] = q0 + 64 * u + lane;
+        L.nent[sd][at] = en[u];
+        L.nst[sd][at] = s[u];
+      }
+      n += __popcll(b);
+    }
   }
   return n;
+}
+
+// run bounds for long runs: 64 probes 64 positions apart, then one window
+// (two memory round trips for a run of up to 4096 instead of one per 64)
+// first position >= from whose key is not `key` (or m)
+__device__ uint32_t wave_find_end(const Axis &ax, uint32_t from, uint32_t key, uint32_t lane) {
+  for (uint64_t b = from;; b += 64 * 64) {
+    const uint64_t q = b + 64 * lane;
+    const uint64_t e = __ballot(q >= ax.m || ax.key[q] != key);
+    if (e) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(e);
+      return j == 0 ? (uint32_t)b : wave_scan_end(ax, (uint32_t)b + 64 * (j - 1) + 1, key, lane);
+    }
+  }
+}
+// smallest p with key `key` on all of [p, before), key[before - 1] == key
+__device__ uint32_t wave_find_begin(const Axis &ax, uint32_t before, uint32_t key,
+                                    uint32_t lane) {
+  for (int64_t b = (int64_t)before - 1;; b -= 64 * 64) {
+    const int64_t q = b - 64 * (int64_t)lane;
+    const uint64_t e = __ballot(q < 0 || ax.key[q] != key);
+    if (e) {  // lane j's probe is the first miss; lane j-1's position is in the run
+      const uint32_t j = (uint32_t)__builtin_ctzll(e);
+      return j == 0 ? (uint32_t)(b + 1)
+                    : wave_scan_begin(ax, (uint32_t)(b - 64 * (int64_t)(j - 1)) + 1, key, lane);
+    }
+  }
 }
 
 // lflag[w] = 1: a run of more than LONG_RUN entries starts in window w (at
@@ -1022,30 +1059,44 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
       const uint32_t beg = w * 64 + (uint32_t)__builtin_ctzll(sb);
       if (!rpend[beg]) continue;
       const uint32_t key = ax.key[beg];
-      const uint32_t end = wave_scan_end(ax, beg + LONG_RUN, key, lane);
+      const uint32_t end = wave_find_end(ax, beg + LONG_RUN, key, lane);
       uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
       const bool has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
-      if (has_lo) lo_e = beg, lo_b = wave_scan_begin(ax, beg, key - 1, lane);
+      if (has_lo) lo_e = beg, lo_b = wave_find_begin(ax, beg, key - 1, lane);
       const bool has_hi = end < ax.m && ax.key[end] == key + 1;
-      if (has_hi) hi_b = end, hi_e = wave_scan_end(ax, end + 1, key + 1, lane);
+      if (has_hi) hi_b = end, hi_e = wave_find_end(ax, end + 1, key + 1, lane);
       wave_sync_lds();  // the previous run's LDS reads are done
       const int nn0 = has_lo ? neighbour_list(ax, lo_b, lo_e, L, 0, lane) : 0;
       const int nn1 = has_hi ? neighbour_list(ax, hi_b, hi_e, L, 1, lane) : 0;
       int nl = 0;
       bool pending = false;
       uint32_t cb = beg;
+      // a chunk's entries (and the neighbour states) are loaded one chunk
+      // ahead: only this walk changes them
+      uint2 nme;
+      uint32_t ni;
+      uint8_t nst, nnd, ns0 = ST_HIT, ns1 = ST_HIT;
+      auto fetch = [&](uint32_t c) {
+        const uint32_t t = c + lane;
+        nme = make_uint2(0, 0), ni = 0, nst = ST_HIT, nnd = 0;
+        if (t < end) nme = ax.pk[t], ni = ax.ent[t], nst = load_state(&ax.state[t]), nnd = ax.nbd[t];
+        if ((int)lane < nn0) ns0 = load_state(&ax.state[L.npos[0][lane]]);
+        if ((int)lane < nn1) ns1 = load_state(&ax.state[L.npos[1][lane]]);
+      };
+      fetch(beg);
       for (; cb < end; cb += 64) {
         const uint32_t t = cb + lane;
         const bool in = t < end;
-        uint2 me = make_uint2(0, 0);
-        uint32_t i = 0;
-        uint8_t st = ST_HIT, nd = 0;
-        if (in) me = ax.pk[t], i = ax.ent[t], st = load_state(&ax.state[t]), nd = ax.nbd[t];
+        const uint2 me = nme;
+        const uint32_t i = ni;
+        uint8_t st = nst;
+        const uint8_t nd = nnd, s0 = ns0, s1 = ns1;
+        if (cb + 64 < end) fetch(cb + 64);
         wave_sync_lds();  // the previous chunk's LDS reads are done
         L.cpk[lane] = me;
         L.cent[lane] = i;
-        if ((int)lane < nn0) L.nst[0][lane] = load_state(&ax.state[L.npos[0][lane]]);
-        if ((int)lane < nn1) L.nst[1][lane] = load_state(&ax.state[L.npos[1][lane]]);
+        if ((int)lane < nn0) L.nst[0][lane] = s0;
+        if ((int)lane < nn1) L.nst[1][lane] = s1;
         wave_sync_lds();
         const uint8_t st0 = st;
         const bool open = in && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
@@ -1279,7 +1330,7 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     kt_begin(st);
     k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<const uint8_t *>(rl.big), rl.nwin,
                                          rpend, counters);
-    kt_end(st, KID_SWEEP_WAVE, 0.0);
+    kt_end(st, KID_SWEEP_LONG, 0.0);
   } else if (rl.nbig) {
     kt_begin(st);
     k_sweep_wave<false><<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, nullptr,
