@@ -669,10 +669,31 @@ __host__ __device__ constexpr size_t seg_lds_bytes(uint32_t cap, size_t key_byte
   return (size_t)cap * (key_bytes + 4 + 2 + 2 + 1) +
          (SPLIT_STACK + 2 * (cap / (THRESH + 1) + 2)) * sizeof(Frame) + 16;
 }
+__global__ void __launch_bounds__(256) k_clear_if_tier(TierLists tl, int tier, uint8_t *b,
+                                                       uint32_t m) {
+  uint32_t lo, hi;
+  tl.range(tier, lo, hi);
+  if (lo == hi) return;
+  for (uint32_t x = (blockIdx.x * blockDim.x + threadIdx.x) * 16; x < m;
+       x += gridDim.x * blockDim.x * 16) {
+    if (x + 16 <= m) {
+      *reinterpret_cast<uint4 *>(b + x) = make_uint4(0, 0, 0, 0);
+    } else {
+      for (uint32_t y = x; y < m; ++y) b[y] = 0;
+    }
+  }
+}
+
 template <class KT>
-__global__ void __launch_bounds__(64) k_sort_segments(uint32_t m, const uint8_t *bnd,
-                                                      const uint32_t *head, const uint64_t *key,
-                                                      const uint32_t *tag, uint32_t *otag) {
+__global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, uint32_t m,
+                                                      const uint8_t *bnd, const uint32_t *head,
+                                                      const uint64_t *key, const uint32_t *tag,
+                                                      uint32_t *otag) {
+  {
+    uint32_t lo, hi;
+    tl.range(tier, lo, hi);
+    if (lo == hi) return;
+  }
   extern __shared__ __align__(16) uint8_t smem[];
   constexpr uint32_t cap = SPLIT_T;
   const uint32_t lane = threadIdx.x;
@@ -816,7 +837,7 @@ size_t groupsort_scratch_bytes(uint32_t n) {
   const size_t nblk = (size_t)n / TCH + 1;
   // pl, pr (stopper lists; segment heads); tier lists; bounds; block counts
   // (+ scan), block members
-  return (size_t)n * 4 * 2 + ((size_t)n + 1) * 4 + (size_t)n + 64 +
+  return (size_t)n * 4 * 2 + ((size_t)n + 1) * 4 + (size_t)n + 128 +
          (nblk * (NTIER - 1) + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + 256;
 }
 
@@ -834,7 +855,8 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   uint32_t *pl = reinterpret_cast<uint32_t *>(scratch);
   uint32_t *pr = pl + m;
   uint32_t *list = pr + m;
-  uint8_t *bnd = reinterpret_cast<uint8_t *>(list + ngroups + 1);
+  uint8_t *bnd = reinterpret_cast<uint8_t *>(
+      (reinterpret_cast<uintptr_t>(list + ngroups + 1) + 15) & ~(uintptr_t)15);
   uint32_t *bc = reinterpret_cast<uint32_t *>(
       (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
   uint32_t *boff = bc + (size_t)NL * nblk + 1;
@@ -888,18 +910,20 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     kt_end(st, KID_SORT_LDS, 0.0);
     tier_slot(2 + j);
   }
-  (void)hipMemsetAsync(bnd, 0, m, st);  // phase A marks the final segments' starts
+  // phase A marks the final segments' starts in bnd (cleared first); both
+  // kernels return at once when no group is that large
+  k_clear_if_tier<<<1024, 256, 0, st>>>(tl, NTIER - 1, bnd, m);
   kt_begin(st);
   k_sort_groups_split<<<2048, 256, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd);
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
   kt_begin(st);
   if (narrow_keys)
-    k_sort_segments<uint32_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 4), st>>>(m, bnd, pl, key, tag,
-                                                                          otag);
+    k_sort_segments<uint32_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 4), st>>>(
+        tl, NTIER - 1, m, bnd, pl, key, tag, otag);
   else
-    k_sort_segments<uint64_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 8), st>>>(m, bnd, pl, key, tag,
-                                                                          otag);
+    k_sort_segments<uint64_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 8), st>>>(
+        tl, NTIER - 1, m, bnd, pl, key, tag, otag);
   kt_end(st, KID_SORT_SEGS, 0.0);
   tier_slot(NTIER);
   if (side) (void)hipStreamWaitEvent(st, ev_join, 0);
