@@ -20,6 +20,9 @@ def load_case(case):
         import numpy as np
         e = np.empty(0, np.uint64)
         return rk.Frags(e, e.copy(), e.copy(), np.empty(0, np.uint8)), case["L"], case["L"]
+    if case["kind"] == "long_runs":
+        from long_runs import long_run_set
+        return long_run_set(case["runs_len"], case["seed"]), case["L"], case["L"]
     if case["kind"] == "synth":
         f = rk.synth(case["n"], case["L"], seed=case["seed"], family_frac=case.get("ff", 0.8),
                      copies=tuple(case.get("copies", (2, 30))))
