@@ -103,7 +103,7 @@ int err_status(rk_ctx *ctx, uint32_t bits) {
 int resolve_axis(rk_ctx *ctx, const Axis &ax, SweepScratch sc, bool fast32, uint32_t *sweeps) {
   uint32_t *counters = sc.counters;
   uint8_t *rpend = sc.rpend;
-  RunList rl{sc.runs, sc.wpend, 0, 0, fast32, nullptr};
+  RunList rl{sc.runs, sc.wpend, 0, 0, fast32};
   build_runs(ax, rl, sc.dev_count, ctx->host + 128, ctx->stream);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));

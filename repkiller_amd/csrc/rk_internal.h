@@ -116,14 +116,15 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   double len_ratio, pos_ratio;
 };
 // The axis' bucket runs: the 64-position windows (wpend[w] = window w still
-// owns undecided entries) and the runs longer than 64 entries (big, nbig),
-// which take a wavefront each.  build_runs also fills Axis::rlen_at/rbeg_at.
+// owns undecided entries) and the runs longer than 64 entries, which take a
+// wavefront each.  32-bit path: `big` holds one byte per window, set by the
+// first sweep when a long run starts there.  64-bit path: `big` lists the
+// long runs' starts (nbig of them) and build_runs fills Axis::rlen_at/rbeg_at.
 struct RunList {
   uint32_t *big;
   uint8_t *wpend;
   uint32_t nbig, nwin;
   bool fast32;          // every length < 2^31: the 32-bit window kernel applies
-  uint32_t *nbig_dev;   // fast32: the long-run count, found by the first sweep
 };
 size_t runs_scratch_words(uint32_t m);
 void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host_words,

@@ -820,66 +820,41 @@ __device__ __forceinline__ uint32_t wave_scan_begin(const Axis &ax, uint32_t bef
   }
 }
 
-template <bool FAST>
+// 64-bit lengths (k_sweep_tile's long runs): one wavefront per listed run,
+// entries decided one after another; big = the starts of the runs of more
+// than LONG_RUN entries (k_run_bounds), run and neighbour bounds from the run
+// tables
 __global__ void __launch_bounds__(256) k_sweep_wave(Axis ax, const uint32_t *big, uint32_t nbig,
-                                                    const uint32_t *nbig_dev, uint8_t *rpend,
-                                                    uint32_t *counters) {
-  // big = starts of the runs of more than LONG_RUN entries; FAST: the run
-  // table is not built, runs and their neighbours are found by their keys
+                                                    uint8_t *rpend, uint32_t *counters) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t count = FAST ? *nbig_dev : nbig;
-  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < count;
+  for (uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nbig;
        w += (gridDim.x * blockDim.x) >> 6) {
     const uint32_t beg = big[w];
     if (!rpend[beg]) continue;
     const uint32_t key = ax.key[beg];
-    uint32_t end, lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
-    bool has_lo, has_hi;
-    if (FAST) {
-      end = wave_scan_end(ax, beg + LONG_RUN, key, lane);
-      has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
-      if (has_lo) lo_e = beg, lo_b = wave_scan_begin(ax, beg, key - 1, lane);
-      has_hi = end < ax.m && ax.key[end] == key + 1;
-      if (has_hi) hi_b = end, hi_e = wave_scan_end(ax, end + 1, key + 1, lane);
-    } else {
-      end = beg + ax.rlen_at[beg];
-      has_lo = neighbour_run(ax, beg, end, key, -1, lo_b, lo_e);
-      has_hi = neighbour_run(ax, beg, end, key, 1, hi_b, hi_e);
-    }
+    const uint32_t end = beg + ax.rlen_at[beg];
+    uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
+    const bool has_lo = neighbour_run(ax, beg, end, key, -1, lo_b, lo_e);
+    const bool has_hi = neighbour_run(ax, beg, end, key, 1, hi_b, hi_e);
     bool pending = false;
     for (uint32_t t = beg; t < end; ++t) {
       const uint8_t st = load_state(&ax.state[t]);
       if (st == ST_ACTIVE || st == ST_HIT) continue;
       const uint32_t i = ax.ent[t];
-      Query qy;
-      Q32 q32;
-      int dir;
-      if (FAST) {
-        const uint2 me = ax.pk[t];
-        q32 = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
-        dir = ax.nbd[t] == 1 ? -1 : ax.nbd[t] == 2 ? 1 : 0;
-      } else {
-        const uint64_t c = ax.cen[t];
-        qy = make_query(c, ax.len[t], ax.len_ratio, ax.pos_ratio);
-        dir = neighbour_dir(c, ax.max_index);
-      }
+      const uint64_t c = ax.cen[t];
+      const Query qy = make_query(c, ax.len[t], ax.len_ratio, ax.pos_ratio);
+      const int dir = neighbour_dir(c, ax.max_index);
       Scan s{0.0, NONE, 0xFFFFFFFFu, false, false};
       for (uint32_t q0 = beg; q0 < t; q0 += 64) {  // own run, newest first: rank t-1-q
         const uint32_t q = q0 + lane;
-        if (q < t) {
-          if (FAST) consider_ranked32(ax, s, q, t - 1 - q, q32);
-          else consider_ranked(ax, s, q, t - 1 - q, qy);
-        }
+        if (q < t) consider_ranked(ax, s, q, t - 1 - q, qy);
       }
       if ((dir < 0 && has_lo) || (dir > 0 && has_hi)) {
         const uint32_t nb = dir < 0 ? lo_b : hi_b, ne = dir < 0 ? lo_e : hi_e;
         const uint32_t own = t - beg;
         for (uint32_t q0 = nb; q0 < ne; q0 += 64) {
           const uint32_t q = q0 + lane;
-          if (q < ne && ax.ent[q] < i) {
-            if (FAST) consider_ranked32(ax, s, q, own + (ne - 1 - q), q32);
-            else consider_ranked(ax, s, q, own + (ne - 1 - q), qy);
-          }
+          if (q < ne && ax.ent[q] < i) consider_ranked(ax, s, q, own + (ne - 1 - q), qy);
         }
       }
       wave_combine(s);
@@ -937,7 +912,8 @@ struct LongLds {
   uint8_t nst[2][NCAP];
 };
 
-// the entry-by-entry walk of k_sweep_wave<true> over [from, end) of run [beg, end)
+// the entry-by-entry walk (k_sweep_wave's, on the 32-bit records) over
+// [from, end) of run [beg, end)
 __device__ bool walk_entries32(const Axis &ax, uint32_t beg, uint32_t from, uint32_t end,
                                bool has_lo, uint32_t lo_b, uint32_t lo_e, bool has_hi,
                                uint32_t hi_b, uint32_t hi_e, uint32_t lane) {
@@ -1293,11 +1269,10 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
                 hipStream_t st) {
   rl.nbig = 0;
   rl.nwin = (ax.m + 63) / 64;
-  rl.nbig_dev = dev_count;
   if (!ax.m) return;
-  (void)hipMemsetAsync(dev_count, 0, 4, st);
   (void)hipMemsetAsync(rl.wpend, 1, rl.nwin, st);
-  if (rl.fast32) return;  // the first sweep lists the long runs itself
+  if (rl.fast32) return;  // the first sweep flags the long runs itself
+  (void)hipMemsetAsync(dev_count, 0, 4, st);
   kt_begin(st);
   k_run_bounds<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.nwin, rl.big, dev_count);
   kt_end(st, KID_RUN_BOUNDS, 4.0 * ax.m);  // keys read once (boundary writes not counted)
@@ -1333,8 +1308,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     kt_end(st, KID_SWEEP_LONG, 0.0);
   } else if (rl.nbig) {
     kt_begin(st);
-    k_sweep_wave<false><<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, nullptr,
-                                                                    rpend, counters);
+    k_sweep_wave<<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
+                                                             counters);
     kt_end(st, KID_SWEEP_WAVE, 0.0);
   }
 }

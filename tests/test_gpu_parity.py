@@ -131,6 +131,20 @@ def test_wide_lengths_generic_sweep(gpu_ctx):
     gpu_vs_oracle(gpu_ctx, g, 5_000_000_000, 5_000_000_000)
 
 
+@pytest.mark.parametrize("lr,pr", [(0.05, 0.05), (0.3, 0.3)])
+def test_wide_lengths_long_runs(gpu_ctx, lr, pr):
+    """The 64-bit sweep on bucket runs of 2500 entries (its long-run walk,
+    k_sweep_wave): the long-run set plus a few lengths >= 2^31."""
+    f = long_run_set(2500, seed=77)
+    k = 8
+    rng = np.random.default_rng(77)
+    g = rk.Frags(np.concatenate([f.x_start, rng.integers(1, 1_000_000, k).astype(np.uint64)]),
+                 np.concatenate([f.y_start, rng.integers(1, 1_000_000, k).astype(np.uint64)]),
+                 np.concatenate([f.length, np.full(k, 2**31 + 5, np.uint64)]),
+                 np.concatenate([f.strand, np.full(k, ord('r'), np.uint8)]))
+    gpu_vs_oracle(gpu_ctx, g, 5_000_000_000, 5_000_000_000, lr, pr)
+
+
 def test_empty_and_tiny(gpu_ctx):
     f = rk.Frags(np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint64),
                  np.zeros(0, np.uint8))
