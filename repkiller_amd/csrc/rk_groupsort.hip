@@ -725,19 +725,43 @@ __global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, ui
 }
 
 // groups of 1..16 members: insertion sort == stable rank; one thread per member
+// (members are group-major, so a small group usually lies inside one
+// wavefront's 64 members: its keys come from the other lanes by ds_bpermute;
+// a group that straddles two wavefronts reads them from memory)
 __global__ void k_sort_small(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t m,
                              const uint64_t *key, const uint32_t *tag, uint32_t *otag) {
-  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
-    const uint32_t g = gid_sorted[x];
-    const uint32_t b = goff[g], e = goff[g + 1];
-    if (e - b > (uint32_t)THRESH) continue;
-    const uint64_t kx = key[x];
-    uint32_t r = 0;
-    for (uint32_t y = b; y < e; ++y) {
-      const uint64_t ky = key[y];
-      r += (ky < kx) || (ky == kx && y < x);
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; base < m;
+       base += gridDim.x * blockDim.x) {
+    const uint32_t x = base + lane;
+    const bool in = x < m;
+    uint32_t b = 0, e = 0;
+    uint64_t kx = 0;
+    if (in) {
+      const uint32_t g = gid_sorted[x];
+      b = goff[g], e = goff[g + 1];
+      kx = key[x];
     }
-    otag[b + r] = tag[x];
+    const bool small = in && e - b <= (uint32_t)THRESH;
+    const bool local = small && b >= base && e <= base + 64;
+    uint32_t r = 0;
+    // in-wave groups: up to 16 rounds of lane pulls (the round count is the
+    // largest such group of the wave)
+    const uint32_t len = local ? e - b : 0;
+    for (uint32_t j = 0; __ballot(j < len); ++j) {
+      const int src = j < len ? (int)(b - base + j) : (int)lane;
+      const uint64_t ky = (uint64_t)(uint32_t)__shfl((int)(uint32_t)kx, src) |
+                          (uint64_t)(uint32_t)__shfl((int)(uint32_t)(kx >> 32), src) << 32;
+      const uint32_t y = b + j;
+      r += j < len && ((ky < kx) || (ky == kx && y < x));
+    }
+    if (small && !local) {
+      for (uint32_t y = b; y < e; ++y) {
+        const uint64_t ky = key[y];
+        r += (ky < kx) || (ky == kx && y < x);
+      }
+    }
+    if (small) otag[b + r] = tag[x];
   }
 }
 
