@@ -88,6 +88,8 @@ SYNTH = [
     # dense: ~40 entries per 100-bp bucket and strand, no lead-in -> reruns
     dict(kind="synth", n=20_000, L=60_000, seed=24, lead_in=0),
     dict(kind="synth", n=20_000, L=60_000, seed=25, lead_in=0, lr=1.5, pr=0.7),
+    # a 15-Gbp genome: coordinates and in-group keys above 2^32
+    dict(kind="synth", n=300_000, L=15_000_000_000, seed=29, ff=0.95, copies=(100, 600)),
     # bucket runs of 300 / 2500 entries whose LDS lists overflow at tight ratios
     dict(kind="long_runs", runs_len=300, seed=300, L=10_000_000, lr=0.05, pr=0.05),
     dict(kind="long_runs", runs_len=2500, seed=2500, L=10_000_000, lr=0.05, pr=0.05),
