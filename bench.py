@@ -54,11 +54,11 @@ CONFIGS = {
                  desc="cfg3: 50M fragments, 3 Gbp human-scale self-comparison"),
     # BASELINE.json configs[3] is quoted for 8 GPUs; its 200M fragments also fit
     # one MI355X (~62 GB of HBM), so it runs here as a single-GPU stress case
-    "cfg4": dict(n=200_000_000, genome_len=3_000_000_000,
+    "cfg4": dict(n=200_000_000, genome_len=3_000_000_000, total=True,
                  desc="cfg4: 200M fragments, 3 Gbp x 3 Gbp"),
     # BASELINE.json configs[4] is quoted for 8 GPUs ("streaming / HBM-spill");
     # its 1B fragments fit one MI355X's HBM too (run it with --no-cpu)
-    "cfg5": dict(n=1_000_000_000, genome_len=15_000_000_000,
+    "cfg5": dict(n=1_000_000_000, genome_len=15_000_000_000, total=True,
                  synth=dict(family_frac=0.95, copies=(100, 600)),
                  desc="cfg5: 1B fragments, 15 Gbp repeat-rich self-comparison"),
 }
@@ -219,8 +219,12 @@ def upload(f, dev):
 
 
 def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
-    """ONE fragment set of n x world rows, rank r holding rows [r*n, (r+1)*n)."""
-    n, L = cfg["n"], cfg["genome_len"]
+    """ONE fragment set, rank r holding its block of rows: n x world rows (weak
+    scaling), or -- for the configs BASELINE quotes as one set over 8 GPUs
+    (cfg4, cfg5: `total`) -- the config's n rows split over the ranks (strong)."""
+    n_cfg, L = cfg["n"], cfg["genome_len"]
+    total = cfg.get("total", False)
+    n = n_cfg // world + (1 if rank < n_cfg % world else 0) if total else n_cfg
     f = rk.synth(n, L, seed=rank_seed(rank), **cfg.get("synth", {}))  # this rank's block
     x, y, ln, s = upload(f, dev)
     del f
@@ -238,12 +242,14 @@ def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
     kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps)
     comm.close()
     value = frags_total * args.steps / dt_max
+    n_all = int(frags_total)
     return {
         "value": round(value, 1), "unit": "fragments/s", "n_gpus": world,
-        "ms_per_step": round(dt_max / args.steps * 1e3, 3), "scaling": "weak",
-        "workload": f"ONE {n * world}-fragment set over a {L} bp genome, sharded "
-                    f"({n} fragments per GPU; N=4 is cfg4's 200M)",
-        "fragments_total": n * world, "comm": args.comm,
+        "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+        "scaling": "strong" if total else "weak",
+        "workload": (f"ONE {n_all}-fragment set over a {L} bp genome, sharded over {world} GPUs"
+                     + ("" if total else f" ({n} fragments per GPU; N=4 is cfg4's 200M)")),
+        "fragments_total": n_all, "comm": args.comm,
         "hbm_algorithmic_GBps": round(50 * value / 1e9, 3),
         "roofline": roofline, "kernels": kernels,
         "shard_rank0": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
@@ -343,11 +349,12 @@ def main():
         sh = bench_sharded(args, cfg, rank, world, local, dev, ctx)
         line = {"metric": METRIC, "value": sh["value"], "unit": "fragments/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": sh["ms_per_step"],
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "higher_is_better": True, "scaling": sh["scaling"], "vs_baseline": None,
                 "dtype": "u64/f64",
                 "data": f"synthetic (SURVEY.md §8d generator; rank r's block seeded 3+r), ONE "
                         f"fragment set of {sh['fragments_total']} fragments",
-                "config": {"workload": sh["workload"], "fragments_per_gpu": cfg["n"],
+                "config": {"workload": sh["workload"],
+                           "fragments_per_gpu": sh["fragments_total"] // world,
                            "genome_bp": cfg["genome_len"], "len_ratio": args.len_ratio,
                            "pos_ratio": args.pos_ratio,
                            "parallelism": f"sharded x{world} ({args.comm})"},
