@@ -424,8 +424,8 @@ struct TierLists {
   const uint32_t *list, *off;
   uint32_t nblk;
   __device__ __forceinline__ void range(int u, uint32_t &lo, uint32_t &hi) const {
-    lo = off[(size_t)(u - 1) * nblk];
-    hi = off[(size_t)u * nblk];
+    lo = off[(size_t)u * nblk];
+    hi = off[(size_t)(u + 1) * nblk];
   }
 };
 
@@ -725,43 +725,34 @@ __global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, ui
 }
 
 // groups of 1..16 members: insertion sort == stable rank; one thread per member
-// (members are group-major, so a small group usually lies inside one
-// wavefront's 64 members: its keys come from the other lanes by ds_bpermute;
-// a group that straddles two wavefronts reads them from memory)
-__global__ void k_sort_small(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t m,
-                             const uint64_t *key, const uint32_t *tag, uint32_t *otag) {
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; base < m;
-       base += gridDim.x * blockDim.x) {
-    const uint32_t x = base + lane;
-    const bool in = x < m;
-    uint32_t b = 0, e = 0;
-    uint64_t kx = 0;
-    if (in) {
-      const uint32_t g = gid_sorted[x];
-      b = goff[g], e = goff[g + 1];
-      kx = key[x];
+// groups of 1..16 members (tier 0): insertion sort == stable rank; one thread
+// per group, the keys in registers
+__global__ void __launch_bounds__(256) k_sort_small(TierLists tl, const uint32_t *goff,
+                                                    const uint64_t *key, const uint32_t *tag,
+                                                    uint32_t *otag) {
+  uint32_t lo, hi;
+  tl.range(0, lo, hi);
+  for (uint32_t w = lo + blockIdx.x * blockDim.x + threadIdx.x; w < hi;
+       w += gridDim.x * blockDim.x) {
+    const uint32_t g = tl.list[w];
+    const uint32_t b = goff[g], n = goff[g + 1] - b;
+    if (n == 1) {
+      otag[b] = tag[b];
+      continue;
     }
-    const bool small = in && e - b <= (uint32_t)THRESH;
-    const bool local = small && b >= base && e <= base + 64;
-    uint32_t r = 0;
-    // in-wave groups: up to 16 rounds of lane pulls (the round count is the
-    // largest such group of the wave)
-    const uint32_t len = local ? e - b : 0;
-    for (uint32_t j = 0; __ballot(j < len); ++j) {
-      const int src = j < len ? (int)(b - base + j) : (int)lane;
-      const uint64_t ky = (uint64_t)(uint32_t)__shfl((int)(uint32_t)kx, src) |
-                          (uint64_t)(uint32_t)__shfl((int)(uint32_t)(kx >> 32), src) << 32;
-      const uint32_t y = b + j;
-      r += j < len && ((ky < kx) || (ky == kx && y < x));
-    }
-    if (small && !local) {
-      for (uint32_t y = b; y < e; ++y) {
-        const uint64_t ky = key[y];
-        r += (ky < kx) || (ky == kx && y < x);
+    uint64_t k[THRESH];
+#pragma unroll
+    for (int i = 0; i < THRESH; ++i) k[i] = i < (int)n ? key[b + i] : 0ull;
+#pragma unroll
+    for (int i = 0; i < THRESH; ++i) {
+      if (i < (int)n) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < THRESH; ++j)
+          r += j < (int)n && (k[j] < k[i] || (k[j] == k[i] && j < i));
+        otag[b + r] = tag[b + i];
       }
     }
-    if (small) otag[b + r] = tag[x];
   }
 }
 
@@ -811,8 +802,7 @@ __global__ void __launch_bounds__(256) k_tier_count(const uint32_t *goff, uint32
     if ((threadIdx.x & 63) == 0 && (v || x)) atomicAdd(&cnt[u], v), atomicAdd(&mem[u], x);
   }
   __syncthreads();
-  if (threadIdx.x >= 1 && threadIdx.x < NTIER)
-    bc[(size_t)(threadIdx.x - 1) * nblk + blockIdx.x] = cnt[threadIdx.x];
+  if (threadIdx.x < NTIER) bc[(size_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
   if (bm && threadIdx.x < NTIER) bm[(size_t)threadIdx.x * nblk + blockIdx.x] = mem[threadIdx.x];
 }
 
@@ -823,28 +813,28 @@ __global__ void __launch_bounds__(256) k_tier_lists(const uint32_t *goff, uint32
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t run[NTIER];
 #pragma unroll
-  for (int u = 1; u < NTIER; ++u) run[u] = off[(size_t)(u - 1) * nblk + blockIdx.x];
+  for (int u = 0; u < NTIER; ++u) run[u] = off[(size_t)u * nblk + blockIdx.x];
   const uint32_t g0 = blockIdx.x * TCH, g1 = min(g0 + TCH, ngroups);
   for (uint32_t c0 = g0; c0 < g1; c0 += 256) {
     const uint32_t g = c0 + threadIdx.x;
     const int t = g < g1 ? tier_of(goff[g + 1] - goff[g]) : 0;
     uint32_t rank = 0;
 #pragma unroll
-    for (int u = 1; u < NTIER; ++u) {
-      const uint64_t b = __ballot(t == u);
+    for (int u = 0; u < NTIER; ++u) {
+      const uint64_t b = __ballot(g < g1 && t == u);
       if (t == u) rank = __popcll(b & ((1ull << lane) - 1ull));
       if (lane == 0) wc[wv][u] = (uint32_t)__popcll(b);
     }
     __syncthreads();
-    if (t > 0) {
+    if (g < g1) {
       uint32_t before = 0;
       for (int k = 0; k < wv; ++k) before += wc[k][t];
 #pragma unroll
-      for (int u = 1; u < NTIER; ++u)
+      for (int u = 0; u < NTIER; ++u)
         if (u == t) list[run[u] + before + rank] = g;
     }
 #pragma unroll
-    for (int u = 1; u < NTIER; ++u) run[u] += wc[0][u] + wc[1][u] + wc[2][u] + wc[3][u];
+    for (int u = 0; u < NTIER; ++u) run[u] += wc[0][u] + wc[1][u] + wc[2][u] + wc[3][u];
     __syncthreads();
   }
 }
@@ -862,7 +852,7 @@ size_t groupsort_scratch_bytes(uint32_t n) {
   // pl, pr (stopper lists; segment heads); tier lists; bounds; block counts
   // (+ scan), block members
   return (size_t)n * 4 * 2 + ((size_t)n + 1) * 4 + (size_t)n + 128 +
-         (nblk * (NTIER - 1) + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + 256;
+         (nblk * NTIER + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + 256;
 }
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
@@ -870,7 +860,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
                        ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
                        hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
   if (!m) return;
-  constexpr int NL = NTIER - 1;  // listed tiers 1..6
+  constexpr int NL = NTIER;  // every tier is listed
   // groups of <= 64 members (k_sort_small, registers) run on `side`,
   // concurrently with the LDS tiers
   hipStream_t s2 = side ? side : st;
@@ -886,17 +876,9 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   uint32_t *boff = bc + (size_t)NL * nblk + 1;
   uint32_t *bm = boff + (size_t)NL * nblk + 1;
   const bool timing = g_ktimer != nullptr;
-  if (side) {
-    (void)hipEventRecord(ev_fork, st);
-    (void)hipStreamWaitEvent(s2, ev_fork, 0);
-  }
-  kt_begin(s2);
-  k_sort_small<<<grid_for(m, 256), 256, 0, s2>>>(gid_sorted, goff, m, key, tag, otag);
-  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
   if (timing) {
     g_ktimer->tier_nblk = nblk;
     for (int u = 0; u < KernelTimer::TIERS; ++u) g_ktimer->tier_slot[u] = -1;
-    g_ktimer->tier_slot[0] = g_ktimer->n - 1;
   }
   k_tier_count<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, bc, timing ? bm : nullptr);
   (void)hipMemsetAsync(bc + (size_t)NL * nblk, 0, 4, st);
@@ -916,6 +898,10 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     (void)hipEventRecord(ev_fork, st);  // the tier lists are ready
     (void)hipStreamWaitEvent(s2, ev_fork, 0);
   }
+  kt_begin(s2);
+  k_sort_small<<<4096, 256, 0, s2>>>(tl, goff, key, tag, otag);
+  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
+  tier_slot(0);
   kt_begin(s2);
   k_sort_groups_reg<<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
   kt_end(s2, KID_SORT_REG, 0.0);
