@@ -372,7 +372,7 @@ def main():
                     line["sharded"] = {"error": f"timeout after {args.sharded_timeout} s"}
                     line["cpu_baseline"] = None
                     print(json.dumps(line), flush=True)
-                os._exit(0)
+                os._exit(3)  # a stuck collective is a failure, not a clean exit
             dog = threading.Timer(args.sharded_timeout, give_up)
             dog.daemon = True
             dog.start()

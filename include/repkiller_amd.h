@@ -46,6 +46,8 @@ typedef enum {
   RK_E_NODEVICE = -8,    /* no usable gfx950 device */
   RK_E_TOO_MANY = -9,    /* n >= 2^32 - 1 (32-bit row ids) */
   RK_E_INTERNAL = -10,   /* a device-side consistency check failed */
+  RK_E_PEER = -11,       /* rk_classify_sharded*: another rank of the comm failed; every
+                            rank returns an error together (rk_last_error names the rank) */
 } rk_status;
 
 /* ---- classification (the hot path) ----------------------------------- */
@@ -159,6 +161,11 @@ int rk_comm_rccl_id(uint8_t id[RK_COMM_ID_BYTES]);
 int rk_comm_create_rccl(int rank, int size, int device, const uint8_t id[RK_COMM_ID_BYTES],
                         rk_comm **comm);
 void rk_comm_destroy(rk_comm *comm);
+/* A rank that cannot make its rk_classify_sharded* call (e.g. rk_create
+ * failed) calls this instead, once: it takes part in the peers' first
+ * collective with `status`, and every peer's call returns RK_E_PEER instead of
+ * waiting for it. */
+int rk_comm_abandon(rk_comm *comm, int status);
 const char *rk_comm_last_error(const rk_comm *comm);
 
 typedef struct {

@@ -35,7 +35,7 @@ N_PHASES = 10  # RK_N_PHASES
 STATUS = {
     0: "RK_OK", -1: "RK_E_ARG", -2: "RK_E_IO", -3: "RK_E_COUNT", -4: "RK_E_UB_BUCKET",
     -5: "RK_E_UB_CENTER", -6: "RK_E_NOMEM", -7: "RK_E_HIP", -8: "RK_E_NODEVICE",
-    -9: "RK_E_TOO_MANY", -10: "RK_E_INTERNAL",
+    -9: "RK_E_TOO_MANY", -10: "RK_E_INTERNAL", -11: "RK_E_PEER",
 }
 
 # every symbol include/repkiller_amd.h declares (checked by tests/test_abi.py)
@@ -49,6 +49,7 @@ EXPORTS = (
     "rk_synth_write_csv", "rk_comm_create_host", "rk_comm_rccl_id", "rk_comm_create_rccl",
     "rk_comm_destroy", "rk_comm_last_error", "rk_classify_sharded", "rk_get_shard_stats",
     "rk_shard_copy_result", "rk_comm_create_local", "rk_classify_sharded_host",
+    "rk_comm_abandon",
 )
 
 
@@ -187,6 +188,7 @@ def load_library() -> ctypes.CDLL:
                                                ctypes.POINTER(vp)]),
         "rk_comm_destroy": (None, [vp]),
         "rk_comm_last_error": (ctypes.c_char_p, [vp]),
+        "rk_comm_abandon": (ctypes.c_int, [vp, ctypes.c_int]),
         "rk_classify_sharded": (ctypes.c_int, [vp, vp, ctypes.POINTER(FragsSoA),
                                                ctypes.POINTER(Params), ctypes.c_int32,
                                                ctypes.POINTER(ShardResult)]),
@@ -231,14 +233,16 @@ class Frags:
 
 
 def synth(n: int, genome_len: int, seed: int, family_frac: float = 0.8,
-          copies: tuple[int, int] = (2, 30)) -> Frags:
-    """Deterministic synthetic fragment set (SURVEY.md §8d generator)."""
+          copies: tuple[int, int] = (2, 30), with_ident: bool = True) -> Frags:
+    """Deterministic synthetic fragment set (SURVEY.md §8d generator).
+    with_ident=False skips the identity column (only the CSV writer reads it)."""
     lib = load_library()
     f = Frags(np.empty(n, np.uint64), np.empty(n, np.uint64), np.empty(n, np.uint64),
-              np.empty(n, np.uint8), np.empty(n, np.uint64))
+              np.empty(n, np.uint8), np.empty(n, np.uint64) if with_ident else None)
     p = SynthParams(n, genome_len, seed, family_frac, copies[0], copies[1])
     _check(lib.rk_synth_generate(ctypes.byref(p), _ptr(f.x_start), _ptr(f.y_start),
-                                 _ptr(f.length), _ptr(f.strand), _ptr(f.ident)))
+                                 _ptr(f.length), _ptr(f.strand),
+                                 _ptr(f.ident) if f.ident is not None else 0))
     return f
 
 

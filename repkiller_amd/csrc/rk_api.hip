@@ -628,8 +628,9 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
   for (uint32_t s = 0; s < nseg; ++s)
     for (uint32_t x = seg_off[s]; x < seg_off[s + 1]; ++x) sg[x] = s, tags[x] = x;
   const size_t gs = rk::groupsort_scratch_bytes(m), sc = rk::scan_blocks(nseg + 2) + 64;
-  const size_t bytes = align_up(m * 8 + 16) + align_up(m * 4 + 16) * 3 +
-                       align_up((nseg + 1) * 4 + 16) + align_up(gs) + align_up(sc * 4);
+  const size_t M = m;  // byte sizes in 64 bits: m * 8 wraps a uint32_t from m = 2^29
+  const size_t bytes = align_up(M * 8 + 16) + align_up(M * 4 + 16) * 3 +
+                       align_up(((size_t)nseg + 1) * 4 + 16) + align_up(gs) + align_up(sc * 4);
   void *buf = nullptr;
   HIPCHK(ctx, hipMalloc(&buf, bytes));
   Carve c{(char *)buf};
@@ -640,10 +641,11 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
   uint32_t *dsc = c.take<uint32_t>(sc);
   hipStream_t st = ctx->stream;
   int rc = RK_OK;
-  if (hipMemcpyAsync(dk, keys, m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(dt, tags.data(), m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(dg, sg.data(), m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(doff, seg_off, (nseg + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+  if (hipMemcpyAsync(dk, keys, M * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dt, tags.data(), M * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dg, sg.data(), M * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(doff, seg_off, ((size_t)nseg + 1) * 4, hipMemcpyHostToDevice, st) !=
+          hipSuccess) {
     rc = RK_E_HIP;
   } else {
     bool narrow = true;
@@ -651,7 +653,7 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
     rk::sort_groups_exact(dg, doff, nseg, m, dk, dt, dot, dgs, rk::ScanScratch{dsc, sc},
                           ctx->host + 128, narrow, st);
     if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(perm, dot, m * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(perm, dot, M * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
       rc = RK_E_HIP;
   }

@@ -79,6 +79,8 @@ static int classify_sharded_threads(const rk_frags_soa &soa, int device, int gpu
       rk_ctx *ctx = nullptr;
       if ((status[r] = rk_create(&ctx, dev))) {
         msgs[r] = "no usable gfx950 device " + std::to_string(dev);
+        // the peers' first pair waits for this rank: release them
+        (void)rk_comm_abandon(comms[r], status[r]);
         return;
       }
       const uint64_t a = soa.n * (uint64_t)r / gpus, b = soa.n * (uint64_t)(r + 1) / gpus;

@@ -46,6 +46,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
 
 #include "rk_comm.h"
 #include "rk_ctx.h"
@@ -590,6 +593,37 @@ struct PartPlan {
   uint64_t total = 0;
 };
 
+// The driver's all-gather message (see Shard::allgather): a 16-B header whose
+// first word is the sender's status, then up to GMAX payload bytes.
+constexpr size_t GMAX = NBINS * 4, GHDR = 16;
+constexpr int STATUS_COMM_FAILED = 0x7fffffff;
+int status_message(rk_comm *comm, hipStream_t st, int32_t status, const void *mine, void *all,
+                   size_t bytes, uint32_t *who, std::string *err, std::vector<char> &snd,
+                   std::vector<char> &rcv) {
+  if (bytes > GMAX) {
+    *err = "allgather payload above the fixed message size";
+    return STATUS_COMM_FAILED;
+  }
+  const size_t P = (size_t)comm->size;
+  snd.assign(GHDR + GMAX, 0);
+  rcv.resize((GHDR + GMAX) * P);
+  std::memcpy(snd.data(), &status, 4);
+  if (bytes) std::memcpy(snd.data() + GHDR, mine, bytes);
+  if (comm->allgather(snd.data(), rcv.data(), GHDR + GMAX, st)) {
+    *err = "allgather: " + comm->err;
+    return STATUS_COMM_FAILED;
+  }
+  int first = 0;
+  for (size_t q = 0; q < P; ++q) {
+    int32_t sq;
+    std::memcpy(&sq, rcv.data() + (GHDR + GMAX) * q, 4);
+    if (sq && !first) first = sq, *who = (uint32_t)q;
+    if (bytes && all)
+      std::memcpy((char *)all + bytes * q, rcv.data() + (GHDR + GMAX) * q + GHDR, bytes);
+  }
+  return first;
+}
+
 struct Shard {
   rk_ctx *ctx;
   rk_comm *comm;
@@ -630,11 +664,50 @@ struct Shard {
   }
   void launched(const char *what) { hip(hipGetLastError(), what); }
 
+  // Every all-gather of the driver is one fixed-size message per rank: a
+  // status word plus up to GMAX payload bytes.  A rank that fails locally
+  // (allocation, HIP error, consistency check) sends its status in ONE such
+  // message from the top-level handler (fail_broadcast): its peers are then
+  // inside their next all-gather (every all-to-all is preceded by one, see
+  // exchange()), receive the status and fail together with RK_E_PEER instead
+  // of waiting forever, and the comm stays in step for the next call.
+  bool peer_failed = false;  // a collective reported a failure on some rank
+  bool comm_broken = false;  // the comm itself failed: no further collectives
+  std::vector<char> gsend, grecv;
   void allgather(const void *mine, void *all, size_t bytes) {
-    if (comm->allgather(mine, all, bytes, st)) {
-      ctx->err = "allgather: " + comm->err;
+    if (status_gather(0, mine, all, bytes)) throw RK_E_PEER;
+  }
+  // returns the first non-zero status of any rank (0: every rank is fine)
+  int status_gather(int32_t status, const void *mine, void *all, size_t bytes) {
+    uint32_t who = 0;
+    std::string cerr;
+    const int first = status_message(comm, st, status, mine, all, bytes, &who, &cerr, gsend,
+                                     grecv);
+    if (first == STATUS_COMM_FAILED) {
+      comm_broken = true;
+      ctx->err = cerr;
       throw RK_E_HIP;
     }
+    if (first) {
+      peer_failed = true;
+      if (!status)
+        ctx->err = "rank " + std::to_string(who) + " failed (status " + std::to_string(first) +
+                   "); every rank stops";
+    }
+    return first;
+  }
+  // a rank that failed outside a collective releases its peers (see allgather)
+  void fail_broadcast(int code) {
+    if (peer_failed || comm_broken) return;
+    try {
+      (void)status_gather(code ? code : RK_E_INTERNAL, nullptr, nullptr, 0);
+    } catch (...) {
+    }
+  }
+  // every rank's local status at an agreement point (before each all-to-all):
+  // all continue or all fail
+  void agree(int rc) {
+    if (status_gather(rc, nullptr, nullptr, 0)) throw rc ? rc : (int)RK_E_PEER;
   }
   template <class T>
   std::vector<T> gather1(T v) {
@@ -708,7 +781,16 @@ struct Shard {
       ctx->err = "a rank would receive more than 2^32-1 records";
       throw RK_E_TOO_MANY;
     }
-    T *recv = take<T>(recv_slot, tot / esz + 1);
+    // the receive buffer (its size depends on the other ranks' data: the
+    // allocation most likely to fail under skew) is agreed before data moves
+    T *recv = nullptr;
+    int rc = RK_OK;
+    try {
+      recv = take<T>(recv_slot, tot / esz + 1);
+    } catch (int code) {
+      rc = code;
+    }
+    agree(rc);
     run_a2a(send, sb, recv, rb);
     *nrecv = (uint32_t)(tot / esz);
     if (from)
@@ -724,6 +806,7 @@ struct Shard {
     const int rc = comm->alltoallv(send, sb, recv, rb, st);
     kt_end(st, KID_EXCHANGE, moved);  // bytes read + written (device time of the a2a)
     if (rc) {
+      comm_broken = true;
       ctx->err = "alltoallv: " + comm->err;
       throw RK_E_HIP;
     }
@@ -858,45 +941,53 @@ uint32_t resolve(Shard &S, const AxisIn &a, const AxisSlots &sl, const rk_params
   return sweep_axis(S, a, c, p);
 }
 
-int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const rk_params *prm,
-                     int32_t lead_in, rk_shard_result *out) {
-  if (!ctx || !comm || !in || !prm || !out) return RK_E_ARG;
-  if (comm->size < 1 || (uint32_t)comm->size > MAXP) return RK_E_ARG;
-  if (in->n && (!in->x_start || !in->y_start || !in->length || !in->strand)) return RK_E_ARG;
-  HIPCHK(ctx, hipSetDevice(ctx->device));
+int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm,
+                          int32_t lead_in, rk_shard_result *out, int pre) {
+  rk_ctx *ctx = S.ctx;
   const auto t0 = std::chrono::steady_clock::now();
   rk_shard_stats &ss = ctx->shard_stats;
   std::memset(&ss, 0, sizeof ss);
-  Shard S{ctx, comm, ctx->stream, ctx->stream2, (uint32_t)comm->size, (uint32_t)comm->rank};
   const uint32_t P = S.P, me = S.me;
   const uint64_t H = lead_in < 0 ? 2 : (uint64_t)lead_in;
-  const rk_params p = *prm;
+  const rk_params p = pre ? rk_params{1000, 1000, 1, 1} : *prm;
   const uint64_t len_x = p.len_x_hdr + 1, len_y = p.len_y_hdr + 1;  // FragmentsDatabase.cpp:62,65
   const uint64_t vsize = 1 + len_x / 10;                             // :84
   const uint64_t max_x = len_x / 100, max_y = len_y / 100;           // SequenceOcupationList.cpp:4
-  // every rank validates the same arguments, so all return together
-  if (!(p.len_ratio > 0) && !std::isnan(p.len_ratio)) return RK_E_ARG;
-  if (!(p.pos_ratio > 0) && !std::isnan(p.pos_ratio)) return RK_E_ARG;
-  if (vsize - 1 >= 0xFFFFFFF0ull || 2 * (max_x + 1) >= 0xFFFFFFF0ull ||
-      2 * (max_y + 1) >= 0xFFFFFFF0ull) {
+  // local argument checks become this rank's status in the first collective,
+  // so a rank that cannot run never leaves its peers waiting
+  int rc = pre;
+  if (!rc && ((!(p.len_ratio > 0) && !std::isnan(p.len_ratio)) ||
+              (!(p.pos_ratio > 0) && !std::isnan(p.pos_ratio))))
+    rc = RK_E_ARG;
+  if (!rc && (vsize - 1 >= 0xFFFFFFF0ull || 2 * (max_x + 1) >= 0xFFFFFFF0ull ||
+              2 * (max_y + 1) >= 0xFFFFFFF0ull)) {
     ctx->err = "sequence length too large for 32-bit bucket ids";
-    return RK_E_ARG;
+    rc = RK_E_ARG;
   }
   const uint32_t nbx = (uint32_t)(max_x + 1), nby = (uint32_t)(max_y + 1);
   const uint32_t drop = (uint32_t)(vsize - 1);  // the never-iterated last bucket
 
-  if (ctx->profiling) {  // launch-level timing of the pipeline kernels (rk_get_kernel_timing)
+  if (!rc && ctx->profiling) {  // launch-level timing of the pipeline kernels
     ctx->kt.n = 0;
     g_ktimer = &ctx->kt;
   }
-  S.ctrl = S.take<uint32_t>(SL_CTRL, 256);
-  S.zero(S.ctrl, 256 * 4);
+  if (!rc) {
+    try {
+      S.ctrl = S.take<uint32_t>(SL_CTRL, 256);
+      S.zero(S.ctrl, 256 * 4);
+    } catch (int code) {
+      rc = code;
+    }
+  }
 
-  // ---- 0: global row numbering (rank blocks are consecutive in file order)
-  std::vector<uint64_t> nall = S.gather1<uint64_t>(in->n);
+  // ---- 0: global row numbering (rank blocks are consecutive in file order);
+  // the first collective carries every rank's status
+  const uint64_t n_mine = rc ? 0 : in->n;
+  std::vector<uint64_t> nall(P);
+  if (S.status_gather(rc, &n_mine, nall.data(), sizeof n_mine)) throw rc ? rc : (int)RK_E_PEER;
   uint64_t row_base = 0, N = 0;
   for (uint32_t q = 0; q < P; ++q) N += nall[q], row_base += q < me ? nall[q] : 0;
-  if (N >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
+  if (N >= 0xFFFFFFFFull) return RK_E_TOO_MANY;  // every rank sees the same N
   const uint32_t nl = (uint32_t)in->n;
   ss.n_in = nl;
   ss.n_total = N;
@@ -1435,16 +1526,54 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
   return RK_OK;
 }
 
+// A rank that cannot run the call at all joins its peers' first collective
+// with a failure status, so that they stop too.
+int status_broadcast(rk_comm *comm, int status) {
+  std::vector<char> a, b;
+  uint32_t who = 0;
+  std::string err;
+  const int r = status_message(comm, nullptr, status, nullptr, nullptr, 0, &who, &err, a, b);
+  return r == STATUS_COMM_FAILED ? RK_E_HIP : RK_OK;
+}
+
+// A failure on one rank becomes a failure of every rank (Shard::allgather):
+// `pre` is a status this rank already has (e.g. its input upload failed).
+int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const rk_params *prm,
+                     int32_t lead_in, rk_shard_result *out, int pre) {
+  if (!comm || comm->size < 1 || (uint32_t)comm->size > MAXP) return RK_E_ARG;
+  if (!ctx) {
+    (void)status_broadcast(comm, RK_E_ARG);
+    return RK_E_ARG;
+  }
+  int rc = pre;
+  if (!rc && (!in || !prm || !out)) rc = RK_E_ARG;
+  if (!rc && in->n && (!in->x_start || !in->y_start || !in->length || !in->strand))
+    rc = RK_E_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) {
+    ctx->err = "hipSetDevice failed";
+    if (!rc) rc = RK_E_HIP;
+  }
+  Shard S{ctx, comm, ctx->stream, ctx->stream2, (uint32_t)comm->size, (uint32_t)comm->rank};
+  try {
+    return classify_sharded_impl(S, in, prm, lead_in, out, rc);
+  } catch (int code) {
+    S.fail_broadcast(code);  // no-op when the failure is already shared
+    throw;
+  } catch (...) {
+    S.fail_broadcast(RK_E_INTERNAL);
+    throw;
+  }
+}
+
 }  // namespace
 }  // namespace rk
 
-extern "C" int rk_classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in_dev,
-                                   const rk_params *p, int32_t lead_in, rk_shard_result *out) {
-  if (!ctx) return RK_E_ARG;
-  ctx->err.clear();
+static int classify_sharded_entry(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in_dev,
+                                  const rk_params *p, int32_t lead_in, rk_shard_result *out,
+                                  int pre) {
   int rc;
   try {
-    rc = rk::classify_sharded(ctx, comm, in_dev, p, lead_in, out);
+    rc = rk::classify_sharded(ctx, comm, in_dev, p, lead_in, out, pre);
   } catch (int code) {
     rc = code;
   } catch (...) {
@@ -1453,7 +1582,15 @@ extern "C" int rk_classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_so
   }
   rk::g_ktimer = nullptr;
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   return rc;
+}
+
+extern "C" int rk_classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in_dev,
+                                   const rk_params *p, int32_t lead_in, rk_shard_result *out) {
+  if (!ctx) return rk::classify_sharded(ctx, comm, in_dev, p, lead_in, out, RK_E_ARG);
+  ctx->err.clear();
+  return classify_sharded_entry(ctx, comm, in_dev, p, lead_in, out, RK_OK);
 }
 
 extern "C" int rk_get_shard_stats(const rk_ctx *ctx, rk_shard_stats *st) {
@@ -1479,28 +1616,44 @@ extern "C" int rk_shard_copy_result(rk_ctx *ctx, const rk_shard_result *res, uin
 extern "C" int rk_classify_sharded_host(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in,
                                         const rk_params *p, int32_t lead_in,
                                         rk_shard_result *out) {
-  if (!ctx || !in) return RK_E_ARG;
+  if (!ctx) return rk::classify_sharded(ctx, comm, in, p, lead_in, out, RK_E_ARG);
   ctx->err.clear();
-  const size_t n = in->n;
-  if (n && (!in->x_start || !in->y_start || !in->length || !in->strand)) return RK_E_ARG;
-  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // a failure here is this rank's status in the first collective of
+  // classify_sharded, so the peers stop with it instead of waiting
+  int pre = RK_OK;
+  const size_t n = in ? in->n : 0;
+  if (!in || (n && (!in->x_start || !in->y_start || !in->length || !in->strand))) pre = RK_E_ARG;
+  if (!pre && hipSetDevice(ctx->device) != hipSuccess) pre = RK_E_HIP;
   const size_t need = rk::align_up(n * 8 + 16) * 3 + rk::align_up(n + 16);
-  if (need > ctx->io_cap) {
+  if (!pre && need > ctx->io_cap) {
     if (ctx->io) (void)hipFree(ctx->io);
     ctx->io = nullptr;
     ctx->io_cap = 0;
-    HIPCHK(ctx, hipMalloc(&ctx->io, need));
-    ctx->io_cap = need;
+    if (hipMalloc(&ctx->io, need) != hipSuccess) {
+      ctx->err = "sharded input hipMalloc(" + std::to_string(need) + ") failed";
+      pre = RK_E_NOMEM;
+    } else {
+      ctx->io_cap = need;
+    }
   }
-  rk::Carve c{(char *)ctx->io};
-  uint64_t *dx = c.take<uint64_t>(n), *dy = c.take<uint64_t>(n), *dl = c.take<uint64_t>(n);
-  uint8_t *ds = c.take<uint8_t>(n);
-  if (n) {
-    HIPCHK(ctx, hipMemcpyAsync(dx, in->x_start, n * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(dy, in->y_start, n * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(dl, in->length, n * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ds, in->strand, n, hipMemcpyHostToDevice, ctx->stream));
+  rk_frags_soa din{nullptr, nullptr, nullptr, nullptr, 0};
+  if (!pre) {
+    rk::Carve c{(char *)ctx->io};
+    uint64_t *dx = c.take<uint64_t>(n), *dy = c.take<uint64_t>(n), *dl = c.take<uint64_t>(n);
+    uint8_t *ds = c.take<uint8_t>(n);
+    if (n && (hipMemcpyAsync(dx, in->x_start, n * 8, hipMemcpyHostToDevice, ctx->stream) ||
+              hipMemcpyAsync(dy, in->y_start, n * 8, hipMemcpyHostToDevice, ctx->stream) ||
+              hipMemcpyAsync(dl, in->length, n * 8, hipMemcpyHostToDevice, ctx->stream) ||
+              hipMemcpyAsync(ds, in->strand, n, hipMemcpyHostToDevice, ctx->stream))) {
+      ctx->err = "sharded input upload failed";
+      pre = RK_E_HIP;
+    }
+    din = rk_frags_soa{dx, dy, dl, ds, n};
   }
-  rk_frags_soa din{dx, dy, dl, ds, n};
-  return rk_classify_sharded(ctx, comm, &din, p, lead_in, out);
+  return classify_sharded_entry(ctx, comm, &din, p, lead_in, out, pre);
+}
+
+extern "C" int rk_comm_abandon(rk_comm *comm, int status) {
+  if (!comm) return RK_E_ARG;
+  return rk::status_broadcast(comm, status ? status : RK_E_INTERNAL);
 }

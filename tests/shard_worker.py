@@ -51,8 +51,11 @@ def worker(rank, world, port, cases, q, comm_kind="host"):
                 return torch.from_numpy(arr[a:b].astype(dt, copy=True)).to(dev)
             x, y = t(f.x_start, "int64"), t(f.y_start, "int64")
             ln, s = t(f.length, "int64"), t(f.strand, "uint8")
+            lr = case.get("lr", 0.3)
+            if case.get("bad_rank") == rank:
+                lr = -1.0  # this rank alone fails its argument check
             try:
-                out = rk.classify_sharded(ctx, comm, x, y, ln, s, lx, ly, case.get("lr", 0.3),
+                out = rk.classify_sharded(ctx, comm, x, y, ln, s, lx, ly, lr,
                                           case.get("pr", 0.3), case.get("lead_in", -1))
             except rk.RkError as e:
                 q.put((ci, rank, "error", e.code))

@@ -311,75 +311,3 @@ def test_std_sort_large_segments_vs_restatement(gpu_ctx):
     for a, b, s in zip(off[:-1], off[1:], segs):
         want = ro.std_sort(s) + a
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
-
-
-def full_size_properties(gpu_ctx, f, L):
-    """Size-independent properties of the reference's output on a set too
-    large for the oracle -- determinism, output order a permutation of the
-    kept rows (the last xStart/10 bucket is dropped), gids dense and in
-    creation order, repeat flags 0 / 1 / 2 by group position, and every group
-    sorted by the sort_groups key |yStart - diag_func[xStart/10]| (std::sort's
-    result is sorted; commonFunctions.cpp:148-177)."""
-    import torch
-    n = f.n
-    dev = torch.device("cuda", 0)
-    x = torch.from_numpy(f.x_start.view(np.int64)).to(dev)
-    y = torch.from_numpy(f.y_start.view(np.int64)).to(dev)
-    ln = torch.from_numpy(f.length.view(np.int64)).to(dev)
-    s = torch.from_numpy(f.strand).to(dev)
-    outs = []
-    for _ in range(2):
-        gid = torch.empty(n, dtype=torch.int32, device=dev)
-        rep = torch.empty(n, dtype=torch.uint8, device=dev)
-        order = torch.empty(n, dtype=torch.int32, device=dev)
-        n_out, ng = gpu_ctx.classify_device(x, y, ln, s, gid, rep, order, L, L)
-        outs.append((n_out, ng, gid[:n_out].cpu().numpy().view(np.uint32),
-                     rep[:n_out].cpu().numpy(), order[:n_out].cpu().numpy().view(np.uint32)))
-        del gid, rep, order
-    del x, y, ln, s
-    assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1]
-    for a, b in zip(outs[0][2:], outs[1][2:]):
-        assert np.array_equal(a, b)
-    n_out, ng, gid, rep, order = outs[0]
-    xs, ys = f.x_start.astype(np.int64), f.y_start.astype(np.int64)
-    vsize = 1 + (L + 1) // 10
-    kept = np.flatnonzero(xs // 10 != vsize - 1)
-    assert n_out == kept.size
-    assert np.array_equal(np.sort(order), kept)
-    # gids: 0, 1, 2, ... in output order, each group contiguous
-    step = np.diff(gid.astype(np.int64))
-    assert gid[0] == 0 and gid[-1] == ng - 1 and np.all((step == 0) | (step == 1))
-    starts = np.flatnonzero(np.r_[True, step != 0])
-    sizes = np.diff(np.r_[starts, n_out])
-    want = np.full(n_out, 2, np.uint8)
-    want[starts] = 1
-    want[starts[sizes == 1]] = 0
-    assert np.array_equal(rep, want)
-    # diag_func[b] = yStart of the LAST fragment of xStart/10 bucket b (file order)
-    b = xs // 10
-    ordb = np.argsort(b, kind="stable")
-    last = np.r_[b[ordb][1:] != b[ordb][:-1], True]
-    bl, yl = b[ordb][last], ys[ordb][last]
-    idx = np.searchsorted(bl, b[order])
-    ha = np.abs(ys[order] - yl[idx])
-    same = step == 0
-    assert np.all(ha[1:][same] >= ha[:-1][same])
-    return ng
-
-
-def test_cfg3_full_size_properties(gpu_ctx):
-    """BASELINE cfg3 at full size (50M fragments, 3 Gbp)."""
-    full_size_properties(gpu_ctx, rk.synth(50_000_000, 3_000_000_000, seed=3), 3_000_000_000)
-
-
-def test_cfg5_shaped_properties(gpu_ctx):
-    """BASELINE cfg5's shape on one GPU: a 15 Gbp repeat-rich comparison (95 %
-    family fragments, 100-600 copies per family) at 60M fragments (cfg5 itself,
-    1B fragments, needs ~310 GB: the sharded path over 8 GPUs).  Exercises
-    300M occupancy buckets per axis, long bucket runs (the wave-per-run sweep)
-    and very large groups (the global group-sort tier)."""
-    L = 15_000_000_000
-    f = rk.synth(60_000_000, L, seed=5, family_frac=0.95, copies=(100, 600))
-    ng = full_size_properties(gpu_ctx, f, L)
-    assert ng > 0
-

@@ -156,6 +156,26 @@ def test_sharded_edge_fixtures(gpu_ctx, tmp_path):
             assert out.read_bytes() == f.read(), name
 
 
+def test_sharded_one_rank_fails(gpu_ctx):
+    """A rank that fails locally takes its peers down with it (status word in
+    the driver's all-gather message): the failing rank returns its own error,
+    every other rank RK_E_PEER, nobody waits, and the comm is still in step
+    for the next call (the case after it succeeds bit-exactly)."""
+    base = dict(kind="synth", n=50_000, L=5_000_000, seed=33)
+    world = 3
+    cases = [dict(base, bad_rank=1), dict(base, bad_rank=0), base]
+    got = run_ranks(world, cases)
+    for ci, bad in ((0, 1), (1, 0)):
+        for r in range(world):
+            kind, code = got[(ci, r)]
+            assert kind == "error", (ci, r, kind)
+            assert code == (-1 if r == bad else -11), (ci, r, code)
+    order, gid, rep, ng, _ = assemble(got, 2, world)
+    want, *_ = reference(gpu_ctx, base)
+    assert ng == want.n_groups and np.array_equal(order, want.out_order)
+    assert np.array_equal(gid, want.gid) and np.array_equal(rep, want.repval)
+
+
 def test_sharded_rccl_single_rank(gpu_ctx):
     cases = [dict(kind="synth", n=100_000, L=10_000_000, seed=31)]
     got = run_ranks(1, cases, comm_kind="rccl")

@@ -3,7 +3,7 @@
 Classifies the full set three times from HBM-resident inputs and prints one JSON
 line: per-run wall time, workspace footprint, group counts and a verdict on the
 size-independent properties the full-size parity tests check at 50-60M
-(tests/test_gpu_parity.py::full_size_properties), restated in O(n) host memory:
+(tests/test_large_configs.py::device_properties), restated in O(n) host memory:
 run 1 == run 3 (determinism), output order a permutation of the kept rows, gids
 dense in output order, repeat flags by group position, and every group sorted
 by |yStart - diag_func[xStart/10]| (commonFunctions.cpp:148-177).
