@@ -90,6 +90,10 @@ typedef struct {
   uint32_t x_sweeps, y_sweeps, jump_rounds;
   uint64_t x_hits, y_hits;
   double device_ms; /* HIP-event time of the whole device pipeline */
+  uint32_t pipeline; /* the pipeline that produced the result: 1 record, 2 generic */
+  uint32_t record_fallback; /* why the record pipeline handed over: 0 it did not, 1 a row
+                               does not pack into a record, 2 an X bucket denser than a
+                               chunk's LDS list */
 } rk_stats;
 
 int rk_create(rk_ctx **ctx, int device);
@@ -117,6 +121,14 @@ int rk_classify_device_pairs(rk_ctx *ctx, const rk_frags_soa *in_dev, const rk_p
                              uint32_t npairs, rk_result *out_dev);
 
 int rk_get_stats(const rk_ctx *ctx, rk_stats *st);
+
+/* Which device pipeline rk_classify* uses on this context.  AUTO (default):
+ * the record pipeline whenever every row packs into its 16-B record (length
+ * < 2^24, yStart < 2^35, fewer than 2^30 rows, X chunks within their LDS
+ * capacity), else the generic one; GENERIC: always the generic pipeline.
+ * Both produce the same output. */
+enum { RK_PIPELINE_AUTO = 0, RK_PIPELINE_GENERIC = 1 };
+int rk_set_pipeline(rk_ctx *ctx, int pipeline);
 
 /* ---- ONE fragment set sharded over several GPUs ----------------------
  *

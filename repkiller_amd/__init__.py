@@ -49,7 +49,7 @@ EXPORTS = (
     "rk_synth_write_csv", "rk_comm_create_host", "rk_comm_rccl_id", "rk_comm_create_rccl",
     "rk_comm_destroy", "rk_comm_last_error", "rk_classify_sharded", "rk_get_shard_stats",
     "rk_shard_copy_result", "rk_comm_create_local", "rk_classify_sharded_host",
-    "rk_comm_abandon",
+    "rk_comm_abandon", "rk_set_pipeline",
 )
 
 
@@ -85,7 +85,8 @@ class Stats(ctypes.Structure):
                 ("n_groups", ctypes.c_uint64), ("x_sweeps", ctypes.c_uint32),
                 ("y_sweeps", ctypes.c_uint32), ("jump_rounds", ctypes.c_uint32),
                 ("x_hits", ctypes.c_uint64), ("y_hits", ctypes.c_uint64),
-                ("device_ms", ctypes.c_double)]
+                ("device_ms", ctypes.c_double), ("pipeline", ctypes.c_uint32),
+                ("record_fallback", ctypes.c_uint32)]
 
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -189,6 +190,7 @@ def load_library() -> ctypes.CDLL:
         "rk_comm_destroy": (None, [vp]),
         "rk_comm_last_error": (ctypes.c_char_p, [vp]),
         "rk_comm_abandon": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rk_set_pipeline": (ctypes.c_int, [vp, ctypes.c_int]),
         "rk_classify_sharded": (ctypes.c_int, [vp, vp, ctypes.POINTER(FragsSoA),
                                                ctypes.POINTER(Params), ctypes.c_int32,
                                                ctypes.POINTER(ShardResult)]),
@@ -377,6 +379,11 @@ class Context:
         s = Stats()
         _check(load_library().rk_get_stats(self._h, ctypes.byref(s)))
         return {k: getattr(s, k) for k, _ in Stats._fields_}
+
+    def set_pipeline(self, pipeline: str) -> None:
+        """'auto' (the record pipeline where rows pack into 16-B records) or
+        'generic' (rk_set_pipeline)."""
+        _check(load_library().rk_set_pipeline(self._h, {"auto": 0, "generic": 1}[pipeline]))
 
     def set_profiling(self, on: bool = True) -> None:
         _check(load_library().rk_set_profiling(self._h, int(on)))

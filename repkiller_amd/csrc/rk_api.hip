@@ -37,7 +37,8 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_sort_small",    "k_sort_groups_reg", "k_sort_groups_lds", "k_sort_groups_split",
     "k_emit",          "k_part (sharded)", "exchange (sharded)", "k_aux (sharded)",
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
-    "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32",
+    "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32", "k_nw_order_hist",
+    "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign",
 };
 }  // namespace rk
 
@@ -252,7 +253,16 @@ rk::SweepScratch sweep_scratch(const Work &w) {
 // second grow-only buffer, so the common case does not carry 36 B per entry.
 int ensure_wide(rk_ctx *ctx, size_t n1, Work &w) {
   const size_t n = n1 + 1;
-  const size_t need = rk::align_up(4 * n) + 4 * rk::align_up(8 * n);
+  auto carve_wide = [&](Carve &c) {
+    w.p.ylenhi = c.take<uint32_t>(n);
+    w.cx.cen = c.take<uint64_t>(n);
+    w.cx.len = c.take<uint64_t>(n);
+    w.cy.cen = c.take<uint64_t>(n);
+    w.cy.len = c.take<uint64_t>(n);
+  };
+  Carve probe{nullptr};
+  carve_wide(probe);
+  const size_t need = probe.off;  // with take()'s slack
   if (need > ctx->ws_wide_cap) {
     if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
     ctx->ws_wide = nullptr;
@@ -265,11 +275,7 @@ int ensure_wide(rk_ctx *ctx, size_t n1, Work &w) {
     ctx->ws_wide_cap = need;
   }
   Carve c{(char *)ctx->ws_wide};
-  w.p.ylenhi = c.take<uint32_t>(n);
-  w.cx.cen = c.take<uint64_t>(n);
-  w.cx.len = c.take<uint64_t>(n);
-  w.cy.cen = c.take<uint64_t>(n);
-  w.cy.len = c.take<uint64_t>(n);
+  carve_wide(c);
   return RK_OK;
 }
 
@@ -300,6 +306,239 @@ void collect_phases(rk_ctx *ctx) {
     }
   }
   for (auto &u : ctx->pev_used) u = false;
+}
+
+// ---------------------------------------------------------------------------
+// The record pipeline (rk_narrow.hip): used when every row packs into a
+// 16-B record; returns with *fallback set when the input turns out not to
+// (a length >= 2^24, a yStart >= 2^35, or an X chunk denser than its LDS
+// capacity) -- the generic pipeline then classifies from scratch.
+struct NWork {
+  uint32_t *ctrl, *ahist, *yhist, *ehist;
+  uint32_t *astatus, *ystatus, *xstatus;
+  uint4 *Ra, *Rb, *yrec, *erec;
+  rk::Csr cx, cy;
+  uint8_t *xhit;
+  uint32_t *par, *isnew, *newrank, *sgid, *tag, *otag, *mrow, *goff;
+  uint64_t *reckey;
+  void *gsort;
+  uint32_t *rpend, *runs, *rlen_at, *rbeg_at;
+  uint8_t *wpend;
+  uint32_t *scan;
+  size_t scan_cap;
+};
+
+size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
+  const size_t n = n1 + 1;
+  const size_t sw = rk::nw_status_words((uint32_t)n);
+  w.ctrl = c.take<uint32_t>(64 + rk::PEND_WORDS);
+  w.ahist = c.take<uint32_t>(3 * 4096);
+  w.yhist = w.ahist + 4096;
+  w.ehist = w.ahist + 8192;
+  w.astatus = c.take<uint32_t>(sw);
+  w.ystatus = c.take<uint32_t>(sw);
+  w.xstatus = c.take<uint32_t>((size_t)(nbx / 128 + 2) * 2 + 64);
+  w.Ra = c.take<uint4>(n);
+  w.Rb = c.take<uint4>(n);
+  w.yrec = c.take<uint4>(n);
+  w.erec = c.take<uint4>(n);
+  for (rk::Csr *cs : {&w.cx, &w.cy}) {
+    cs->key = c.take<uint32_t>(n);
+    cs->ent = c.take<uint32_t>(n);
+    cs->cen = cs->len = nullptr;
+    cs->state = c.take<uint8_t>(n);
+    cs->pk = c.take<uint2>(n);
+    cs->nbd = c.take<uint8_t>(n);
+  }
+  w.xhit = c.take<uint8_t>(n);
+  w.par = c.take<uint32_t>(n);
+  w.isnew = c.take<uint32_t>(n);
+  w.newrank = c.take<uint32_t>(n);
+  w.sgid = c.take<uint32_t>(n);
+  w.tag = c.take<uint32_t>(n);
+  w.otag = c.take<uint32_t>(n);
+  w.mrow = c.take<uint32_t>(n);
+  w.goff = c.take<uint32_t>(n);
+  w.reckey = c.take<uint64_t>(n);
+  w.gsort = c.take<uint8_t>(rk::groupsort_scratch_bytes((uint32_t)n));
+  w.rpend = c.take<uint32_t>(n / 4 + 1);
+  w.wpend = c.take<uint8_t>(n / 64 + 1);
+  w.runs = c.take<uint32_t>(rk::runs_scratch_words((uint32_t)n));
+  w.rlen_at = c.take<uint32_t>(n);
+  w.rbeg_at = c.take<uint32_t>(n);
+  w.scan_cap = rk::scan_blocks(n + 1) + 64;
+  w.scan = c.take<uint32_t>(w.scan_cap);
+  return c.off;
+}
+
+int ensure_nw(rk_ctx *ctx, uint64_t n, uint32_t nbx, NWork &w) {
+  Carve probe{nullptr};
+  const size_t need = carve_nw(probe, n, nbx, w);
+  if (need > ctx->ws_nw_cap) {
+    if (ctx->ws_nw) (void)hipFree(ctx->ws_nw);
+    ctx->ws_nw = nullptr;
+    ctx->ws_nw_cap = 0;
+    hipError_t e = hipMalloc(&ctx->ws_nw, need);
+    if (e == hipErrorOutOfMemory && (ctx->ws || ctx->ws_wide)) {
+      // the generic pipeline's buffers (a previous fallback) give way
+      (void)hipGetLastError();
+      if (ctx->ws) (void)hipFree(ctx->ws);
+      if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
+      ctx->ws = ctx->ws_wide = nullptr;
+      ctx->ws_cap = ctx->ws_wide_cap = 0;
+      e = hipMalloc(&ctx->ws_nw, need);
+    }
+    if (e != hipSuccess) {
+      ctx->err = std::string("record-pipeline workspace hipMalloc(") + std::to_string(need) +
+                 "): " + hipGetErrorString(e);
+      return e == hipErrorOutOfMemory ? RK_E_NOMEM : RK_E_HIP;
+    }
+    ctx->ws_nw_cap = need;
+  }
+  Carve real{(char *)ctx->ws_nw};
+  carve_nw(real, n, nbx, w);
+  return RK_OK;
+}
+
+// RK_RECORD_PIPELINE=0 forces the generic pipeline (A/B measurements)
+bool record_pipeline_enabled() {
+  static const bool on = [] {
+    const char *e = std::getenv("RK_RECORD_PIPELINE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, uint32_t npairs,
+                    rk_result *outs, const Plan &pl, bool *fallback) {
+  *fallback = false;
+  const uint32_t n = (uint32_t)pl.n;
+  NWork w{};
+  int rc = ensure_nw(ctx, pl.n, pl.nbx, w);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream, st2 = ctx->stream2;
+  rk::ScanScratch ss{w.scan, w.scan_cap};
+  ctx->stats.n_in = n;
+  const rk::NwDigits ad = rk::nw_plan(rk::bit_length(pl.vsize - 1));
+  const rk::NwDigits yd = rk::nw_plan(rk::bit_length(2ull * pl.nby - 1));
+
+  HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
+  HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));
+  HIPCHK(ctx, hipMemsetAsync(w.ahist, 0, 3 * 4096 * sizeof(uint32_t), st));
+  mark(ctx, RK_PH_PREP);
+  rk::nw_order_hist(*in, pl.vsize, ad, w.ahist, w.ctrl, st);
+  mark(ctx, RK_PH_ORDER);
+  rk::nw_order_sort(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, ad, yd, w.ahist, w.yhist,
+                    w.astatus, w.Ra, w.Rb, w.yrec, w.ctrl, st);
+  HIPCHK(ctx, hipGetLastError());
+  if ((rc = readback(ctx, w.ctrl, 9))) return rc;
+  if ((rc = err_status(ctx, ctx->host[0]))) return rc;
+  if (ctx->host[3]) {  // some row does not pack into a record
+    *fallback = true;
+    ctx->stats.record_fallback = 1;
+    return RK_OK;
+  }
+  const uint32_t m = ctx->host[1], maxlen = ctx->host[4], M0 = ctx->host[8];
+  ctx->stats.n_proc = m;
+  for (uint32_t q = 0; q < npairs; ++q) outs[q].n_out = m, outs[q].n_groups = 0;
+  if (m == 0) {
+    mark(ctx, RK_N_PHASES);
+    collect_phases(ctx);
+    HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    return RK_OK;
+  }
+  // the Y axis sorts on the second stream while the X axis is built and resolved
+  HIPCHK(ctx, hipEventRecord(ctx->fork, st));
+  HIPCHK(ctx, hipStreamWaitEvent(st2, ctx->fork, 0));
+  rk::nw_y_sort(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y, st2);
+  HIPCHK(ctx, hipEventRecord(ctx->join, st2));
+  mark(ctx, RK_PH_GATHER);
+  rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, M0, w.cx, w.erec, w.xstatus, w.ctrl,
+                  rk::nw_chunk_width(m, pl.nbx), st);
+  HIPCHK(ctx, hipGetLastError());
+  if ((rc = readback(ctx, w.ctrl + 6, 2))) return rc;
+  const bool narrow_keys = ctx->host[0] == 0;
+  if (ctx->host[1]) {  // an X bucket above a chunk's LDS capacity
+    HIPCHK(ctx, hipStreamSynchronize(st2));
+    *fallback = true;
+    ctx->stats.record_fallback = 2;
+    return RK_OK;
+  }
+  mark(ctx, RK_PH_OCC_CSR);
+  rk::SweepScratch sc{w.runs, w.wpend, reinterpret_cast<uint8_t *>(w.rpend), w.ctrl + 64,
+                      w.ctrl + 2};
+  for (uint32_t q = 0; q < npairs; ++q) {
+    const rk_params &pq = prms[q];
+    rk_result *out = &outs[q];
+    const bool prof = q == 0;
+    if (q > 0) HIPCHK(ctx, hipMemsetAsync(w.cx.state, rk::ST_UNKNOWN, m, st));
+    if (prof) mark(ctx, RK_PH_SWEEP_X);
+    rk::Axis ax{w.cx.key, w.cx.ent, nullptr, nullptr, w.cx.state, nullptr, w.xhit, w.par,
+                w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
+                pq.pos_ratio};
+    uint32_t sweeps = 0;
+    if ((rc = rk::resolve_axis(ctx, ax, sc, true, &sweeps))) return rc;
+    ctx->stats.x_sweeps = sweeps;
+    if (prof) mark(ctx, RK_PH_SWEEP_Y);
+    if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
+    rk::nw_fill_y(w.cy.ent, w.xhit, w.cy.state, m, st);
+    rk::Axis ay{w.cy.key, w.cy.ent, nullptr, nullptr, w.cy.state, nullptr, nullptr, w.par,
+                w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
+                pq.pos_ratio};
+    if ((rc = rk::resolve_axis(ctx, ay, sc, true, &sweeps))) return rc;
+    ctx->stats.y_sweeps = sweeps;
+
+    // group roots and ids
+    if (prof) mark(ctx, RK_PH_ROOTS);
+    rk::Proc pr{};
+    pr.par = w.par;
+    HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
+    uint32_t rounds = 0;
+    for (;;) {
+      HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
+      rk::jump_round(pr, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st);
+      if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
+      ++rounds;
+      if (!ctx->host[0]) break;
+      if (rounds > 64) {
+        ctx->err = "pointer jumping did not converge";
+        return RK_E_INTERNAL;
+      }
+    }
+    ctx->stats.jump_rounds = rounds;
+    rk::exclusive_scan_u32(w.isnew, w.newrank, (size_t)m + 1, ss, st);
+    if ((rc = readback(ctx, w.newrank + m, 1))) return rc;
+    const uint32_t G = ctx->host[0];
+    out->n_groups = G;
+    ctx->stats.n_groups = G;
+    const rk::NwDigits ed = rk::nw_plan(rk::bit_length(G ? G - 1 : 0));
+    HIPCHK(ctx, hipMemsetAsync(w.ehist, 0, 4096 * sizeof(uint32_t), st));
+    rk::nw_assign(w.par, w.newrank, w.erec, m, ed, w.ehist, st);
+
+    // members (stable by gid => processing order), in-group order, flags
+    if (prof) mark(ctx, RK_PH_MEMBERS);
+    rk::nw_member_sort(w.erec, w.Ra, w.Rb, m, ed, w.ehist, w.astatus, w.sgid, w.reckey, w.tag,
+                       w.mrow, st);
+    rk::group_offsets(w.sgid, m, G, w.goff, st);
+    if (prof) mark(ctx, RK_PH_GROUP_SORT);
+    rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
+                          ctx->host + 128, narrow_keys, st, st2, ctx->fork, ctx->join);
+    if (prof) mark(ctx, RK_PH_EMIT);
+    rk::emit_result(w.otag, w.sgid, w.goff, w.mrow, m, out->gid, out->repval, out->out_order,
+                    st);
+    HIPCHK(ctx, hipGetLastError());
+    if (prof) mark(ctx, RK_N_PHASES);
+  }
+  HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
+  if ((rc = readback(ctx, w.ctrl, 1))) return rc;
+  collect_phases(ctx);
+  if ((rc = err_status(ctx, ctx->host[0]))) return rc;
+  float ms = 0;
+  HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->stats.device_ms = ms;
+  ctx->stats.pipeline = 1;
+  return RK_OK;
 }
 
 // All pairs share one fragment set: the ratio-independent part (processing
@@ -342,8 +581,24 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   }
   pl.nbx = (uint32_t)(pl.max_x + 1);
   pl.nby = (uint32_t)(pl.max_y + 1);
+  int rc;
+  if (ctx->pipeline == RK_PIPELINE_AUTO && record_pipeline_enabled() && pl.n > 0 &&
+      pl.n < (1ull << 30)) {
+    bool fallback = false;
+    rc = classify_narrow(ctx, in, prms, npairs, outs, pl, &fallback);
+    if (rc || !fallback) return rc;
+    // the generic pipeline needs its own ~200 B per row: give the HBM back
+    (void)hipStreamSynchronize(ctx->stream2);
+    (void)hipFree(ctx->ws_nw);
+    ctx->ws_nw = nullptr;
+    ctx->ws_nw_cap = 0;
+    if (ctx->profiling) ctx->kt.n = 0;  // the timings of the abandoned attempt
+    const uint32_t why = ctx->stats.record_fallback;
+    std::memset(&ctx->stats, 0, sizeof ctx->stats);
+    ctx->stats.record_fallback = why;
+  }
   Work w{};  // value-initialised: optional Proc columns (grow, ...) stay null
-  int rc = ensure_ws(ctx, pl, w);
+  rc = ensure_ws(ctx, pl, w);
   if (rc) return rc;
   const uint32_t n = (uint32_t)pl.n;
   rk::ScanScratch ss{w.scan, w.scan_cap};
@@ -404,7 +659,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (prof) mark(ctx, RK_PH_SWEEP_X);
     // X decisions write X results into the Y records and X hits' parents
     rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state,
-                reinterpret_cast<uint32_t *>(w.p.yrec), w.p.par,
+                reinterpret_cast<uint32_t *>(w.p.yrec), nullptr, w.p.par,
                 w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
                 pq.pos_ratio};
     uint32_t sweeps = 0;
@@ -414,7 +669,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
     rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, pl.max_y, st);
     // X misses: the Y sweeps write parent = Y winner, or itself (new group)
-    rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, nullptr, w.p.par,
+    rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, nullptr, nullptr, w.p.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
     if ((rc = rk::resolve_axis(ctx, ay, sweep_scratch(w), fast32, &sweeps))) return rc;
@@ -466,6 +721,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   float ms = 0;
   HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->stats.device_ms = ms;
+  ctx->stats.pipeline = 2;
   return RK_OK;
 }
 
@@ -524,6 +780,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->io) (void)hipFree(ctx->io);
   if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
+  if (ctx->ws_nw) (void)hipFree(ctx->ws_nw);
   for (void *p : ctx->pool.ptr)
     if (p) (void)hipFree(p);
   if (ctx->host) (void)hipHostFree(ctx->host);
@@ -583,6 +840,12 @@ extern "C" int rk_reset_phases(rk_ctx *ctx) {
 
 extern "C" const char *rk_phase_name(int phase) {
   return phase >= 0 && phase < RK_N_PHASES ? kPhaseNames[phase] : "";
+}
+
+extern "C" int rk_set_pipeline(rk_ctx *ctx, int pipeline) {
+  if (!ctx || (pipeline != RK_PIPELINE_AUTO && pipeline != RK_PIPELINE_GENERIC)) return RK_E_ARG;
+  ctx->pipeline = pipeline;
+  return RK_OK;
 }
 
 extern "C" int rk_get_stats(const rk_ctx *ctx, rk_stats *st) {

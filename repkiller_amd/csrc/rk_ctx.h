@@ -29,6 +29,9 @@ struct rk_ctx {
   size_t ws_cap = 0;
   void *ws_wide = nullptr;  // 64-bit length columns, only when a length is >= 2^31
   size_t ws_wide_cap = 0;
+  int pipeline = RK_PIPELINE_AUTO;
+  void *ws_nw = nullptr;  // workspace of the record pipeline (rk_narrow.hip)
+  size_t ws_nw_cap = 0;
   uint32_t *host = nullptr;  // pinned readback words
   // device copies for rk_classify (host-buffer entry point)
   void *io = nullptr;

@@ -71,7 +71,9 @@ __global__ void k_prep_keys(Frags f, uint64_t vsize, uint64_t max_x, uint64_t ma
     const uint32_t t = part[0] + part[1] + part[2] + part[3];
     if (t) atomicAdd(kept, t);
   }
-  if ((threadIdx.x & 63) == 0 && __ballot(wide)) atomicOr(err, ERRB_WIDE_LENGTH);
+  // the ballot runs in every lane (inside `lane == 0 && ...` it would see lane 0 only)
+  const uint64_t any_wide = __ballot(wide);
+  if ((threadIdx.x & 63) == 0 && any_wide) atomicOr(err, ERRB_WIDE_LENGTH);
 }
 
 // Processing-order SoA and bucket keys (one 32-B record gather per row).

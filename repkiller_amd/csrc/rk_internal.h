@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/repkiller_amd.h"
+
 namespace rk {
 
 // per-fragment resolution state on one axis (X or Y occupancy lists)
@@ -56,7 +58,8 @@ enum KernelId : int {
   KID_SWEEP_TILE, KID_SWEEP_FAST, KID_SWEEP_MORE, KID_SWEEP_WAVE, KID_CSR_FILL_Y, KID_JUMP,
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
-  KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_COUNT
+  KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_NW_HIST,
+  KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 struct KernelTimer {
@@ -105,6 +108,8 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   uint8_t *state;      // ST_*
   uint32_t *xres;      // X axis only: the Y records as 32-bit words; word 4k+3 of
                        // entry k receives its X result (winner id, or NONE)
+  uint8_t *xhit;       // X axis, record pipeline (rk_narrow.hip): 1 = X hit, by processing
+                       // index (instead of xres)
   uint32_t *par;       // parent by processing index: X hits -> X winner; Y axis
                        // (X misses) -> Y winner, or itself for a new group
   const uint2 *pk;     // {centre low 32, length low 32}: the 32-bit sweep's record
@@ -216,5 +221,36 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
 void emit_result(const uint32_t *otag, const uint32_t *sgid, const uint32_t *goff,
                  const uint32_t *mrow, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st);
+
+// -------------------------------------------------------- rk_narrow.hip --
+// The record-carrying pipeline (16-B records, one-sweep radix sorts, X axis by
+// chunks of the processing order).  ctrl words: [0] error bits, [1] kept rows,
+// [3] not representable, [4] longest length, [6] wide sort keys, [7] X chunk
+// overflow, [8] forward-strand kept rows.
+struct NwDigits {
+  int passes;
+  int shift[4], db[4];
+};
+NwDigits nw_plan(int bits);
+size_t nw_status_words(uint32_t n);
+uint32_t nw_chunk_width(uint32_t m, uint32_t nbx);
+void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, const NwDigits &a, uint32_t *ghist,
+                   uint32_t *ctrl, hipStream_t st);
+void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
+                   uint32_t nby, const NwDigits &a, const NwDigits &y, const uint32_t *ghist,
+                   uint32_t *yhist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
+                   uint32_t *ctrl, hipStream_t st);
+void nw_y_sort(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y, const uint32_t *yhist,
+               uint32_t *status, Csr cy, uint32_t nby, uint64_t max_y, hipStream_t st);
+void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
+                 uint32_t M0, Csr cx, uint4 *erec, uint32_t *status, uint32_t *ctrl, uint32_t W,
+                 hipStream_t st);
+void nw_fill_y(const uint32_t *ent, const uint8_t *xhit, uint8_t *state, uint32_t m,
+               hipStream_t st);
+void nw_assign(const uint32_t *par, const uint32_t *newrank, uint4 *erec, uint32_t m,
+               const NwDigits &e, uint32_t *ehist, hipStream_t st);
+void nw_member_sort(const uint4 *erec, uint4 *t0, uint4 *t1, uint32_t m, const NwDigits &e,
+                    const uint32_t *ehist, uint32_t *status, uint32_t *sgid, uint64_t *key,
+                    uint32_t *tag, uint32_t *mrow, hipStream_t st);
 
 }  // namespace rk

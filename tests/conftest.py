@@ -40,3 +40,19 @@ def gpu_ctx():
     ctx = rk.Context(0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture(scope="session")
+def generic_ctx():
+    import repkiller_amd as rk
+    ctx = rk.Context(0)
+    ctx.set_pipeline("generic")
+    yield ctx
+    ctx.close()
+
+
+@pytest.fixture(params=["record", "generic"])
+def pctx(request, gpu_ctx, generic_ctx):
+    """Both device pipelines (the record pipeline where inputs pack into 16-B
+    records -- gpu_ctx's default -- and the generic one)."""
+    return gpu_ctx if request.param == "record" else generic_ctx

@@ -41,7 +41,7 @@ def gpu_vs_oracle(ctx, f, lx, ly, lr=0.3, pr=0.3):
 
 
 @pytest.mark.parametrize("name,case", edge_cases(), ids=[n for n, _ in edge_cases()])
-def test_edge_fixture(gpu_ctx, tmp_path, name, case):
+def test_edge_fixture(pctx, tmp_path, name, case):
     inp = os.path.join(EDGE, name + ".in.csv")
     if case["expect"] == "error:RK_E_COUNT":
         with pytest.raises(rk.RkError):
@@ -50,11 +50,11 @@ def test_edge_fixture(gpu_ctx, tmp_path, name, case):
     db = rk.FragmentsDatabase(inp)
     if case["expect"] != "ref":
         with pytest.raises(rk.RkError) as e:
-            gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, case["len_ratio"],
+            pctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, case["len_ratio"],
                              case["pos_ratio"])
         assert e.value.code == ERR[case["expect"]]
         return
-    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, case["len_ratio"],
+    res = pctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, case["len_ratio"],
                            case["pos_ratio"])
     out = tmp_path / "out.csv"
     db.save_all_frag_pairs(str(out), res)
@@ -62,12 +62,12 @@ def test_edge_fixture(gpu_ctx, tmp_path, name, case):
         assert out.read_bytes() == f.read()
 
 
-def test_corpus10k_csv(gpu_ctx, tmp_path):
+def test_corpus10k_csv(pctx, tmp_path):
     inp, out = tmp_path / "in.csv", tmp_path / "out.csv"
     with gzip.open(os.path.join(GOLDEN, "corpus10k.in.csv.gz"), "rb") as fi, open(inp, "wb") as fo:
         shutil.copyfileobj(fi, fo)
     db = rk.FragmentsDatabase(str(inp))
-    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr)
+    res = pctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr)
     db.save_all_frag_pairs(str(out), res)
     with gzip.open(os.path.join(GOLDEN, "corpus10k.out.csv.gz"), "rb") as f:
         assert out.read_bytes() == f.read()
@@ -75,9 +75,9 @@ def test_corpus10k_csv(gpu_ctx, tmp_path):
 
 @pytest.mark.parametrize("seed", [1, 11, 12])
 @pytest.mark.parametrize("lr,pr", [(0.3, 0.3), (0.05, 0.05), (1.5, 0.7), (0.3, 2.0)])
-def test_cfg1_vs_oracle(gpu_ctx, seed, lr, pr):
+def test_cfg1_vs_oracle(pctx, seed, lr, pr):
     f = rk.synth(10000, 1_000_000, seed=seed)
-    gpu_vs_oracle(gpu_ctx, f, 1_000_000, 1_000_000, lr, pr)
+    gpu_vs_oracle(pctx, f, 1_000_000, 1_000_000, lr, pr)
 
 
 @pytest.mark.parametrize("n,L,kw", [
@@ -86,9 +86,9 @@ def test_cfg1_vs_oracle(gpu_ctx, seed, lr, pr):
     (50_000, 200_000, dict(family_frac=0.95, copies=(100, 600))),  # very dense buckets
     (30_000, 100_000, {}),  # upward probes active over the first 1% (c < max_index)
 ])
-def test_synthetic_vs_oracle(gpu_ctx, n, L, kw):
+def test_synthetic_vs_oracle(pctx, n, L, kw):
     f = rk.synth(n, L, seed=21, **kw)
-    gpu_vs_oracle(gpu_ctx, f, L, L)
+    gpu_vs_oracle(pctx, f, L, L)
 
 
 with open(os.path.join(GOLDEN, "boundary_hashes.json")) as _f:
@@ -97,24 +97,24 @@ with open(os.path.join(GOLDEN, "boundary_hashes.json")) as _f:
 
 @pytest.mark.parametrize("runs_len", [70, 300, 2500])
 @pytest.mark.parametrize("lr,pr", [(0.05, 0.05), (0.3, 0.3), (1.5, 0.7)])
-def test_long_runs_vs_oracle(gpu_ctx, runs_len, lr, pr):
+def test_long_runs_vs_oracle(pctx, runs_len, lr, pr):
     """Bucket runs longer than 64 entries (the long-run sweep), including runs
     whose ACTIVE entries overflow its LDS lists."""
     f = long_run_set(runs_len, seed=runs_len)
-    gpu_vs_oracle(gpu_ctx, f, 10_000_000, 10_000_000, lr, pr)
+    gpu_vs_oracle(pctx, f, 10_000_000, 10_000_000, lr, pr)
 
 
 @pytest.mark.parametrize("lr,pr", bc.RATIOS)
-def test_deviation_boundaries(gpu_ctx, tmp_path, lr, pr):
+def test_deviation_boundaries(pctx, tmp_path, lr, pr):
     """sl == 0 / sp == 0 boundaries and NaN/inf/extreme ratios: bit-exact with
     the reference's own output (hash) and with the oracle."""
     f = bc.short_dense(rk)
     inp = str(tmp_path / "in.csv")
     rk.write_input_csv(inp, f, bc.GENOME, bc.GENOME)
     db = rk.FragmentsDatabase(inp)
-    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, float(lr), float(pr))
+    res = pctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, float(lr), float(pr))
     assert sha256_csv(db, res, str(tmp_path / "out.csv")) == BOUNDARY["outputs"][f"{lr},{pr}"]
-    gpu_vs_oracle(gpu_ctx, f, bc.GENOME, bc.GENOME, float(lr), float(pr))
+    gpu_vs_oracle(pctx, f, bc.GENOME, bc.GENOME, float(lr), float(pr))
 
 
 def test_wide_lengths_generic_sweep(gpu_ctx):
@@ -145,14 +145,14 @@ def test_wide_lengths_long_runs(gpu_ctx, lr, pr):
     gpu_vs_oracle(gpu_ctx, g, 5_000_000_000, 5_000_000_000, lr, pr)
 
 
-def test_empty_and_tiny(gpu_ctx):
+def test_empty_and_tiny(pctx):
     f = rk.Frags(np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint64),
                  np.zeros(0, np.uint8))
-    r = gpu_ctx.classify(f, 1000, 1000)
+    r = pctx.classify(f, 1000, 1000)
     assert r.n_groups == 0 and r.out_order.size == 0
     f = rk.Frags(np.array([10], np.uint64), np.array([20], np.uint64), np.array([30], np.uint64),
                  np.array([ord('f')], np.uint8))
-    gpu_vs_oracle(gpu_ctx, f, 1000, 1000)
+    gpu_vs_oracle(pctx, f, 1000, 1000)
 
 
 def sha256_csv(db, res, path):
@@ -169,7 +169,7 @@ with open(os.path.join(GOLDEN, "hashes.json")) as _f:
 
 
 @pytest.mark.parametrize("key", sorted(HASHES))
-def test_1M_reference_hash(gpu_ctx, tmp_path, key):
+def test_1M_reference_hash(pctx, tmp_path, key):
     h = HASHES[key]
     kw = dict(h["synth"])
     if "copies" in kw:
@@ -181,7 +181,7 @@ def test_1M_reference_hash(gpu_ctx, tmp_path, key):
     with open(inp, "rb") as fh:
         assert hashlib.sha256(fh.read()).hexdigest() == h["input_sha256"]
     db = rk.FragmentsDatabase(inp)
-    res = gpu_ctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, h["len_ratio"], h["pos_ratio"])
+    res = pctx.classify(db.frags, db.len_x_hdr, db.len_y_hdr, h["len_ratio"], h["pos_ratio"])
     assert sha256_csv(db, res, str(tmp_path / "out.csv")) == h["output_sha256"]
 
 
@@ -205,13 +205,13 @@ def test_classify_device_torch(gpu_ctx):
     assert np.array_equal(order[:n_out].cpu().numpy().view(np.uint32), o2)
 
 
-def test_repeat_calls_same_context(gpu_ctx):
+def test_repeat_calls_same_context(pctx):
     """Workspace reuse across sizes must not leak state between calls."""
     a = rk.synth(20_000, 2_000_000, seed=31)
     b = rk.synth(3_000, 300_000, seed=32)
-    r1 = gpu_vs_oracle(gpu_ctx, a, 2_000_000, 2_000_000)
-    gpu_vs_oracle(gpu_ctx, b, 300_000, 300_000)
-    r3 = gpu_ctx.classify(a, 2_000_000, 2_000_000)
+    r1 = gpu_vs_oracle(pctx, a, 2_000_000, 2_000_000)
+    gpu_vs_oracle(pctx, b, 300_000, 300_000)
+    r3 = pctx.classify(a, 2_000_000, 2_000_000)
     assert np.array_equal(r1.out_order, r3.out_order)
 
 
@@ -222,11 +222,11 @@ PAIRS = [(0.3, 0.3), (0.05, 0.05), (1.5, 0.7), (0.3, 2.0), (float("nan"), 0.3), 
     (200_000, 10_000_000, {}),
     (50_000, 200_000, dict(family_frac=0.95, copies=(100, 600))),
 ])
-def test_classify_pairs_vs_oracle(gpu_ctx, n, L, kw):
+def test_classify_pairs_vs_oracle(pctx, n, L, kw):
     """rk_classify_pairs: the shared prefix is built once and every pair's
     result equals the oracle's for that pair alone (repkiller.cpp:60-72)."""
     f = rk.synth(n, L, seed=23, **kw)
-    got = gpu_ctx.classify_pairs(f, L, L, PAIRS)
+    got = pctx.classify_pairs(f, L, L, PAIRS)
     assert len(got) == len(PAIRS)
     for (lr, pr), r in zip(PAIRS, got):
         rc, gid, rep, order, ng = ro.classify(f.x_start, f.y_start, f.length, f.strand, L, L,
@@ -311,3 +311,47 @@ def test_std_sort_large_segments_vs_restatement(gpu_ctx):
     for a, b, s in zip(off[:-1], off[1:], segs):
         want = ro.std_sort(s) + a
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
+
+
+def test_pipeline_choice(gpu_ctx, generic_ctx):
+    """The record pipeline runs on the BASELINE-shaped sets; inputs it cannot
+    represent (a length >= 2^24) take the generic one with the same result."""
+    f = rk.synth(20_000, 2_000_000, seed=61)
+    gpu_vs_oracle(gpu_ctx, f, 2_000_000, 2_000_000)
+    assert gpu_ctx.stats()["pipeline"] == 1
+    gpu_vs_oracle(generic_ctx, f, 2_000_000, 2_000_000)
+    assert generic_ctx.stats()["pipeline"] == 2
+    g = rk.synth(20_000, 50_000_000, seed=62)
+    g.length[777] = np.uint64(1 << 24)  # not a record: generic pipeline
+    gpu_vs_oracle(gpu_ctx, g, 50_000_000, 50_000_000)
+    assert gpu_ctx.stats()["pipeline"] == 2
+
+
+def test_dense_x_chunks(gpu_ctx):
+    """X chunks denser than their LDS list are placed bin range by bin range
+    (record pipeline); a single 100-bp bucket of one strand above the list
+    capacity hands the classification to the generic pipeline -- same output
+    either way."""
+    L = 30_000
+    f = rk.synth(60_000, L, seed=63, family_frac=0.95, copies=(100, 600))
+    gpu_vs_oracle(gpu_ctx, f, L, L)
+    st = gpu_ctx.stats()
+    assert st["pipeline"] == 1 and st["record_fallback"] == 0
+    rng = np.random.default_rng(65)
+    k = 3000  # one bucket, one strand: more entries than a chunk's list holds
+    g = rk.Frags(np.concatenate([f.x_start, np.full(k, 5000, np.uint64)]),
+                 np.concatenate([f.y_start, rng.integers(1, 20_000, k).astype(np.uint64)]),
+                 np.concatenate([f.length, rng.integers(90, 110, k).astype(np.uint64)]),
+                 np.concatenate([f.strand, np.full(k, ord("f"), np.uint8)]))
+    gpu_vs_oracle(gpu_ctx, g, L, L)
+    st = gpu_ctx.stats()
+    assert st["pipeline"] == 2 and st["record_fallback"] == 2
+
+
+@pytest.mark.parametrize("pos", [1, 63, 65, 1000, 19_999])
+def test_wide_length_detected_in_any_lane(pctx, pos):
+    """A single length >= 2^31 at any row position switches to the 64-bit
+    sweep (the device flag is a wave-wide ballot)."""
+    f = rk.synth(20_000, 1_000_000, seed=64)
+    f.length[pos] = np.uint64(2**31 + 3)
+    gpu_vs_oracle(pctx, f, 5_000_000_000, 5_000_000_000)
