@@ -92,8 +92,7 @@ typedef struct {
   double device_ms; /* HIP-event time of the whole device pipeline */
   uint32_t pipeline; /* the pipeline that produced the result: 1 record, 2 generic */
   uint32_t record_fallback; /* why the record pipeline handed over: 0 it did not, 1 a row
-                               does not pack into a record, 2 an X bucket denser than a
-                               chunk's LDS list */
+                               does not pack into a record */
 } rk_stats;
 
 int rk_create(rk_ctx **ctx, int device);

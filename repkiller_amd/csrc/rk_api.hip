@@ -38,7 +38,7 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_emit",          "k_part (sharded)", "exchange (sharded)", "k_aux (sharded)",
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
     "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32", "k_nw_order_hist",
-    "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign",
+    "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign", "k_nw_xcount",
 };
 }  // namespace rk
 
@@ -315,7 +315,7 @@ void collect_phases(rk_ctx *ctx) {
 // capacity) -- the generic pipeline then classifies from scratch.
 struct NWork {
   uint32_t *ctrl, *ahist, *yhist, *ehist;
-  uint32_t *astatus, *ystatus, *xstatus;
+  uint32_t *astatus, *ystatus, *xcnt, *xoff;
   uint4 *Ra, *Rb, *yrec, *erec;
   rk::Csr cx, cy;
   uint8_t *xhit;
@@ -337,7 +337,9 @@ size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
   w.ehist = w.ahist + 8192;
   w.astatus = c.take<uint32_t>(sw);
   w.ystatus = c.take<uint32_t>(sw);
-  w.xstatus = c.take<uint32_t>((size_t)(nbx / 128 + 2) * 2 + 64);
+  // X-chunk counts and their scan (chunks of >= 64 buckets)
+  w.xcnt = c.take<uint32_t>((size_t)3 * (nbx / 64 + 2) + 64);
+  w.xoff = c.take<uint32_t>((size_t)3 * (nbx / 64 + 2) + 64);
   w.Ra = c.take<uint4>(n);
   w.Rb = c.take<uint4>(n);
   w.yrec = c.take<uint4>(n);
@@ -426,10 +428,8 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));
   HIPCHK(ctx, hipMemsetAsync(w.ahist, 0, 3 * 4096 * sizeof(uint32_t), st));
   mark(ctx, RK_PH_PREP);
-  rk::nw_order_hist(*in, pl.vsize, ad, w.ahist, w.ctrl, st);
-  mark(ctx, RK_PH_ORDER);
-  rk::nw_order_sort(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, ad, yd, w.ahist, w.yhist,
-                    w.astatus, w.Ra, w.Rb, w.yrec, w.ctrl, st);
+  rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, ad, yd, w.ahist, w.yhist, w.ctrl,
+                    st);
   HIPCHK(ctx, hipGetLastError());
   if ((rc = readback(ctx, w.ctrl, 9))) return rc;
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
@@ -438,7 +438,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     ctx->stats.record_fallback = 1;
     return RK_OK;
   }
-  const uint32_t m = ctx->host[1], maxlen = ctx->host[4], M0 = ctx->host[8];
+  const uint32_t m = ctx->host[1], maxlen = ctx->host[4];
   ctx->stats.n_proc = m;
   for (uint32_t q = 0; q < npairs; ++q) outs[q].n_out = m, outs[q].n_groups = 0;
   if (m == 0) {
@@ -448,23 +448,26 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     HIPCHK(ctx, hipStreamSynchronize(st));
     return RK_OK;
   }
+  // X chunks: entries per (strand, chunk) and owned rows per chunk, counted
+  // over the processing order; one scan turns the counts into offsets
+  rk::NwChunkCounts cc{};
+  cc.W = rk::nw_chunk_width(m, pl.nbx);
+  while ((1u << cc.lgW) < cc.W) ++cc.lgW;
+  cc.nch = rk::nw_chunks(pl.nbx, cc.W);
+  cc.cnts = w.xcnt;
+  mark(ctx, RK_PH_ORDER);
+  rk::nw_order_sort(*in, pl.vsize, pl.nby, ad, w.ahist, w.astatus, w.Ra, w.Rb, w.yrec, st);
+  rk::nw_x_count(w.Ra, m, cc, st);
+  rk::exclusive_scan_u32(w.xcnt, w.xoff, (size_t)3 * cc.nch + 1, ss, st);
+  HIPCHK(ctx, hipGetLastError());
   // the Y axis sorts on the second stream while the X axis is built and resolved
   HIPCHK(ctx, hipEventRecord(ctx->fork, st));
   HIPCHK(ctx, hipStreamWaitEvent(st2, ctx->fork, 0));
   rk::nw_y_sort(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y, st2);
   HIPCHK(ctx, hipEventRecord(ctx->join, st2));
   mark(ctx, RK_PH_GATHER);
-  rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, M0, w.cx, w.erec, w.xstatus, w.ctrl,
-                  rk::nw_chunk_width(m, pl.nbx), st);
+  rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, w.xoff, w.cx, w.erec, w.ctrl, cc.W, st);
   HIPCHK(ctx, hipGetLastError());
-  if ((rc = readback(ctx, w.ctrl + 6, 2))) return rc;
-  const bool narrow_keys = ctx->host[0] == 0;
-  if (ctx->host[1]) {  // an X bucket above a chunk's LDS capacity
-    HIPCHK(ctx, hipStreamSynchronize(st2));
-    *fallback = true;
-    ctx->stats.record_fallback = 2;
-    return RK_OK;
-  }
   mark(ctx, RK_PH_OCC_CSR);
   rk::SweepScratch sc{w.runs, w.wpend, reinterpret_cast<uint8_t *>(w.rpend), w.ctrl + 64,
                       w.ctrl + 2};
@@ -493,13 +496,15 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (prof) mark(ctx, RK_PH_ROOTS);
     rk::Proc pr{};
     pr.par = w.par;
+    bool narrow_keys = true;
     HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
     uint32_t rounds = 0;
     for (;;) {
       HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
       rk::jump_round(pr, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st);
-      if ((rc = readback(ctx, w.ctrl + 5, 1))) return rc;
+      if ((rc = readback(ctx, w.ctrl + 5, 2))) return rc;  // + the wide-key flag
       ++rounds;
+      narrow_keys = ctx->host[1] == 0;
       if (!ctx->host[0]) break;
       if (rounds > 64) {
         ctx->err = "pointer jumping did not converge";
@@ -538,6 +543,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->stats.device_ms = ms;
   ctx->stats.pipeline = 1;
+  rk::nw_trace_dump(st);
   return RK_OK;
 }
 

@@ -59,7 +59,7 @@ enum KernelId : int {
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
   KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_NW_HIST,
-  KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_COUNT
+  KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 struct KernelTimer {
@@ -225,25 +225,33 @@ void emit_result(const uint32_t *otag, const uint32_t *sgid, const uint32_t *gof
 // -------------------------------------------------------- rk_narrow.hip --
 // The record-carrying pipeline (16-B records, one-sweep radix sorts, X axis by
 // chunks of the processing order).  ctrl words: [0] error bits, [1] kept rows,
-// [3] not representable, [4] longest length, [6] wide sort keys, [7] X chunk
-// overflow, [8] forward-strand kept rows.
+// [3] not representable, [4] longest length, [6] wide sort keys, [8]
+// forward-strand kept rows.
 struct NwDigits {
   int passes;
   int shift[4], db[4];
 };
 NwDigits nw_plan(int bits);
+void nw_trace_dump(hipStream_t st);  // RK_NW_TRACE (measurement only)
 size_t nw_status_words(uint32_t n);
 uint32_t nw_chunk_width(uint32_t m, uint32_t nbx);
-void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, const NwDigits &a, uint32_t *ghist,
-                   uint32_t *ctrl, hipStream_t st);
-void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
-                   uint32_t nby, const NwDigits &a, const NwDigits &y, const uint32_t *ghist,
-                   uint32_t *yhist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
-                   uint32_t *ctrl, hipStream_t st);
+uint32_t nw_chunks(uint32_t nbx, uint32_t W);
+// the X-chunk counts (3 nch + 1 words: entries per strand and chunk, owned rows per chunk)
+struct NwChunkCounts {
+  uint32_t W, lgW, nch;
+  uint32_t *cnts;
+};
+void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
+                   uint32_t nby, const NwDigits &a, const NwDigits &y, uint32_t *ghist,
+                   uint32_t *yhist, uint32_t *ctrl, hipStream_t st);
+void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
+                   const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
+                   hipStream_t st);
+void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st);
 void nw_y_sort(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y, const uint32_t *yhist,
                uint32_t *status, Csr cy, uint32_t nby, uint64_t max_y, hipStream_t st);
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
-                 uint32_t M0, Csr cx, uint4 *erec, uint32_t *status, uint32_t *ctrl, uint32_t W,
+                 const uint32_t *xoff, Csr cx, uint4 *erec, uint32_t *ctrl, uint32_t W,
                  hipStream_t st);
 void nw_fill_y(const uint32_t *ent, const uint8_t *xhit, uint8_t *state, uint32_t m,
                hipStream_t st);

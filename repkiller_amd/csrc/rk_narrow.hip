@@ -33,6 +33,10 @@
 //     byte per fragment (xhit);
 //   * group members {gid, row, sort key} are sorted by gid with the records
 //     carried, straight into the arrays the in-group sort reads.
+#include <cstdio>
+#include <cstdlib>
+#include <utility>
+
 #include "rk_ctx.h"
 
 namespace rk {
@@ -53,15 +57,34 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 // through that tile, stop), then publish this tile's inclusive prefix.  Tile
 // ids come from an atomic counter in dispatch order, so every earlier tile is
 // resident or done and publishes its AGG before it waits on anything.
+// The walk reads LB_BATCH predecessors per round trip: with hundreds of tiles
+// resident, the nearest INC is often hundreds of tiles back, and one
+// dependent load per tile made the look-back the slowest part of a pass.
+constexpr uint32_t LB_BATCH = 32;
 __device__ __forceinline__ uint32_t look_back(uint32_t *status, uint32_t tile, uint32_t stride,
                                               uint32_t slot, uint32_t mine) {
   uint32_t acc = 0;
-  for (uint32_t j = tile; j-- > 0;) {
-    uint32_t v;
-    while (((v = sw_load(&status[(size_t)j * stride + slot])) & ~SW_VAL) == 0)
-      __builtin_amdgcn_s_sleep(1);
-    acc += v & SW_VAL;
-    if ((v & ~SW_VAL) == SW_INC) break;
+  uint32_t j = tile;  // tiles [0, j) not yet accounted for
+  while (j > 0) {
+    const uint32_t cnt = j < LB_BATCH ? j : LB_BATCH;
+    uint32_t v[LB_BATCH];
+#pragma unroll
+    for (uint32_t k = 0; k < LB_BATCH; ++k)
+      v[k] = k < cnt ? sw_load(&status[(size_t)(j - 1 - k) * stride + slot]) : 0u;
+    uint32_t k = 0;
+    bool done = false;
+#pragma unroll
+    for (uint32_t q = 0; q < LB_BATCH; ++q) {
+      if (done || q != k || q >= cnt) continue;
+      const uint32_t f = v[q] & ~SW_VAL;
+      if (f == 0) continue;  // not published yet: poll again from here
+      acc += v[q] & SW_VAL;
+      ++k;
+      done = f == SW_INC;
+    }
+    if (done) break;
+    j -= k;
+    if (k < cnt) __builtin_amdgcn_s_sleep(1);
   }
   sw_store(&status[(size_t)tile * stride + slot], SW_INC | (acc + mine));
   return acc;
@@ -122,238 +145,244 @@ __device__ __forceinline__ void hist_flush(HistLds &L, const Digits &D, uint32_t
 }
 
 // ---------------------------------------------------------------------------
-// One LSD pass: tile = T threads x ITEMS records; wave w ranks its contiguous
-// slice (ITEMS rounds of 64) against a wave-private digit counter by DB
-// ballots (index order = rank order: stable), one barrier turns the counts
-// into tile-local starts, the look-back gives the tile's global start per
-// digit, the records are placed in LDS at their sorted slot and written out
-// slot by slot (consecutive lanes -> consecutive addresses of one segment).
-// Src: load(i, thr) -> record i (and folds per-thread side data into thr),
-// key(rec); Dst: store(pos, rec); Side: extra per-block work on every loaded
-// record (histograms of a later sort, flags), flushed at the end.
-struct NoSide {
-  struct Lds {
-    uint32_t unused;
-  };
-  struct Thr {};
-  __device__ void init(Lds &) const {}
-  __device__ void add(Lds &, const uint4 &, Thr &) const {}
-  __device__ void flush(Lds &, Thr &) const {}
-};
-
-template <int T, int ITEMS, int DB, class Src, class Dst, class Side>
-__global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, Side side, uint32_t n, int shift,
-                                                const uint32_t *__restrict__ ghist,
+// One LSD pass, persistent: each block claims tiles (T threads x ITEMS
+// records) from an atomic counter in dispatch order and, per tile:
+//   1 ranks its records (held in registers) -- wave w ranks its contiguous
+//     slice, ITEMS rounds of 64, against a wave-private digit counter by DB
+//     ballots (index order = rank order: stable);
+//   2 publishes the tile's digit counts for the look-back, turns the counts
+//     into tile-local starts and places the records at their sorted LDS slot;
+//   3 issues the loads of its NEXT tile, then walks the look-back (the global
+//     start of each digit in this tile) -- the next tile's loads are in
+//     flight during the look-back, whose cross-CU round trips (~2-5 us each
+//     under streaming load) made it half of a tile's time when every tile
+//     was its own block;
+//   4 writes the tile out slot by slot (consecutive lanes -> consecutive
+//     addresses of one digit segment).
+// Deadlock-free: a block holds at most its current tile and the claimed next
+// one, and a tile's look-back only waits for smaller tiles, each of which is
+// held by a running block that publishes it without waiting for larger ones.
+// Src: load(i) -> record i, key(rec); Dst: store(pos, rec).
+template <int T, int ITEMS, int DB, bool PERSIST, class Src, class Dst>
+__global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, uint32_t tiles,
+                                                int shift, const uint32_t *__restrict__ ghist,
                                                 uint32_t *__restrict__ status,
-                                                uint32_t *__restrict__ tile_ctr) {
+                                                uint32_t *__restrict__ tile_ctr,
+                                                uint64_t *__restrict__ trace) {
   constexpr int RADIX = 1 << DB, NW = T / 64, TILE = T * ITEMS, DPT = RADIX / T;
   static_assert(RADIX % T == 0, "whole digits per thread");
   __shared__ uint4 srec[TILE];
   __shared__ uint32_t wcnt[NW][RADIX];  // per-wave digit counters, then per-wave starts
   __shared__ uint32_t lbase[RADIX];     // tile-local start of digit d
+  __shared__ uint32_t gbase[RADIX];     // global start of digit d (all tiles)
   __shared__ uint32_t gpos[RADIX];      // global position of the tile's first digit-d record
-  __shared__ uint32_t wsum[2][NW];
-  __shared__ uint32_t s_tile;
-  __shared__ typename Side::Lds sl;
+  __shared__ uint32_t wsum[NW];
+  __shared__ uint32_t s_tile[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
-  if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
-  for (uint32_t j = threadIdx.x; j < NW * RADIX; j += T) (&wcnt[0][0])[j] = 0;
-  side.init(sl);
+  if (threadIdx.x == 0) s_tile[0] = atomicAdd(tile_ctr, 1u);
+  // the digits' global starts: exclusive scan of the pass histogram
+  {
+    uint32_t g[DPT], gs = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) g[j] = ghist[threadIdx.x * DPT + j], gs += g[j];
+    uint32_t inc = gs;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(inc, off);
+      if (lane >= off) inc += o;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t at = inc - gs;
+    for (int k2 = 0; k2 < w; ++k2) at += wsum[k2];
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) gbase[threadIdx.x * DPT + j] = at, at += g[j];
+  }
   __syncthreads();
-  const uint32_t tile = s_tile;
-  const uint32_t tile0 = tile * (uint32_t)TILE;
-  const uint32_t cnt = n - tile0 < (uint32_t)TILE ? n - tile0 : (uint32_t)TILE;
-
+  uint32_t tile = s_tile[0];
+  if (tile >= tiles) return;
+  const uint32_t wbase = (uint32_t)w * (TILE / NW) + lane;
   uint4 rec[ITEMS];
   uint32_t rk[ITEMS];
-  typename Side::Thr thr{};
-  const uint32_t wbase = (uint32_t)w * (TILE / NW) + lane;
-#pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const uint32_t i = wbase + r * 64;
-    rec[r] = i < cnt ? src.load(tile0 + i, thr) : make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (int r = 0; r < ITEMS; ++r)
-    if (wbase + r * 64 < cnt) side.add(sl, rec[r], thr);
-  uint32_t *mycnt = wcnt[w];
-#pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const bool live = wbase + r * 64 < cnt;
-    const uint32_t d = (src.key(rec[r]) >> shift) & (RADIX - 1);
-    uint64_t peer = __ballot(live);
-#pragma unroll
-    for (int b = 0; b < DB; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      peer &= bit ? bb : ~bb;
-    }
-    const uint32_t below = __popcll(peer & lt);
-    const uint32_t before = live ? mycnt[d] : 0u;  // all reads precede the leaders' writes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (live && below == 0) mycnt[d] = before + __popcll(peer);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    rk[r] = live ? before + below : 0xFFFFFFFFu;
-  }
-  __syncthreads();
-  // thread t owns digits [t*DPT, (t+1)*DPT): tile totals, wave starts, and the
-  // exclusive scans of the tile totals (lbase) and of the global totals
-  uint32_t run[DPT], gtot[DPT], tsum = 0, gsum = 0;
-#pragma unroll
-  for (int j = 0; j < DPT; ++j) {
-    const uint32_t d = threadIdx.x * DPT + j;
-    uint32_t r0 = 0;
-#pragma unroll
-    for (int k2 = 0; k2 < NW; ++k2) {
-      const uint32_t c = wcnt[k2][d];
-      wcnt[k2][d] = r0;
-      r0 += c;
-    }
-    run[j] = r0;
-    tsum += r0;
-    gtot[j] = ghist[d];
-    gsum += gtot[j];
-  }
-  // publish this tile's counts first (later tiles may be waiting for them)
-#pragma unroll
-  for (int j = 0; j < DPT; ++j)
-    sw_store(&status[(size_t)tile * RADIX + threadIdx.x * DPT + j],
-             (tile ? SW_AGG : SW_INC) | run[j]);
-  uint32_t inc = tsum, ginc = gsum;
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t o = __shfl_up(inc, off), go = __shfl_up(ginc, off);
-    if (lane >= off) inc += o, ginc += go;
-  }
-  if (lane == 63) wsum[0][w] = inc, wsum[1][w] = ginc;
-  __syncthreads();
   {
-    uint32_t pre = 0, gpre = 0;
-    for (int k2 = 0; k2 < w; ++k2) pre += wsum[0][k2], gpre += wsum[1][k2];
-    uint32_t at = pre + inc - tsum, gat = gpre + ginc - gsum;
+    const uint32_t tile0 = tile * (uint32_t)TILE;
+    const uint32_t cnt = n - tile0 < (uint32_t)TILE ? n - tile0 : (uint32_t)TILE;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t i = wbase + r * 64;
+      rec[r] = i < cnt ? src.load(tile0 + i) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  uint32_t *mycnt = wcnt[w];
+  for (uint32_t it = 0;; ++it) {
+    const uint64_t tr0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint32_t tile0 = tile * (uint32_t)TILE;
+    const uint32_t cnt = n - tile0 < (uint32_t)TILE ? n - tile0 : (uint32_t)TILE;
+    if (PERSIST && threadIdx.x == 0) s_tile[(it + 1) & 1] = atomicAdd(tile_ctr, 1u);
+    // 1: rank (the wave's own counter row: no block barrier before it)
+    for (uint32_t d = lane; d < RADIX; d += 64) mycnt[d] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t i = wbase + r * 64;
+      const bool live = i < cnt;
+      const uint32_t d = (src.key(rec[r]) >> shift) & (RADIX - 1);
+      uint64_t peer = __ballot(live);
+#pragma unroll
+      for (int b = 0; b < DB; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peer &= bit ? bb : ~bb;
+      }
+      const uint32_t below = __popcll(peer & lt);
+      const uint32_t before = live ? mycnt[d] : 0u;  // all reads precede the leaders' writes
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (live && below == 0) mycnt[d] = before + __popcll(peer);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      rk[r] = live ? before + below : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint64_t tr1 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    // 2: thread t owns digits [t*DPT, (t+1)*DPT): tile totals (published at
+    // once: later tiles may be waiting for them), wave starts, tile-local starts
+    uint32_t run[DPT], tsum = 0;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       const uint32_t d = threadIdx.x * DPT + j;
-      lbase[d] = at;
-      at += run[j];
-      const uint32_t before = tile ? look_back(status, tile, RADIX, d, run[j]) : 0u;
-      gpos[d] = gat + before;
-      gat += gtot[j];
-    }
-  }
-  __syncthreads();
+      uint32_t r0 = 0;
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    if (rk[r] == 0xFFFFFFFFu) continue;
-    const uint32_t d = (src.key(rec[r]) >> shift) & (RADIX - 1);
-    srec[lbase[d] + mycnt[d] + rk[r]] = rec[r];
+      for (int k2 = 0; k2 < NW; ++k2) {
+        const uint32_t c = wcnt[k2][d];
+        wcnt[k2][d] = r0;
+        r0 += c;
+      }
+      run[j] = r0;
+      tsum += r0;
+      sw_store(&status[(size_t)tile * RADIX + d], (tile ? SW_AGG : SW_INC) | r0);
+    }
+    uint32_t inc = tsum;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(inc, off);
+      if (lane >= off) inc += o;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    {
+      uint32_t at = inc - tsum;
+      for (int k2 = 0; k2 < w; ++k2) at += wsum[k2];
+#pragma unroll
+      for (int j = 0; j < DPT; ++j) lbase[threadIdx.x * DPT + j] = at, at += run[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      if (rk[r] == 0xFFFFFFFFu) continue;
+      const uint32_t d = (src.key(rec[r]) >> shift) & (RADIX - 1);
+      srec[lbase[d] + mycnt[d] + rk[r]] = rec[r];
+    }
+    // 3: the next tile's loads, then the look-back
+    const uint32_t next = PERSIST ? s_tile[(it + 1) & 1] : tiles;
+    if (next < tiles) {
+      const uint32_t n0 = next * (uint32_t)TILE;
+      const uint32_t ncnt = n - n0 < (uint32_t)TILE ? n - n0 : (uint32_t)TILE;
+#pragma unroll
+      for (int r = 0; r < ITEMS; ++r) {
+        const uint32_t i = wbase + r * 64;
+        rec[r] = i < ncnt ? src.load(n0 + i) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const uint32_t d = threadIdx.x * DPT + j;
+      gpos[d] = gbase[d] + (tile ? look_back(status, tile, RADIX, d, run[j]) : 0u);
+    }
+    __syncthreads();
+    const uint64_t tr2 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    // 4: write-out (the next iteration's LDS writes follow its first barrier,
+    // which every thread reaches only after this loop)
+    for (uint32_t j0 = 0; j0 < cnt; j0 += T) {  // wave-uniform trip count (Dst::wave)
+      const uint32_t j = j0 + threadIdx.x;
+      const bool live = j < cnt;
+      const uint4 r = live ? srec[j] : make_uint4(0, 0, 0, 0);
+      if (live) {
+        const uint32_t d = (src.key(r) >> shift) & (RADIX - 1);
+        dst.store(gpos[d] + (j - lbase[d]), r);
+      }
+      if (Dst::kWave) dst.wave(r, live);
+    }
+    if (trace && threadIdx.x == 0) {  // RK_NW_TRACE: phase timestamps of this tile
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint64_t *o = trace + (size_t)tile * 6;
+      o[0] = tr0;
+      o[1] = tr1;
+      o[2] = tr2;
+      o[3] = __builtin_amdgcn_s_memrealtime();
+      o[4] = xcc & 15u;
+      o[5] = blockIdx.x;
+    }
+    tile = next;
+    if (tile >= tiles) break;
   }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < cnt; j += T) {
-    const uint4 r = srec[j];
-    const uint32_t d = (src.key(r) >> shift) & (RADIX - 1);
-    dst.store(gpos[d] + (j - lbase[d]), r);
-  }
-  side.flush(sl, thr);
 }
 
 // records in a uint4 array, key = .x (streamed once: nontemporal loads)
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 struct SrcRec {
   const uint4 *in;
-  struct Thr0 {};
-  template <class Thr>
-  __device__ __forceinline__ uint4 load(uint32_t i, Thr &) const {
+  __device__ __forceinline__ uint4 load(uint32_t i) const {
     const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(in + i));
     return make_uint4(v.x, v.y, v.z, v.w);
   }
   __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
 };
+// Dst::wave(rec, live): called by every lane of a wave for consecutive
+// sorted slots of the tile (kWave = false: not at all)
+#define RK_NO_WAVE                   \
+  static constexpr bool kWave = false; \
+  __device__ __forceinline__ void wave(const uint4 &, bool) const {}
 struct DstRec {
+  RK_NO_WAVE
   uint4 *out;
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const { out[pos] = r; }
 };
+
+// arr[v] += the length of every run of equal v != NONE over consecutive lanes
+// (one atomic per run: sorted records repeat their chunk ids; arr in LDS)
+__device__ __forceinline__ void wave_run_add(uint32_t v, uint32_t *arr) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t pv = __shfl_up(v, 1), nv = __shfl_down(v, 1);
+  const bool head = v != NONE && (lane == 0 || pv != v);
+  const uint64_t tails = __ballot(v != NONE && (lane == 63 || nv != v));
+  if (head) {
+    const uint32_t e = __builtin_ctzll(tails & ~((1ull << lane) - 1ull));
+    atomicAdd(&arr[v], e - lane + 1);
+  }
+}
 
 // --- processing order, pass 1: the file-order SoA becomes records ----------
 struct SrcFile {
   const uint64_t *x, *y, *len;
   const uint8_t *strand;
   uint64_t vsize;
-  template <class Thr>
-  __device__ __forceinline__ uint4 load(uint32_t i, Thr &t) const {
+  __device__ __forceinline__ uint4 load(uint32_t i) const {
     const uint64_t xs = x[i], ys = y[i], L = len[i];
     const uint32_t s = strand[i] != 'f' ? 1u : 0u;
     const uint64_t pk = xs / 10;
     const uint32_t key = (uint32_t)(pk < vsize - 1 ? pk : vsize - 1);
-    // not representable: the generic pipeline takes over (flag)
-    t.wide |= L >= (1ull << 24) || ys >= (1ull << 35);
+    // (rows that do not pack were flagged by k_nw_order_hist: the generic
+    // pipeline takes over then)
     return make_uint4(key, i, (uint32_t)ys,
                       (uint32_t)(L & 0xFFFFFFu) | s << 24 | (uint32_t)((ys >> 32) & 7u) << 25 |
                           (uint32_t)(xs % 10) << 28);
   }
   __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
 };
-// ... and, on the side, the Y axis' digit histograms, the forward-strand
-// count, the longest length and the probe-range checks of every kept row
-struct SideFile {
-  Digits yd;
-  uint64_t drop, max_x, max_y;
-  uint32_t nby;
-  uint32_t *yhist;  // [4][1024]
-  uint32_t *ctrl;   // [0] error bits, [3] narrow-failure flag, [4] max length, [8] forward kept
-  struct Lds {
-    HistLds h;
-    uint32_t red[3];
-  };
-  struct Thr {
-    bool wide = false, ub = false;
-    uint32_t maxlen = 0, fwd = 0;
-  };
-  __device__ void init(Lds &L) const {
-    hist_init(L.h);
-    if (threadIdx.x < 3) L.red[threadIdx.x] = 0;
-  }
-  __device__ void add(Lds &L, const uint4 &r, Thr &t) const {
-    if (r.x == drop) return;  // the never-iterated last bucket
-    const uint64_t xs = rec_x(r), ys = rec_y(r);
-    const uint32_t len = rec_len(r), s = rec_strand(r);
-    const uint64_t h = len / 2;
-    if (probe_max_bucket_nw(xs + h, max_x) > max_x || probe_max_bucket_nw(ys + h, max_y) > max_y)
-      t.ub = true;
-    t.maxlen = len > t.maxlen ? len : t.maxlen;
-    t.fwd += s == 0;
-    const uint64_t yc = ys + h;
-    hist_add(L.h, yd, s * nby + (uint32_t)(yc / 100));
-  }
-  __device__ void flush(Lds &L, Thr &t) const {
-    // every add() of this block precedes the kernel's last barrier
-    const uint64_t wide = __ballot(t.wide), ub = __ballot(t.ub);
-    uint32_t mx = t.maxlen, fw = t.fwd;
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint32_t o = __shfl_xor(mx, off);
-      mx = o > mx ? o : mx;
-      fw += __shfl_xor(fw, off);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      if (wide) atomicOr(&L.red[0], 1u);
-      if (ub) atomicOr(&L.red[0], 2u);
-      atomicMax(&L.red[1], mx);
-      atomicAdd(&L.red[2], fw);
-    }
-    __syncthreads();
-    hist_flush(L.h, yd, yhist);
-    if (threadIdx.x == 0) {
-      if (L.red[0] & 1u) atomicOr(&ctrl[3], 1u);
-      if (L.red[0] & 2u) atomicOr(&ctrl[0], ERRB_UB_CENTER);
-      atomicMax(&ctrl[4], L.red[1]);
-      if (L.red[2]) atomicAdd(&ctrl[8], L.red[2]);
-    }
-  }
-};
-
 // --- processing order, last pass: the records, and the Y axis' input -------
 // Yrec: {strand * nby + centre/100, processing index, centre low 32, length}
 struct DstProc {
+  RK_NO_WAVE
   uint4 *out, *yrec;
   uint32_t nby;
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const {
@@ -367,6 +396,7 @@ struct DstProc {
 
 // --- Y axis, last pass: the CSR arrays the sweeps read -----------------------
 struct DstCsr {
+  RK_NO_WAVE
   uint32_t *key, *ent;
   uint2 *pk;
   uint8_t *nbd;
@@ -387,6 +417,7 @@ struct DstCsr {
 // members {gid, row, sort key lo, hi} -> group of every slot, sort key, tag =
 // slot, file row
 struct DstMembers {
+  RK_NO_WAVE
   uint32_t *sgid, *tag, *mrow;
   uint64_t *key;
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const {
@@ -398,312 +429,279 @@ struct DstMembers {
 };
 
 // ---------------------------------------------------------------------------
-// processing-order histograms from xStart alone; kept rows; xStart/10 >= vsize
-__global__ void __launch_bounds__(256) k_nw_order_hist(const uint64_t *__restrict__ x, uint32_t n,
-                                                       uint64_t vsize, Digits D,
-                                                       uint32_t *__restrict__ ghist,
-                                                       uint32_t *__restrict__ ctrl) {
-  __shared__ HistLds L;
-  __shared__ uint32_t part[4];
+// One read of the file-order SoA before the sort: the digit histograms of the
+// processing key (all passes) and of the Y axis key of every kept row, the
+// kept-row and forward-strand counts, the longest kept length, the
+// out-of-bounds checks (xStart/10 >= vsize; probes past an occupancy array)
+// and whether every row packs into a record.  ctrl: [0] error bits, [1] kept
+// rows, [3] some row does not pack, [4] longest kept length, [8] forward kept.
+struct OrderHistArgs {
+  const uint64_t *x, *y, *len;
+  const uint8_t *strand;
+  uint32_t n;
+  uint64_t vsize, max_x, max_y;
+  uint32_t nby;
+  Digits D, yd;
+  uint32_t *ghist, *yhist, *ctrl;
+};
+__global__ void __launch_bounds__(256) k_nw_order_hist(OrderHistArgs a) {
+  __shared__ HistLds L, LY;
+  __shared__ uint32_t red[4];
   hist_init(L);
+  hist_init(LY);
+  if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t kept = 0;
-  bool ub = false;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint64_t pk = x[i] / 10;
-    ub |= pk >= vsize;
-    const uint32_t key = (uint32_t)(pk < vsize - 1 ? pk : vsize - 1);
-    kept += key != vsize - 1;
-    hist_add(L, D, key);
+  uint32_t kept = 0, fwd = 0, maxlen = 0;
+  bool ub = false, ubc = false, wide = false;
+  const uint64_t drop = a.vsize - 1;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+    const uint64_t xs = a.x[i], ys = a.y[i], L0 = a.len[i];
+    const uint32_t s = a.strand[i] != 'f' ? 1u : 0u;
+    const uint64_t pk = xs / 10;
+    ub |= pk >= a.vsize;
+    wide |= L0 >= (1ull << 24) || ys >= (1ull << 35);
+    const uint32_t key = (uint32_t)(pk < drop ? pk : drop);
+    hist_add(L, a.D, key);
+    if (key == drop) continue;  // the never-iterated last bucket
+    ++kept;
+    fwd += s == 0;
+    const uint32_t len = (uint32_t)(L0 & 0xFFFFFFu);  // exact whenever the row packs
+    maxlen = len > maxlen ? len : maxlen;
+    const uint64_t h = len / 2;
+    ubc |= probe_max_bucket_nw(xs + h, a.max_x) > a.max_x ||
+           probe_max_bucket_nw(ys + h, a.max_y) > a.max_y;
+    hist_add(LY, a.yd, s * a.nby + (uint32_t)((ys + h) / 100));
   }
-  for (int off = 32; off > 0; off >>= 1) kept += __shfl_xor(kept, off);
-  const uint64_t any_ub = __ballot(ub);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = kept;
-  if ((threadIdx.x & 63) == 0 && any_ub) atomicOr(&ctrl[0], ERRB_UB_BUCKET);
+  for (int off = 32; off > 0; off >>= 1) {
+    kept += __shfl_xor(kept, off);
+    fwd += __shfl_xor(fwd, off);
+    const uint32_t o = __shfl_xor(maxlen, off);
+    maxlen = o > maxlen ? o : maxlen;
+  }
+  const uint64_t bub = __ballot(ub), bubc = __ballot(ubc), bwide = __ballot(wide);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&red[0], kept);
+    atomicAdd(&red[1], fwd);
+    atomicMax(&red[2], maxlen);
+    atomicOr(&red[3], (bub ? 1u : 0u) | (bubc ? 2u : 0u) | (bwide ? 4u : 0u));
+  }
   __syncthreads();
-  hist_flush(L, D, ghist);
+  hist_flush(L, a.D, a.ghist);
+  hist_flush(LY, a.yd, a.yhist);
   if (threadIdx.x == 0) {
-    const uint32_t t = part[0] + part[1] + part[2] + part[3];
-    if (t) atomicAdd(&ctrl[1], t);
+    if (red[0]) atomicAdd(&a.ctrl[1], red[0]);
+    if (red[1]) atomicAdd(&a.ctrl[8], red[1]);
+    if (red[2]) atomicMax(&a.ctrl[4], red[2]);
+    if (red[3] & 1u) atomicOr(&a.ctrl[0], ERRB_UB_BUCKET);
+    if (red[3] & 2u) atomicOr(&a.ctrl[0], ERRB_UB_CENTER);
+    if (red[3] & 4u) atomicOr(&a.ctrl[3], 1u);
   }
 }
 
 // ---------------------------------------------------------------------------
 // X axis by chunks of W centre buckets (both strands), from the processing
-// order.  Chunk c (dynamic id) owns buckets [cW, (c+1)W); its entries are the
-// rows with xStart/10 in [10cW - ceil(H/10), 10(c+1)W) whose centre falls in
-// the chunk (H = longest length / 2): a contiguous row range found by three
-// wave-wide 64-ary searches.  Entries are collected in row order into LDS,
-// ranked within their bucket in that order (stable = processing order),
-// counted per strand and placed by a look-back over the chunks: forward
-// entries at [0, M0), the others after.  The same pass writes every OWNED row's
-// member record {0, row, sort key}: the sort key needs the yStart of the last
-// row of its xStart/10 run, and chunk borders are run borders.
-constexpr int XC_T = 256, XC_CAP = 2048;
-struct XChunkArgs;
-
-__device__ __forceinline__ uint32_t wave_lower_bound(const uint4 *R, uint32_t m, uint32_t T) {
-  const uint32_t *key = reinterpret_cast<const uint32_t *>(R);
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t lo = 0, hi = m;  // answer in [lo, hi]: first row with key >= T
-  while (hi - lo > 64) {
-    const uint32_t step = (hi - lo + 63) / 64;
-    const uint32_t p = lo + lane * step;
-    const bool pred = p < hi && key[4 * (size_t)p] < T;
-    const uint32_t c = __popcll(__ballot(pred));
-    if (c == 0) return lo;
-    const uint32_t nlo = lo + (c - 1) * step + 1;
-    const uint32_t nhi = c < 64 ? min(hi, lo + c * step) : hi;
-    lo = nlo;
-    hi = nhi;
+// order, one wavefront per chunk.  Chunk c owns buckets [cW, (c+1)W); its
+// entries are the rows whose centre falls in the chunk: the rows it OWNS
+// (xStart/100 in the chunk: [kO, kB), from the owner counts of the last order
+// pass) plus a halo of earlier rows (centre <= xStart + H, H = longest length
+// / 2), found by a backward ballot scan from kO.  The wave counts its entries
+// per (strand, bucket) bin in LDS, scans the counts into bin starts, and
+// places every entry at chunk offset (strand-major scan of the per-chunk
+// counts, also from the last order pass) + bin start + its rank among the
+// bin's entries in row order (= processing order: stable).  No look-back, no
+// block barrier.  The same wave writes every owned row's member record
+// {0, row, sort key}: the sort key |yStart - diag_func[xStart/10]| needs the
+// yStart of the LAST row of the row's xStart/10 run (commonFunctions.cpp:
+// 161-177), and chunk borders are run borders.
+// Per-chunk counts for the X axis, from the processing order (sorted by
+// xStart/10, so a block's rows cover a narrow window of chunks): cnts[s * nch
+// + chunk of the row's X bucket] (strand s) and cnts[2 nch + owner chunk]
+// (xStart/10 / 10W).  Runs of equal ids are added per wave into an LDS window
+// of chunks, flushed with one global atomic per non-zero bin.
+constexpr int XN_T = 256, XN_ITEMS = 16, XN_WIN = 1024;
+__global__ void __launch_bounds__(XN_T) k_nw_xcount(const uint4 *__restrict__ R, uint32_t m,
+                                                    uint32_t lgW, uint32_t nch, uint32_t kdiv,
+                                                    uint32_t *__restrict__ cnts) {
+  __shared__ uint32_t win[3 * XN_WIN];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t r0 = blockIdx.x * (XN_T * XN_ITEMS);
+  for (uint32_t j = threadIdx.x; j < 3 * XN_WIN; j += XN_T) win[j] = 0;
+  const uint32_t w0 = R[r0].x / kdiv;  // the block's first owner chunk
+  __syncthreads();
+  const uint32_t wb = r0 + wv * 64 * XN_ITEMS;
+  uint4 rr[XN_ITEMS];
+#pragma unroll
+  for (int i = 0; i < XN_ITEMS; ++i) {
+    const uint32_t k = wb + i * 64 + lane;
+    rr[i] = k < m ? R[k] : make_uint4(NONE, 0, 0, 0);
   }
-  const uint32_t p = lo + lane;
-  const bool pred = p < hi && key[4 * (size_t)p] < T;
-  return lo + (uint32_t)__popcll(__ballot(pred));
+#pragma unroll
+  for (int i = 0; i < XN_ITEMS; ++i) {
+    const uint4 r = rr[i];
+    const bool live = wb + i * 64 + lane < m;
+    uint32_t vx = NONE, vo = NONE;
+    if (live) {
+      const uint32_t cx = (uint32_t)((rec_x(r) + rec_len(r) / 2) / 100) >> lgW;
+      const uint32_t co = r.x / kdiv, st = rec_strand(r);
+      if (cx - w0 < XN_WIN) vx = st * XN_WIN + (cx - w0);
+      else atomicAdd(&cnts[st * nch + cx], 1u);  // outside the window: rare
+      if (co - w0 < XN_WIN) vo = 2 * XN_WIN + (co - w0);
+      else atomicAdd(&cnts[2 * nch + co], 1u);
+    }
+    wave_run_add(vx, win);
+    wave_run_add(vo, win);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < 3 * XN_WIN; j += XN_T) {
+    const uint32_t v = win[j];
+    if (!v) continue;
+    const uint32_t part = j / XN_WIN, ch = w0 + (j - part * XN_WIN);
+    atomicAdd(&cnts[part * nch + ch], v);
+  }
 }
 
+constexpr int XC_WAVES = 4, XC_SLOTS = 8;  // rows per batch: XC_SLOTS x 64
 struct XChunkArgs {
-  const uint4 *R;     // processing order
-  uint32_t m;         // kept rows
-  uint32_t W, lgW;    // chunk width in buckets (power of two)
-  uint32_t nchunks;
-  uint32_t halo;      // ceil(H / 10) in xStart/10 units
-  uint32_t nbx;
+  const uint4 *R;        // processing order
+  uint32_t m;            // kept rows
+  uint32_t W, lgW, nch;  // chunk width in buckets (power of two), chunks
+  uint32_t halo;         // ceil(H / 10) in xStart/10 units
   uint64_t max_x;
-  uint32_t M0;        // forward-strand entries (all chunks)
+  uint32_t nbx;
+  const uint32_t *xoff;  // [2 nch] strand-major entry offsets, [nch + 1] owner row starts (+ m)
   Csr out;
-  uint4 *erec;        // member records (processing order)
-  uint32_t *status;   // [nchunks][2]
-  uint32_t *ctr;
-  uint32_t *ctrl;     // [0] err bits, [6] wide sort keys, [7] chunk overflow
+  uint4 *erec;           // member records (processing order)
+  uint32_t *ctrl;        // [6] some sort key >= 2^32
 };
 
-// a chunk entry from its processing-order record (mine: its centre bucket is
-// in the chunk)
-struct XEnt {
-  bool mine;
-  uint32_t bin, s;
-  uint64_t xc;
-  uint32_t len;
-};
-__device__ __forceinline__ XEnt x_entry(const uint4 &r, bool in, uint64_t b0, uint32_t W) {
-  XEnt e;
-  const uint64_t xs = rec_x(r);
-  e.len = rec_len(r);
-  e.s = rec_strand(r);
-  e.xc = xs + e.len / 2;
-  const uint64_t bk = e.xc / 100;
-  e.mine = in && bk >= b0 && bk < b0 + W;
-  e.bin = (uint32_t)(e.s * W + (bk - b0));
-  return e;
-}
-
-// Rank the LDS list ent[0, cnt) (row order) within each bin against the
-// running per-bin counters rcnt, by one wavefront 64 entries at a time
-// (DB ballots; stable), and place entry i at CSR position start[bin] + rank.
-__device__ __forceinline__ void rank_and_write(const XChunkArgs &a, const uint4 *ent, uint32_t cnt,
-                                               uint32_t *rcnt, const uint32_t *start, int bits,
-                                               uint64_t b0, uint32_t off_f, uint32_t off_r,
-                                               uint32_t nf) {
-  const uint32_t lane = threadIdx.x & 63;
-  if (threadIdx.x >= 64) return;
-  for (uint32_t r0 = 0; r0 < cnt; r0 += 64) {
-    const uint32_t i = r0 + lane;
-    const bool live = i < cnt;
-    const uint4 e = live ? ent[i] : make_uint4(0, 0, 0, 0);
-    const uint32_t bin = e.x;
-    uint64_t peer = __ballot(live);
-    for (int b = 0; b < bits; ++b) {
-      const bool bit = (bin >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      peer &= bit ? bb : ~bb;
-    }
-    const uint32_t below = __popcll(peer & ((1ull << lane) - 1ull));
-    const uint32_t before = live ? rcnt[bin] : 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (live && below == 0) rcnt[bin] = before + __popcll(peer);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!live) continue;
-    const uint32_t loc = start[bin] + before + below;
-    const uint32_t s = bin >= a.W ? 1u : 0u;
-    const uint32_t q = s == 0 ? off_f + loc : a.M0 + off_r + (loc - nf);
-    const uint64_t bk = b0 + (bin - s * a.W);
-    const uint64_t cbase = bk * 100;
-    const uint64_t xc = cbase + (uint32_t)(e.z - (uint32_t)cbase);
-    a.out.key[q] = s * a.nbx + (uint32_t)bk;
-    a.out.ent[q] = e.y;
-    a.out.pk[q] = make_uint2(e.z, e.w);
-    a.out.nbd[q] = nbd_code_nw(xc, a.max_x);
-    a.out.state[q] = ST_UNKNOWN;
-  }
-}
-
-__global__ void __launch_bounds__(XC_T) k_nw_xchunk(XChunkArgs a) {
-  constexpr int NW = XC_T / 64;
-  __shared__ uint4 ent[XC_CAP];      // {bin, row k, centre lo, length}, row order
-  __shared__ uint32_t hcnt[2048];    // per-bin counts, then starts
-  __shared__ uint32_t rcnt[2048];    // running per-bin ranks
-  __shared__ uint32_t s_chunk, s_rng[3], s_n, s_nf, s_wofs[NW], s_hi, s_bad;
-  __shared__ uint32_t s_off[2];
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_chunk = atomicAdd(a.ctr, 1u), s_n = 0, s_nf = 0, s_bad = 0;
-  __syncthreads();
-  const uint32_t c = s_chunk;
-  const uint64_t own = (uint64_t)10 * a.W * c, nxt = own + (uint64_t)10 * a.W;
-  if (w < 3) {
-    const uint64_t t64 = w == 0 ? (own > a.halo ? own - a.halo : 0) : w == 1 ? own : nxt;
-    const uint32_t t = t64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t64;
-    const uint32_t r = wave_lower_bound(a.R, a.m, t);
-    if (lane == 0) s_rng[w] = r;
-  }
-  for (uint32_t j = threadIdx.x; j < 2 * a.W; j += XC_T) hcnt[j] = 0, rcnt[j] = 0;
-  __syncthreads();
-  const uint32_t kA = s_rng[0], kO = s_rng[1], kB = s_rng[2];
+__global__ void __launch_bounds__(64 * XC_WAVES) k_nw_xchunk(XChunkArgs a) {
+  extern __shared__ uint32_t xc_lds[];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t c = blockIdx.x * XC_WAVES + wv;
+  if (c >= a.nch) return;  // whole waves; nothing below synchronises the block
+  const uint32_t nb2 = 2 * a.W;
+  uint32_t *bin_at = xc_lds + (size_t)wv * nb2;  // counts, then running positions
+  for (uint32_t j = lane; j < nb2; j += 64) bin_at[j] = 0;
+  const uint32_t *orow = a.xoff + 2 * a.nch;
+  const uint32_t kO = orow[c] - a.m, kB = orow[c + 1] - a.m;
   const uint64_t b0 = (uint64_t)a.W * c;
-  bool wide_key = false;
-  // rows in order: X entries of this chunk -> per-bin counts and the LDS list
-  // (while it fits); owned rows -> sort keys
-  for (uint32_t base = kA; base < kB; base += XC_T) {
-    const uint32_t k = base + threadIdx.x;
-    const bool in = k < kB;
-    const uint4 r = in ? a.R[k] : make_uint4(0, 0, 0, 0);
-    const XEnt e = x_entry(r, in, b0, a.W);
-    const uint64_t bal = __ballot(e.mine), fbal = __ballot(e.mine && e.s == 0);
-    if (lane == 0) s_wofs[w] = __popcll(bal), atomicAdd(&s_nf, (uint32_t)__popcll(fbal));
-    if (e.mine) atomicAdd(&hcnt[e.bin], 1u);
-    __syncthreads();
-    uint32_t at = s_n;
-    for (uint32_t q = 0; q < w; ++q) at += s_wofs[q];
-    at += __popcll(bal & ((1ull << lane) - 1ull));
-    if (e.mine && at < XC_CAP) ent[at] = make_uint4(e.bin, k, (uint32_t)e.xc, e.len);
-    // owned rows: |yStart - yStart(last row of the xStart/10 run)|
-    const bool owned = in && k >= kO;
-    if (__ballot(owned)) {
-      const uint32_t key = r.x;
-      const uint64_t ys = rec_y(r);
-      const bool end = owned && (k + 1 >= kB || a.R[k + 1].x != key);
-      const uint64_t ends = __ballot(end) & ~((1ull << lane) - 1ull);
-      const int src = ends ? __ffsll((unsigned long long)ends) - 1 : 63;
-      uint64_t d = __shfl(ys, src);
-      if (__ballot(owned && !ends)) {  // the wave's last run continues past it
-        const uint32_t klast = __shfl(key, 63);
-        uint32_t eidx = 0;
-        for (uint32_t b = base + (w + 1) * 64;; b += 64) {
-          const uint32_t q = b + lane;
-          const uint64_t stop = __ballot(q >= kB || a.R[q].x != klast);
-          if (stop) {
-            eidx = b + __builtin_ctzll(stop) - 1;
-            break;
-          }
-        }
-        if (owned && !ends) d = rec_y(a.R[eidx]);
-      }
-      if (owned) {
-        const uint64_t h = ys > d ? ys - d : d - ys;
+  // halo rows: the suffix of [0, kO) with xStart/10 >= 10Wc - halo
+  const uint64_t own_key = (uint64_t)10 * a.W * c;
+  const uint64_t hk = own_key > a.halo ? own_key - a.halo : 0;
+  uint32_t kA = kO;
+  while (kA > 0) {
+    const uint32_t lo = kA >= 64 ? kA - 64 : 0;
+    const uint32_t k = lo + lane;
+    const bool in = k < kA && a.R[k].x >= hk;
+    const uint32_t nin = (uint32_t)__popcll(__ballot(in));
+    const bool all = nin == kA - lo;
+    kA -= nin;
+    if (!all) break;
+  }
+  const uint32_t nrows = kB - kA, nbatch = (nrows + 64 * XC_SLOTS - 1) / (64 * XC_SLOTS);
+  uint4 rr[XC_SLOTS];
+  // pass 1, batches and slots backwards: bin counts, owned rows' sort keys
+  // (carry: key and run-end yStart of the row just after the current slot)
+  uint32_t carry_key = NONE;
+  uint64_t carry_end = 0;
+  bool wide = false;
+  for (uint32_t bi = nbatch; bi-- > 0;) {
+    const uint32_t base = kA + bi * 64 * XC_SLOTS;
+#pragma unroll
+    for (int s = 0; s < XC_SLOTS; ++s) {
+      const uint32_t k = base + s * 64 + lane;
+      rr[s] = k < kB ? a.R[k] : make_uint4(NONE, 0, 0, 0);
+    }
+#pragma unroll
+    for (int s = XC_SLOTS - 1; s >= 0; --s) {
+      const uint32_t k = base + s * 64 + lane;
+      const bool live = k < kB;
+      const uint4 r = rr[s];
+      const uint64_t xs = rec_x(r), ys = rec_y(r);
+      const uint32_t len = rec_len(r), st = rec_strand(r);
+      const uint64_t bk = (xs + len / 2) / 100;
+      if (live && bk >= b0 && bk < b0 + a.W) atomicAdd(&bin_at[st * a.W + (uint32_t)(bk - b0)], 1u);
+      // run ends inside the slot; the last row's successor is the carry
+      const uint32_t key = live ? r.x : NONE;
+      uint32_t nk = __shfl_down(key, 1);
+      if (lane == 63) nk = carry_key;
+      const uint64_t ends = __ballot(live && nk != key);
+      const uint64_t above = ends & ~((1ull << lane) - 1ull);
+      const uint64_t end_ys =
+          above ? __shfl(ys, (int)__builtin_ctzll(above)) : carry_end;  // all lanes shuffle
+      if (live && k >= kO) {
+        const uint64_t h = ys > end_ys ? ys - end_ys : end_ys - ys;
         a.erec[k] = make_uint4(0, r.y, (uint32_t)h, (uint32_t)(h >> 32));
-        wide_key |= (h >> 32) != 0;
+        wide |= (h >> 32) != 0;
       }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t t = 0;
-      for (uint32_t q = 0; q < NW; ++q) t += s_wofs[q];
-      s_n += t;
-    }
-    __syncthreads();
-  }
-  const uint64_t any_wide = __ballot(wide_key);
-  if ((threadIdx.x & 63) == 0 && any_wide && *(volatile uint32_t *)&a.ctrl[6] == 0)
-    atomicOr(&a.ctrl[6], 1u);
-  const uint32_t n = s_n, nf = s_nf;
-  // place the chunk among the chunks (per strand)
-  if (threadIdx.x < 2) {
-    const uint32_t mine = threadIdx.x == 0 ? nf : n - nf;
-    if (c == 0) {
-      sw_store(&a.status[threadIdx.x], SW_INC | mine);
-      s_off[threadIdx.x] = 0;
-    } else {
-      sw_store(&a.status[2 * (size_t)c + threadIdx.x], SW_AGG | mine);
-      s_off[threadIdx.x] = look_back(a.status, c, 2, threadIdx.x, mine);
+      carry_key = __shfl(key, 0);
+      carry_end = __shfl(end_ys, 0);
     }
   }
-  // bin starts: exclusive scan of the 2W counts
+  if (__ballot(wide) && lane == 0) atomicOr(&a.ctrl[6], 1u);
+  // bin starts (exclusive scan over the 2W bins, W/32 per lane)
   {
-    const uint32_t per = (2 * a.W + XC_T - 1) / XC_T;
+    const uint32_t per = nb2 / 64;
     uint32_t tot = 0;
-    for (uint32_t j = 0; j < per; ++j) {
-      const uint32_t bn = threadIdx.x * per + j;
-      tot += bn < 2 * a.W ? hcnt[bn] : 0u;
-    }
+    for (uint32_t j = 0; j < per; ++j) tot += bin_at[lane * per + j];
     uint32_t inc = tot;
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t o = __shfl_up(inc, off);
       if ((int)lane >= off) inc += o;
     }
-    if (lane == 63) s_wofs[w] = inc;
-    __syncthreads();
     uint32_t at = inc - tot;
-    for (uint32_t q = 0; q < w; ++q) at += s_wofs[q];
     for (uint32_t j = 0; j < per; ++j) {
-      const uint32_t bn = threadIdx.x * per + j;
-      if (bn < 2 * a.W) {
-        const uint32_t cn = hcnt[bn];
-        hcnt[bn] = at;
-        at += cn;
-      }
+      const uint32_t cn = bin_at[lane * per + j];
+      bin_at[lane * per + j] = at;
+      at += cn;
     }
   }
-  __syncthreads();
-  const uint32_t off_f = s_off[0], off_r = s_off[1];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t nf = bin_at[a.W];  // forward entries of the chunk
+  const uint32_t off_f = a.xoff[c], off_r = a.xoff[a.nch + c];
   const int bits = (int)a.lgW + 1;
-  if (n <= XC_CAP) {
-    rank_and_write(a, ent, n, rcnt, hcnt, bits, b0, off_f, off_r, nf);
-    return;
-  }
-  // A chunk denser than the list: its bins in ranges of at most XC_CAP
-  // entries, the rows re-read once per range.
-  for (uint32_t blo = 0; blo < 2 * a.W;) {
-    if (threadIdx.x == 0) {
-      // the widest bin range [blo, hi) of at most XC_CAP entries (at least one bin;
-      // bin starts are non-decreasing, the end of bin b is the start of b + 1)
-      const uint32_t nb = 2 * a.W;
-      auto end_of = [&](uint32_t b) { return b + 1 < nb ? hcnt[b + 1] : n; };
-      uint32_t hi = blo + 1;
-      while (hi < nb && end_of(hi) - hcnt[blo] <= XC_CAP) ++hi;
-      // a single bin above the list capacity: the generic pipeline takes over
-      if (end_of(blo) - hcnt[blo] > XC_CAP) s_bad = 1;
-      s_hi = hi;
-      s_n = 0;
-    }
-    __syncthreads();
-    if (s_bad) break;
-    const uint32_t bhi = s_hi;
-    for (uint32_t base = kA; base < kB; base += XC_T) {
-      const uint32_t k = base + threadIdx.x;
-      const bool in = k < kB;
-      const uint4 r = in ? a.R[k] : make_uint4(0, 0, 0, 0);
-      const XEnt e = x_entry(r, in, b0, a.W);
-      const bool take = e.mine && e.bin >= blo && e.bin < bhi;
-      const uint64_t bal = __ballot(take);
-      if (lane == 0) s_wofs[w] = __popcll(bal);
-      __syncthreads();
-      uint32_t at = s_n;
-      for (uint32_t q = 0; q < w; ++q) at += s_wofs[q];
-      at += __popcll(bal & ((1ull << lane) - 1ull));
-      if (take) ent[at] = make_uint4(e.bin, k, (uint32_t)e.xc, e.len);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (uint32_t q = 0; q < NW; ++q) t += s_wofs[q];
-        s_n += t;
+  // pass 2, forwards: rank within bin (ballots over the bin bits), place
+  for (uint32_t bi = 0; bi < nbatch; ++bi) {
+    const uint32_t base = kA + bi * 64 * XC_SLOTS;
+    if (nbatch > 1) {
+#pragma unroll
+      for (int s = 0; s < XC_SLOTS; ++s) {
+        const uint32_t k = base + s * 64 + lane;
+        rr[s] = k < kB ? a.R[k] : make_uint4(NONE, 0, 0, 0);
       }
-      __syncthreads();
     }
-    rank_and_write(a, ent, s_n, rcnt, hcnt, bits, b0, off_f, off_r, nf);
-    __syncthreads();
-    blo = bhi;
+#pragma unroll
+    for (int s = 0; s < XC_SLOTS; ++s) {
+      const uint32_t k = base + s * 64 + lane;
+      const uint4 r = rr[s];
+      const uint64_t xs = rec_x(r);
+      const uint32_t len = rec_len(r), st = rec_strand(r);
+      const uint64_t xc = xs + len / 2, bk = xc / 100;
+      const bool mine = k < kB && bk >= b0 && bk < b0 + a.W;
+      if (!__ballot(mine)) continue;
+      const uint32_t bin = mine ? st * a.W + (uint32_t)(bk - b0) : 0u;
+      uint64_t peer = __ballot(mine);
+      for (int b = 0; b < bits; ++b) {
+        const bool bit = (bin >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peer &= bit ? bb : ~bb;
+      }
+      const uint32_t below = __popcll(peer & ((1ull << lane) - 1ull));
+      const uint32_t before = mine ? bin_at[bin] : 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (mine && below == 0) bin_at[bin] = before + __popcll(peer);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (!mine) continue;
+      const uint32_t loc = before + below;
+      const uint32_t q = st == 0 ? off_f + loc : off_r + (loc - nf);
+      a.out.key[q] = st * a.nbx + (uint32_t)bk;
+      a.out.ent[q] = k;
+      a.out.pk[q] = make_uint2((uint32_t)xc, len);
+      a.out.nbd[q] = nbd_code_nw(xc, a.max_x);
+      a.out.state[q] = ST_UNKNOWN;
+    }
   }
-  if (s_bad && threadIdx.x == 0) atomicOr(&a.ctrl[7], 1u);
 }
 
 // Y states: X hits sit in the Y lists (commonFunctions.cpp:59), X misses query them
@@ -732,10 +730,24 @@ __global__ void __launch_bounds__(256) k_nw_assign(const uint32_t *__restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// widest digit of the record sorts (RK_NW_BITS=8..10 for measurements): 8-bit
+// digits measured fastest at cfg3 (a 16-B record pass 0.49 ms against 0.69 ms
+// at 9 bits and 1.44 ms at 10: wider digits leave fewer records per digit
+// segment of a tile and fewer resident tiles)
+int nw_max_bits() {
+  static const int v = [] {
+    const char *e = getenv("RK_NW_BITS");
+    const int b = e ? atoi(e) : 8;
+    return b < 8 ? 8 : b > 10 ? 10 : b;
+  }();
+  return v;
+}
+
 Digits plan_digits(int bits) {
   Digits D{};
   if (bits < 1) bits = 1;
-  D.passes = (bits + 9) / 10;
+  const int mb = nw_max_bits();
+  D.passes = (bits + mb - 1) / mb;
   int shift = 0;
   for (int p = 0; p < D.passes; ++p) {
     const int left = bits - shift, w0 = (left + (D.passes - p) - 1) / (D.passes - p);
@@ -747,30 +759,99 @@ Digits plan_digits(int bits) {
 }
 
 constexpr int OS_T = 256;
-int items_for(int db) { return db >= 10 ? 12 : 16; }
+int nw_shape();
+int items_for(int db) { return db >= 10 ? 12 : db == 8 && nw_shape() == 2 ? 8 : 16; }
 uint32_t tiles_for(uint32_t n, int db) {
   const uint32_t tile = OS_T * items_for(db);
   return (n + tile - 1) / tile;
 }
 
-template <int DB, class Src, class Dst, class Side>
-void launch_pass_db(const Src &src, const Dst &dst, const Side &side, uint32_t n, int shift,
-                    const uint32_t *ghist, uint32_t *status, uint32_t *ctr, hipStream_t st) {
-  constexpr int ITEMS = DB >= 10 ? 12 : 16;
-  const uint32_t tiles = (n + OS_T * ITEMS - 1) / (OS_T * ITEMS);
-  k_onesweep<OS_T, ITEMS, DB><<<tiles, OS_T, 0, st>>>(src, dst, side, n, shift, ghist, status,
-                                                       ctr);
+// RK_NW_TRACE=<file>: per-tile phase timestamps of every record pass, written
+// to <file> after each classification (measurement only)
+struct NwTrace {
+  uint64_t *buf = nullptr;
+  size_t cap = 0, used = 0;
+  std::vector<std::pair<size_t, uint32_t>> passes;  // (offset, tiles)
+};
+NwTrace &nw_trace() {
+  static NwTrace t;
+  return t;
 }
-template <class Src, class Dst, class Side>
-void launch_pass(const Src &src, const Dst &dst, const Side &side, uint32_t n, int shift, int db,
+const char *nw_trace_path() {
+  static const char *p = getenv("RK_NW_TRACE");
+  return p;
+}
+uint64_t *trace_slot(uint32_t tiles) {
+  if (!nw_trace_path()) return nullptr;
+  NwTrace &t = nw_trace();
+  if (!t.buf) {
+    t.cap = (size_t)8 << 20;  // words
+    if (hipMalloc(&t.buf, t.cap * 8) != hipSuccess) return t.buf = nullptr;
+  }
+  const size_t need = (size_t)tiles * 6;
+  if (t.used + need > t.cap) return nullptr;
+  uint64_t *p = t.buf + t.used;
+  t.passes.push_back({t.used, tiles});
+  t.used += need;
+  return p;
+}
+
+// persistent grid: as many blocks as stay resident (occupancy x CUs)
+template <class K>
+uint32_t resident_blocks(K kernel, int threads) {
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0);
+  const int b = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+  return (uint32_t)b;
+}
+
+// RK_NW_SHAPE (measurements): 0 = one tile of 4096 records per block
+// (default), 1 = persistent blocks, next tile's loads behind the look-back,
+// 2 = one tile of 2048 records per block (more resident blocks)
+int nw_shape() {
+  static const int v = [] {
+    const char *e = getenv("RK_NW_SHAPE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int ITEMS, int DB, bool PERSIST, class Src, class Dst>
+void launch_shape(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
+                  uint32_t *status, uint32_t *ctr, hipStream_t st) {
+  const uint32_t tiles = (n + OS_T * ITEMS - 1) / (OS_T * ITEMS);
+  auto kern = k_onesweep<OS_T, ITEMS, DB, PERSIST, Src, Dst>;
+  uint32_t grid = tiles;
+  if (PERSIST) {
+    static const uint32_t resident = resident_blocks(kern, OS_T);
+    grid = tiles < resident ? tiles : resident;
+  }
+  kern<<<grid, OS_T, 0, st>>>(src, dst, n, tiles, shift, ghist, status, ctr, trace_slot(tiles));
+}
+template <int DB, class Src, class Dst>
+void launch_pass_db(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
+                    uint32_t *status, uint32_t *ctr, hipStream_t st) {
+  constexpr int ITEMS = DB >= 10 ? 12 : 16;
+  const int shape = DB == 8 ? nw_shape() : 0;
+  if (shape == 1)
+    launch_shape<ITEMS, DB, true>(src, dst, n, shift, ghist, status, ctr, st);
+  else if (shape == 2)
+    launch_shape<8, DB, false>(src, dst, n, shift, ghist, status, ctr, st);
+  else
+    launch_shape<ITEMS, DB, false>(src, dst, n, shift, ghist, status, ctr, st);
+}
+template <class Src, class Dst>
+void launch_pass(const Src &src, const Dst &dst, uint32_t n, int shift, int db,
                  const uint32_t *ghist, uint32_t *status, uint32_t *ctr, hipStream_t st,
                  double bytes) {
   if (!n) return;
   kt_begin(st);
   switch (db) {
-    case 8: launch_pass_db<8>(src, dst, side, n, shift, ghist, status, ctr, st); break;
-    case 9: launch_pass_db<9>(src, dst, side, n, shift, ghist, status, ctr, st); break;
-    default: launch_pass_db<10>(src, dst, side, n, shift, ghist, status, ctr, st); break;
+    case 8: launch_pass_db<8>(src, dst, n, shift, ghist, status, ctr, st); break;
+    case 9: launch_pass_db<9>(src, dst, n, shift, ghist, status, ctr, st); break;
+    default: launch_pass_db<10>(src, dst, n, shift, ghist, status, ctr, st); break;
   }
   kt_end(st, KID_ONESWEEP, bytes);
 }
@@ -779,6 +860,28 @@ void launch_pass(const Src &src, const Dst &dst, const Side &side, uint32_t n, i
 
 // ===========================================================================
 // host side
+void nw_trace_dump(hipStream_t st) {
+  if (!nw_trace_path()) return;
+  NwTrace &t = nw_trace();
+  if (!t.buf || t.passes.empty()) return;
+  (void)hipStreamSynchronize(st);
+  std::vector<uint64_t> h(t.used);
+  if (hipMemcpy(h.data(), t.buf, t.used * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+    if (FILE *f = fopen(nw_trace_path(), "wb")) {
+      const uint64_t np = t.passes.size();
+      fwrite(&np, 8, 1, f);
+      for (auto &p : t.passes) {
+        const uint64_t hdr[2] = {p.first, p.second};
+        fwrite(hdr, 8, 2, f);
+      }
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+  }
+  t.used = 0;
+  t.passes.clear();
+}
+
 size_t nw_status_words(uint32_t n) {
   // the largest pass: tiles of 3072 records x 1024 digits, + per-pass tile counters
   return (size_t)((n + 3071) / 3072 + 1) * 1024 + 64;
@@ -799,21 +902,22 @@ static Digits to_digits(const NwDigits &o) {
   return D;
 }
 
-void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, const NwDigits &a, uint32_t *ghist,
-                   uint32_t *ctrl, hipStream_t st) {
+void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
+                   uint32_t nby, const NwDigits &a, const NwDigits &y, uint32_t *ghist,
+                   uint32_t *yhist, uint32_t *ctrl, hipStream_t st) {
   const uint32_t n = (uint32_t)in.n;
   if (!n) return;
+  OrderHistArgs args{in.x_start, in.y_start, in.length, in.strand, n, vsize, max_x, max_y, nby,
+                     to_digits(a), to_digits(y), ghist, yhist, ctrl};
   kt_begin(st);
-  k_nw_order_hist<<<grid_for(n, 256, 2048), 256, 0, st>>>(in.x_start, n, vsize, to_digits(a),
-                                                          ghist, ctrl);
-  kt_end(st, KID_NW_HIST, 8.0 * n);  // xStart read once
+  k_nw_order_hist<<<grid_for(n, 256, 2048), 256, 0, st>>>(args);
+  kt_end(st, KID_NW_HIST, 25.0 * n);  // the SoA read once
 }
 
 // the processing order: passes over records, the first one from the file SoA
-void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
-                   uint32_t nby, const NwDigits &a, const NwDigits &y, const uint32_t *ghist,
-                   uint32_t *yhist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
-                   uint32_t *ctrl, hipStream_t st) {
+void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
+                   const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
+                   hipStream_t st) {
   const uint32_t n = (uint32_t)in.n;
   const Digits D = to_digits(a);
   const size_t sw = nw_status_words(n);
@@ -827,20 +931,18 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint6
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     const bool last = p == D.passes - 1;
+    const DstProc dp{out, yrec, nby};
     if (p == 0) {
       SrcFile sf{in.x_start, in.y_start, in.length, in.strand, vsize};
-      SideFile side{to_digits(y), vsize - 1, max_x, max_y, nby, yhist, ctrl};
       if (last)
-        launch_pass(sf, DstProc{out, yrec, nby}, side, n, D.shift[p], D.db[p], gh, status, ctr,
-                    st, 25.0 * n + 32.0 * n);
+        launch_pass(sf, dp, n, D.shift[p], D.db[p], gh, status, ctr, st, 25.0 * n + 32.0 * n);
       else
-        launch_pass(sf, DstRec{out}, side, n, D.shift[p], D.db[p], gh, status, ctr, st,
+        launch_pass(sf, DstRec{out}, n, D.shift[p], D.db[p], gh, status, ctr, st,
                     25.0 * n + 16.0 * n);
     } else if (last) {
-      launch_pass(SrcRec{src}, DstProc{out, yrec, nby}, NoSide{}, n, D.shift[p], D.db[p], gh,
-                  status, ctr, st, 48.0 * n);
+      launch_pass(SrcRec{src}, dp, n, D.shift[p], D.db[p], gh, status, ctr, st, 48.0 * n);
     } else {
-      launch_pass(SrcRec{src}, DstRec{out}, NoSide{}, n, D.shift[p], D.db[p], gh, status, ctr, st,
+      launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, status, ctr, st,
                   32.0 * n);
     }
   }
@@ -861,11 +963,11 @@ static void nw_sort_records(const uint4 *in, uint4 *t0, uint4 *t1, uint32_t m, c
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     if (p == D.passes - 1) {
-      launch_pass(SrcRec{src}, fin, NoSide{}, m, D.shift[p], D.db[p], gh, status, ctr, st,
+      launch_pass(SrcRec{src}, fin, m, D.shift[p], D.db[p], gh, status, ctr, st,
                   16.0 * m + final_bytes);
     } else {
       uint4 *out = p % 2 == 0 ? t0 : t1;
-      launch_pass(SrcRec{src}, DstRec{out}, NoSide{}, m, D.shift[p], D.db[p], gh, status, ctr,
+      launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], gh, status, ctr,
                   st, 32.0 * m);
       src = out;
     }
@@ -887,25 +989,35 @@ void nw_member_sort(const uint4 *erec, uint4 *t0, uint4 *t1, uint32_t m, const N
 }
 
 uint32_t nw_chunk_width(uint32_t m, uint32_t nbx) {
-  // about XC_CAP / 3 entries per chunk on average, 128..1024 buckets
-  const double per_bucket = (double)m / (double)nbx;
-  uint32_t W = 128;
-  while (W < 1024 && per_bucket * (2 * W) <= XC_CAP / 3.0) W *= 2;
+  // about 256-512 rows per chunk (one batch of the chunk kernel), 64..1024 buckets
+  const double per_bucket = (double)m / (double)(nbx ? nbx : 1);
+  uint32_t W = 64;
+  while (W < 1024 && per_bucket * (2 * W) <= 64.0 * XC_SLOTS) W *= 2;
   return W;
 }
 
+uint32_t nw_chunks(uint32_t nbx, uint32_t W) { return (nbx + W - 1) / W; }
+
+void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st) {
+  (void)hipMemsetAsync(cc.cnts, 0, ((size_t)3 * cc.nch + 1) * 4, st);
+  if (!m) return;
+  kt_begin(st);
+  k_nw_xcount<<<(m + XN_T * XN_ITEMS - 1) / (XN_T * XN_ITEMS), XN_T, 0, st>>>(R, m, cc.lgW, cc.nch,
+                                                                             10 * cc.W, cc.cnts);
+  kt_end(st, KID_NW_XCOUNT, 16.0 * m);
+}
+
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
-                 uint32_t M0, Csr cx, uint4 *erec, uint32_t *status, uint32_t *ctrl,
-                 uint32_t W, hipStream_t st) {
+                 const uint32_t *xoff, Csr cx, uint4 *erec, uint32_t *ctrl, uint32_t W,
+                 hipStream_t st) {
   if (!m) return;
   uint32_t lgW = 0;
   while ((1u << lgW) < W) ++lgW;
-  const uint32_t nchunks = (nbx + W - 1) / W;
-  (void)hipMemsetAsync(status, 0, ((size_t)nchunks * 2 + 64) * 4, st);
-  XChunkArgs a{R, m, W, lgW, nchunks, (maxlen / 2 + 9) / 10, nbx, max_x, M0, cx, erec,
-               status, status + (size_t)nchunks * 2 + 32, ctrl};
+  const uint32_t nch = nw_chunks(nbx, W);
+  XChunkArgs a{R, m, W, lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx, erec, ctrl};
   kt_begin(st);
-  k_nw_xchunk<<<nchunks, XC_T, 0, st>>>(a);
+  k_nw_xchunk<<<(nch + XC_WAVES - 1) / XC_WAVES, 64 * XC_WAVES,
+                XC_WAVES * 2 * W * sizeof(uint32_t), st>>>(a);
   // records in (+ halo), X entries (key, id, packed record, code, state) and
   // member records out
   kt_end(st, KID_NW_XCHUNK, 16.0 * m + 18.0 * m + 16.0 * m);

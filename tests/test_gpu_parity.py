@@ -328,10 +328,10 @@ def test_pipeline_choice(gpu_ctx, generic_ctx):
 
 
 def test_dense_x_chunks(gpu_ctx):
-    """X chunks denser than their LDS list are placed bin range by bin range
-    (record pipeline); a single 100-bp bucket of one strand above the list
-    capacity hands the classification to the generic pipeline -- same output
-    either way."""
+    """Dense X chunks (record pipeline): a chunk's rows are streamed in
+    batches of 512 and its bins have no capacity limit, so even a single
+    100-bp bucket of one strand holding thousands of entries stays on the
+    record pipeline, bit-exact."""
     L = 30_000
     f = rk.synth(60_000, L, seed=63, family_frac=0.95, copies=(100, 600))
     gpu_vs_oracle(gpu_ctx, f, L, L)
@@ -345,7 +345,7 @@ def test_dense_x_chunks(gpu_ctx):
                  np.concatenate([f.strand, np.full(k, ord("f"), np.uint8)]))
     gpu_vs_oracle(gpu_ctx, g, L, L)
     st = gpu_ctx.stats()
-    assert st["pipeline"] == 2 and st["record_fallback"] == 2
+    assert st["pipeline"] == 1 and st["record_fallback"] == 0
 
 
 @pytest.mark.parametrize("pos", [1, 63, 65, 1000, 19_999])
