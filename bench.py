@@ -258,6 +258,44 @@ def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
     }
 
 
+def host_legs(ctx, x, y, ln, s, L, args) -> dict:
+    """rk_classify from host buffers: `steps` calls each with pageable (numpy)
+    and page-locked (pinned torch) buffers; per call the upload, device and
+    download times (rk_stats h2d_ms / device_ms / d2h_ms) and the whole call."""
+    n = x.shape[0]
+    out = {}
+    for kind in ("pageable", "pinned"):
+        pin = kind == "pinned"
+        cols = []
+        for t in (x, y, ln, s):
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+            h.copy_(t)
+            cols.append(h)
+        f = rk.Frags(*[c.numpy().view(np.uint64) if c.dtype == torch.int64 else c.numpy()
+                       for c in cols])
+        res = [torch.empty(n, dtype=dt, pin_memory=pin).numpy() for dt in
+               (torch.int32, torch.uint8, torch.int32)]
+        gid, rep, order = res[0].view(np.uint32), res[1], res[2].view(np.uint32)
+        ctx.classify_into(f, L, L, args.len_ratio, args.pos_ratio, gid, rep, order)  # warm-up
+        acc = {"h2d_ms": 0.0, "kernels_ms": 0.0, "d2h_ms": 0.0}
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.classify_into(f, L, L, args.len_ratio, args.pos_ratio, gid, rep, order)
+            st = ctx.stats()
+            acc["h2d_ms"] += st["h2d_ms"]
+            acc["kernels_ms"] += st["device_ms"]
+            acc["d2h_ms"] += st["d2h_ms"]
+        dt = time.perf_counter() - t0
+        out[kind] = {"fragments_per_s": round(n * args.steps / dt, 1),
+                     "ms_per_call": round(dt / args.steps * 1e3, 3),
+                     **{k: round(v / args.steps, 3) for k, v in acc.items()}}
+        del cols, f, res
+    out["steps"] = args.steps
+    out["note"] = ("host wall time per call; kernels_ms = HIP-event time of the device "
+                   "pipeline inside the call")
+    return out
+
+
 def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
     """rk_classify_device on this rank's own fragment set (inputs resident in HBM)."""
     n, L = cfg["n"], cfg["genome_len"]
@@ -278,16 +316,11 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
     st = ctx.stats()
     kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps)
 
-    # PCIe-inclusive rate (host buffers in and out), reported beside value, never as it
-    pcie = None
+    # host-to-host rate (host SoA in, host results out: rk_classify), reported
+    # beside value, never as it (SURVEY.md §8d's PCIe-inclusive timed region)
+    host = None
     if rank == 0 and args.config in ("cfg2", "cfg3", "cfg4"):  # cfg5: no HBM for a 2nd copy
-        fh = rk.Frags(x.cpu().numpy().view(np.uint64), y.cpu().numpy().view(np.uint64),
-                      ln.cpu().numpy().view(np.uint64), s.cpu().numpy())
-        ctx.classify(fh, L, L, args.len_ratio, args.pos_ratio)
-        t1 = time.perf_counter()
-        ctx.classify(fh, L, L, args.len_ratio, args.pos_ratio)
-        pcie = n / (time.perf_counter() - t1)
-
+        host = host_legs(ctx, x, y, ln, s, L, args)
     per_step = {k: v[0] / max(1, v[1]) for k, v in phases.items()}
     value = frags_total * args.steps / dt_max
     return {
@@ -314,7 +347,8 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
         "device_ms_per_step": round(st["device_ms"], 3),
         "groups": n_groups, "grouped_fragments": n_out,
         "sweeps": {"x": st["x_sweeps"], "y": st["y_sweeps"], "jump_rounds": st["jump_rounds"]},
-        "pcie_inclusive_fragments_per_s": round(pcie, 1) if pcie else None,
+        "pcie_inclusive_fragments_per_s": host["pageable"]["fragments_per_s"] if host else None,
+        "host_to_host": host,
     }
 
 

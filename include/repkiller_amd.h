@@ -93,6 +93,8 @@ typedef struct {
   uint32_t pipeline; /* the pipeline that produced the result: 1 record, 2 generic */
   uint32_t record_fallback; /* why the record pipeline handed over: 0 it did not, 1 a row
                                does not pack into a record */
+  double h2d_ms, d2h_ms;    /* rk_classify*: host wall time of the input upload and of the
+                               result download (0 for the device entry points) */
 } rk_stats;
 
 int rk_create(rk_ctx **ctx, int device);

@@ -86,7 +86,8 @@ class Stats(ctypes.Structure):
                 ("y_sweeps", ctypes.c_uint32), ("jump_rounds", ctypes.c_uint32),
                 ("x_hits", ctypes.c_uint64), ("y_hits", ctypes.c_uint64),
                 ("device_ms", ctypes.c_double), ("pipeline", ctypes.c_uint32),
-                ("record_fallback", ctypes.c_uint32)]
+                ("record_fallback", ctypes.c_uint32), ("h2d_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double)]
 
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -443,6 +444,26 @@ class Context:
             raise RkError(rc, self.last_error())
         k = res.n_out
         return ClassifyResult(gid[:k].copy(), rep[:k].copy(), order[:k].copy(), int(res.n_groups))
+
+    def classify_into(self, f: Frags, len_x_hdr: int, len_y_hdr: int, len_ratio: float,
+                      pos_ratio: float, gid: np.ndarray, rep: np.ndarray,
+                      order: np.ndarray) -> tuple:
+        """rk_classify into caller-owned host arrays (no copies; the arrays may
+        be page-locked, e.g. views of pinned torch tensors).  Returns
+        (n_out, n_groups)."""
+        n = f.n
+        for a, t in ((f.x_start, np.uint64), (f.y_start, np.uint64), (f.length, np.uint64),
+                     (f.strand, np.uint8), (gid, np.uint32), (rep, np.uint8), (order, np.uint32)):
+            if a.dtype != t or not a.flags.c_contiguous or a.shape[0] < n:
+                raise ValueError("classify_into: contiguous arrays of the ABI dtypes required")
+        soa = FragsSoA(_ptr(f.x_start), _ptr(f.y_start), _ptr(f.length), _ptr(f.strand), n)
+        res = Result(_ptr(order), _ptr(gid), _ptr(rep), 0, 0)
+        prm = Params(len_x_hdr, len_y_hdr, len_ratio, pos_ratio)
+        rc = load_library().rk_classify(self._h, ctypes.byref(soa), ctypes.byref(prm),
+                                        ctypes.byref(res))
+        if rc != RK_OK:
+            raise RkError(rc, self.last_error())
+        return int(res.n_out), int(res.n_groups)
 
     def classify_pairs(self, f: Frags, len_x_hdr: int, len_y_hdr: int,
                        pairs) -> list:

@@ -783,6 +783,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  rk::io_destroy(ctx);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->io) (void)hipFree(ctx->io);
   if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
@@ -960,28 +961,33 @@ extern "C" int rk_classify_pairs(rk_ctx *ctx, const rk_frags_soa *in, const rk_p
     uint32_t *dgid = c.take<uint32_t>(n), *dord = c.take<uint32_t>(n);
     dres[q] = rk_result{dord, dgid, drep, 0, 0};
   }
-  hipStream_t st = ctx->stream;
-  if (n) {
-    HIPCHK(ctx, hipMemcpyAsync(dx, in->x_start, n * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(dy, in->y_start, n * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(dl, in->length, n * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(ds, in->strand, n, hipMemcpyHostToDevice, st));
-  }
-  rk_frags_soa din{dx, dy, dl, ds, n};
-  int rc = rk_classify_device_pairs(ctx, &din, p, npairs, dres.data());
+  // 1: upload (copy stream; pinned buffers by DMA, pageable ones staged)
+  const double t0 = rk::wall_ms();
+  int rc = rk::io_h2d(ctx, {{(void *)in->x_start, dx, n * 8},
+                            {(void *)in->y_start, dy, n * 8},
+                            {(void *)in->length, dl, n * 8},
+                            {(void *)in->strand, ds, n}});
   if (rc) return rc;
+  const double t1 = rk::wall_ms();
+  // 2: classify
+  rk_frags_soa din{dx, dy, dl, ds, n};
+  rc = rk_classify_device_pairs(ctx, &din, p, npairs, dres.data());
+  if (rc) return rc;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  // 3: download
+  const double t2 = rk::wall_ms();
+  std::vector<rk::IoPiece> down;
   for (uint32_t q = 0; q < npairs; ++q) {
     out[q].n_out = dres[q].n_out;
     out[q].n_groups = dres[q].n_groups;
-    if (n && dres[q].n_out) {
-      const uint64_t k = dres[q].n_out;
-      HIPCHK(ctx, hipMemcpyAsync(out[q].out_order, dres[q].out_order, k * 4,
-                                 hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(out[q].gid, dres[q].gid, k * 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(out[q].repval, dres[q].repval, k, hipMemcpyDeviceToHost, st));
-    }
+    const size_t k = n ? dres[q].n_out : 0;
+    down.push_back({out[q].out_order, dres[q].out_order, k * 4});
+    down.push_back({out[q].gid, dres[q].gid, k * 4});
+    down.push_back({out[q].repval, dres[q].repval, k});
   }
-  if (n) HIPCHK(ctx, hipStreamSynchronize(st));
+  if ((rc = rk::io_d2h(ctx, down))) return rc;
+  ctx->stats.h2d_ms = t1 - t0;
+  ctx->stats.d2h_ms = rk::wall_ms() - t2;
   return RK_OK;
 }
 

@@ -11,6 +11,10 @@
 #include "../../include/repkiller_amd.h"
 #include "rk_internal.h"
 
+namespace rk {
+struct IoEngine;  // rk_io.hip: copy stream, pinned staging ring, host copy threads
+}
+
 // Grow-only device buffers of the sharded driver, one per slot (the exchange
 // sizes are only known mid-call, so they cannot share the single carve).
 struct rk_pool {
@@ -36,6 +40,7 @@ struct rk_ctx {
   // device copies for rk_classify (host-buffer entry point)
   void *io = nullptr;
   size_t io_cap = 0;
+  rk::IoEngine *ioe = nullptr;
   rk_pool pool;  // rk_classify_sharded buffers
   rk_stats stats{};
   rk_shard_stats shard_stats{};
@@ -77,6 +82,20 @@ struct Carve {
     return p;
   }
 };
+
+// rk_io.hip: host <-> device pieces of rk_classify on the copy stream
+// (pinned host buffers by DMA, pageable ones through the staging ring);
+// both return when the transfer is complete
+struct IoPiece {
+  void *host;
+  void *dev;
+  size_t bytes;
+};
+int io_h2d(rk_ctx *ctx, const std::vector<IoPiece> &pieces);
+int io_d2h(rk_ctx *ctx, const std::vector<IoPiece> &pieces);
+void io_destroy(rk_ctx *ctx);
+bool host_pinned(const void *p);
+double wall_ms();
 
 // copy `count` device words into ctx->host and wait
 int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count);

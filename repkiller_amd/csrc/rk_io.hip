@@ -1,0 +1,230 @@
+// rk_io.hip -- the host side of rk_classify: host buffers <-> HBM.
+//
+// The reference classifies fragments that live in host memory
+// (FragmentsDatabase, FragmentsDatabase.cpp:84-97) and writes host-side
+// results (save_frag_pair, commonFunctions.cpp:119-129).  rk_classify keeps
+// that boundary: caller-owned host SoA in, caller-owned host results out.
+//
+// Transfers run on a dedicated copy stream.  Page-locked caller buffers
+// (hipHostMalloc / hipHostRegister, e.g. the rk_db loader's columns) are
+// copied by DMA directly.  Pageable buffers go through a ring of pinned
+// staging slots: host threads copy chunk k into a free slot while the DMA
+// engine moves chunk k-1 (and, for results, the DMA of chunk k+NS overlaps the
+// host copy of chunk k out of its slot).  HIP's own pageable path stages
+// through one thread; the parallel host copy is what lifts it to PCIe rate.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "rk_ctx.h"
+
+namespace rk {
+
+// A fixed set of worker threads running one job at a time: job(t) on every
+// worker t in [0, n); run() returns when all have finished.
+class HostPool {
+ public:
+  explicit HostPool(int n) : n_(n) {
+    for (int t = 0; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  int size() const { return n_; }
+  void run(const std::function<void(int)> &job) {
+    std::unique_lock<std::mutex> g(mu_);
+    job_ = &job;
+    left_ = n_;
+    ++gen_;
+    cv_.notify_all();
+    done_.wait(g, [this] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)> *job;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        job = job_;
+      }
+      (*job)(t);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)> *job_ = nullptr;
+  uint64_t gen_ = 0;
+  int left_ = 0;
+  bool stop_ = false;
+};
+
+namespace {
+
+constexpr int NSLOT = 4;
+constexpr size_t SLOT = (size_t)32 << 20;
+
+int io_threads() {
+  const char *e = std::getenv("RK_IO_THREADS");
+  int n = e ? std::atoi(e) : 0;
+  if (n <= 0) {
+    const char *o = std::getenv("OMP_NUM_THREADS");  // the box's CPU share
+    n = o ? std::atoi(o) : 0;
+  }
+  if (n <= 0) n = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(n, 16));
+}
+
+// copy len bytes with every pool worker (pieces of at least 1 MiB)
+void par_copy(HostPool *pool, void *dst, const void *src, size_t len) {
+  const size_t piece = std::max<size_t>((len + pool->size() - 1) / pool->size(), (size_t)1 << 20);
+  const std::function<void(int)> job = [&](int t) {
+    const size_t a = (size_t)t * piece;
+    if (a >= len) return;
+    std::memcpy((char *)dst + a, (const char *)src + a, std::min(piece, len - a));
+  };
+  if (len <= piece) std::memcpy(dst, src, len);
+  else pool->run(job);
+}
+
+}  // namespace
+
+struct IoEngine {
+  hipStream_t io = nullptr;
+  char *slot[NSLOT] = {};
+  hipEvent_t ev[NSLOT] = {};
+  HostPool *pool = nullptr;
+  ~IoEngine() {
+    if (io) (void)hipStreamSynchronize(io);
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto &s : slot)
+      if (s) (void)hipHostFree(s);
+    if (io) (void)hipStreamDestroy(io);
+    delete pool;
+  }
+};
+
+void io_destroy(rk_ctx *ctx) {
+  delete ctx->ioe;
+  ctx->ioe = nullptr;
+}
+
+static int io_ready(rk_ctx *ctx) {
+  if (ctx->ioe) return RK_OK;
+  auto *e = new IoEngine;
+  ctx->ioe = e;
+  HIPCHK(ctx, hipStreamCreateWithFlags(&e->io, hipStreamNonBlocking));
+  for (int k = 0; k < NSLOT; ++k) {
+    HIPCHK(ctx, hipHostMalloc((void **)&e->slot[k], SLOT, hipHostMallocDefault));
+    HIPCHK(ctx, hipEventCreateWithFlags(&e->ev[k], hipEventDisableTiming));
+  }
+  e->pool = new HostPool(io_threads());
+  return RK_OK;
+}
+
+bool host_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // an unregistered pointer: pageable
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Host -> device for several (dst, src, bytes) pieces, one pipeline; returns
+// when the last byte has landed.
+int io_h2d(rk_ctx *ctx, const std::vector<IoPiece> &pieces) {
+  int rc = io_ready(ctx);
+  if (rc) return rc;
+  IoEngine &e = *ctx->ioe;
+  bool busy[NSLOT] = {};
+  int k = 0;
+  for (const IoPiece &pc : pieces) {
+    if (!pc.bytes) continue;
+    if (host_pinned(pc.host)) {
+      HIPCHK(ctx, hipMemcpyAsync(pc.dev, pc.host, pc.bytes, hipMemcpyHostToDevice, e.io));
+      continue;
+    }
+    for (size_t off = 0; off < pc.bytes; off += SLOT) {
+      const size_t len = std::min(SLOT, pc.bytes - off);
+      if (busy[k]) HIPCHK(ctx, hipEventSynchronize(e.ev[k]));
+      par_copy(e.pool, e.slot[k], (const char *)pc.host + off, len);
+      HIPCHK(ctx, hipMemcpyAsync((char *)pc.dev + off, e.slot[k], len, hipMemcpyHostToDevice,
+                                 e.io));
+      HIPCHK(ctx, hipEventRecord(e.ev[k], e.io));
+      busy[k] = true;
+      k = (k + 1) % NSLOT;
+    }
+  }
+  HIPCHK(ctx, hipStreamSynchronize(e.io));
+  return RK_OK;
+}
+
+// Device -> host: the DMA of up to NSLOT chunks runs ahead of the host copies
+// out of the slots.
+int io_d2h(rk_ctx *ctx, const std::vector<IoPiece> &pieces) {
+  int rc = io_ready(ctx);
+  if (rc) return rc;
+  IoEngine &e = *ctx->ioe;
+  struct Chunk {
+    void *host;
+    const void *dev;
+    size_t len;
+  };
+  std::vector<Chunk> ch;
+  for (const IoPiece &pc : pieces) {
+    if (!pc.bytes) continue;
+    if (host_pinned(pc.host)) {
+      HIPCHK(ctx, hipMemcpyAsync(pc.host, pc.dev, pc.bytes, hipMemcpyDeviceToHost, e.io));
+      continue;
+    }
+    for (size_t off = 0; off < pc.bytes; off += SLOT)
+      ch.push_back({(char *)pc.host + off, (const char *)pc.dev + off,
+                    std::min(SLOT, pc.bytes - off)});
+  }
+  const size_t nc = ch.size();
+  auto issue = [&](size_t i) -> int {
+    const int k = (int)(i % NSLOT);
+    HIPCHK(ctx, hipMemcpyAsync(e.slot[k], ch[i].dev, ch[i].len, hipMemcpyDeviceToHost, e.io));
+    HIPCHK(ctx, hipEventRecord(e.ev[k], e.io));
+    return RK_OK;
+  };
+  for (size_t i = 0; i < nc && i < (size_t)NSLOT; ++i)
+    if ((rc = issue(i))) return rc;
+  for (size_t i = 0; i < nc; ++i) {
+    const int k = (int)(i % NSLOT);
+    HIPCHK(ctx, hipEventSynchronize(e.ev[k]));
+    par_copy(e.pool, ch[i].host, e.slot[k], ch[i].len);
+    if (i + NSLOT < nc && (rc = issue(i + NSLOT))) return rc;
+  }
+  HIPCHK(ctx, hipStreamSynchronize(e.io));
+  return RK_OK;
+}
+
+double wall_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+}  // namespace rk
