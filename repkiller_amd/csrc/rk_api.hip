@@ -38,7 +38,7 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_emit",          "k_part (sharded)", "exchange (sharded)", "k_aux (sharded)",
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
     "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32", "k_nw_order_hist",
-    "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign", "k_nw_xcount",
+    "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign", "k_nw_xcount", "k_nw_x_bits",
 };
 }  // namespace rk
 
@@ -318,7 +318,7 @@ struct NWork {
   uint32_t *astatus, *ystatus, *xcnt, *xoff;
   uint4 *Ra, *Rb, *yrec, *erec;
   rk::Csr cx, cy;
-  uint8_t *xhit;
+  uint32_t *xpos, *xbits;
   uint32_t *par, *isnew, *newrank, *sgid, *tag, *otag, *mrow, *goff;
   uint64_t *reckey;
   void *gsort;
@@ -352,7 +352,8 @@ size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
     cs->pk = c.take<uint2>(n);
     cs->nbd = c.take<uint8_t>(n);
   }
-  w.xhit = c.take<uint8_t>(n);
+  w.xpos = c.take<uint32_t>(n);
+  w.xbits = c.take<uint32_t>(n / 32 + 2);
   w.par = c.take<uint32_t>(n);
   w.isnew = c.take<uint32_t>(n);
   w.newrank = c.take<uint32_t>(n);
@@ -466,7 +467,8 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   rk::nw_y_sort(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y, st2);
   HIPCHK(ctx, hipEventRecord(ctx->join, st2));
   mark(ctx, RK_PH_GATHER);
-  rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, w.xoff, w.cx, w.erec, w.ctrl, cc.W, st);
+  rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, w.xoff, w.cx, w.xpos, w.erec, w.ctrl, cc.W,
+                  st);
   HIPCHK(ctx, hipGetLastError());
   mark(ctx, RK_PH_OCC_CSR);
   rk::SweepScratch sc{w.runs, w.wpend, reinterpret_cast<uint8_t *>(w.rpend), w.ctrl + 64,
@@ -477,7 +479,8 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     const bool prof = q == 0;
     if (q > 0) HIPCHK(ctx, hipMemsetAsync(w.cx.state, rk::ST_UNKNOWN, m, st));
     if (prof) mark(ctx, RK_PH_SWEEP_X);
-    rk::Axis ax{w.cx.key, w.cx.ent, nullptr, nullptr, w.cx.state, nullptr, w.xhit, w.par,
+    // X decisions: hits' parents (X winner); the X states become a bitmask after
+    rk::Axis ax{w.cx.key, w.cx.ent, nullptr, nullptr, w.cx.state, nullptr, w.par,
                 w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
                 pq.pos_ratio};
     uint32_t sweeps = 0;
@@ -485,8 +488,9 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     ctx->stats.x_sweeps = sweeps;
     if (prof) mark(ctx, RK_PH_SWEEP_Y);
     if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
-    rk::nw_fill_y(w.cy.ent, w.xhit, w.cy.state, m, st);
-    rk::Axis ay{w.cy.key, w.cy.ent, nullptr, nullptr, w.cy.state, nullptr, nullptr, w.par,
+    rk::nw_x_bits(w.xpos, w.cx.state, m, w.xbits, st);
+    rk::nw_fill_y(w.cy.ent, w.xbits, w.cy.state, m, st);
+    rk::Axis ay{w.cy.key, w.cy.ent, nullptr, nullptr, w.cy.state, nullptr, w.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
     if ((rc = rk::resolve_axis(ctx, ay, sc, true, &sweeps))) return rc;
@@ -665,7 +669,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (prof) mark(ctx, RK_PH_SWEEP_X);
     // X decisions write X results into the Y records and X hits' parents
     rk::Axis ax{w.cx.key, w.cx.ent, w.cx.cen, w.cx.len, w.cx.state,
-                reinterpret_cast<uint32_t *>(w.p.yrec), nullptr, w.p.par,
+                reinterpret_cast<uint32_t *>(w.p.yrec), w.p.par,
                 w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
                 pq.pos_ratio};
     uint32_t sweeps = 0;
@@ -675,7 +679,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
     rk::csr_fill_y(w.cy, w.p.yrec, w.p.ylenhi, m, pl.max_y, st);
     // X misses: the Y sweeps write parent = Y winner, or itself (new group)
-    rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, nullptr, nullptr, w.p.par,
+    rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, nullptr, w.p.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
     if ((rc = rk::resolve_axis(ctx, ay, sweep_scratch(w), fast32, &sweeps))) return rc;

@@ -59,7 +59,7 @@ enum KernelId : int {
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
   KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_NW_HIST,
-  KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_COUNT
+  KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_NW_XBITS, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 struct KernelTimer {
@@ -108,8 +108,6 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   uint8_t *state;      // ST_*
   uint32_t *xres;      // X axis only: the Y records as 32-bit words; word 4k+3 of
                        // entry k receives its X result (winner id, or NONE)
-  uint8_t *xhit;       // X axis, record pipeline (rk_narrow.hip): 1 = X hit, by processing
-                       // index (instead of xres)
   uint32_t *par;       // parent by processing index: X hits -> X winner; Y axis
                        // (X misses) -> Y winner, or itself for a new group
   const uint2 *pk;     // {centre low 32, length low 32}: the 32-bit sweep's record
@@ -251,9 +249,13 @@ void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t
 void nw_y_sort(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y, const uint32_t *yhist,
                uint32_t *status, Csr cy, uint32_t nby, uint64_t max_y, hipStream_t st);
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
-                 const uint32_t *xoff, Csr cx, uint4 *erec, uint32_t *ctrl, uint32_t W,
-                 hipStream_t st);
-void nw_fill_y(const uint32_t *ent, const uint8_t *xhit, uint8_t *state, uint32_t m,
+                 const uint32_t *xoff, Csr cx, uint32_t *xpos, uint4 *erec, uint32_t *ctrl,
+                 uint32_t W, hipStream_t st);
+// X hits as a bitmask by processing index, from the resolved X axis (xpos[k] =
+// X position of fragment k); then the Y states: X hits sit in the Y lists
+void nw_x_bits(const uint32_t *xpos, const uint8_t *xstate, uint32_t m, uint32_t *bits,
+               hipStream_t st);
+void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32_t m,
                hipStream_t st);
 void nw_assign(const uint32_t *par, const uint32_t *newrank, uint4 *erec, uint32_t m,
                const NwDigits &e, uint32_t *ehist, hipStream_t st);

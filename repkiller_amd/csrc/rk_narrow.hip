@@ -169,8 +169,11 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
                                                 uint32_t *__restrict__ status,
                                                 uint32_t *__restrict__ tile_ctr,
                                                 uint64_t *__restrict__ trace) {
-  constexpr int RADIX = 1 << DB, NW = T / 64, TILE = T * ITEMS, DPT = RADIX / T;
-  static_assert(RADIX % T == 0, "whole digits per thread");
+  // thread t < RADIX / DPT owns digits [t*DPT, (t+1)*DPT)
+  constexpr int RADIX = 1 << DB, NW = T / 64, TILE = T * ITEMS;
+  constexpr int DPT = RADIX >= T ? RADIX / T : 1, OWNERS = RADIX / DPT;
+  static_assert(RADIX % T == 0 || T % RADIX == 0, "whole digits per thread");
+  const bool owner = (int)threadIdx.x < OWNERS;
   __shared__ uint4 srec[TILE];
   __shared__ uint32_t wcnt[NW][RADIX];  // per-wave digit counters, then per-wave starts
   __shared__ uint32_t lbase[RADIX];     // tile-local start of digit d
@@ -185,7 +188,7 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
   {
     uint32_t g[DPT], gs = 0;
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) g[j] = ghist[threadIdx.x * DPT + j], gs += g[j];
+    for (int j = 0; j < DPT; ++j) g[j] = owner ? ghist[threadIdx.x * DPT + j] : 0u, gs += g[j];
     uint32_t inc = gs;
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t o = __shfl_up(inc, off);
@@ -195,8 +198,9 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     __syncthreads();
     uint32_t at = inc - gs;
     for (int k2 = 0; k2 < w; ++k2) at += wsum[k2];
+    if (owner)
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) gbase[threadIdx.x * DPT + j] = at, at += g[j];
+      for (int j = 0; j < DPT; ++j) gbase[threadIdx.x * DPT + j] = at, at += g[j];
   }
   __syncthreads();
   uint32_t tile = s_tile[0];
@@ -249,6 +253,8 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     uint32_t run[DPT], tsum = 0;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
+      run[j] = 0;
+      if (!owner) continue;
       const uint32_t d = threadIdx.x * DPT + j;
       uint32_t r0 = 0;
 #pragma unroll
@@ -271,8 +277,9 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     {
       uint32_t at = inc - tsum;
       for (int k2 = 0; k2 < w; ++k2) at += wsum[k2];
+      if (owner)
 #pragma unroll
-      for (int j = 0; j < DPT; ++j) lbase[threadIdx.x * DPT + j] = at, at += run[j];
+        for (int j = 0; j < DPT; ++j) lbase[threadIdx.x * DPT + j] = at, at += run[j];
     }
     __syncthreads();
 #pragma unroll
@@ -292,11 +299,12 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
         rec[r] = i < ncnt ? src.load(n0 + i) : make_uint4(0, 0, 0, 0);
       }
     }
+    if (owner)
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) {
-      const uint32_t d = threadIdx.x * DPT + j;
-      gpos[d] = gbase[d] + (tile ? look_back(status, tile, RADIX, d, run[j]) : 0u);
-    }
+      for (int j = 0; j < DPT; ++j) {
+        const uint32_t d = threadIdx.x * DPT + j;
+        gpos[d] = gbase[d] + (tile ? look_back(status, tile, RADIX, d, run[j]) : 0u);
+      }
     __syncthreads();
     const uint64_t tr2 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     // 4: write-out (the next iteration's LDS writes follow its first barrier,
@@ -570,6 +578,7 @@ struct XChunkArgs {
   uint32_t nbx;
   const uint32_t *xoff;  // [2 nch] strand-major entry offsets, [nch + 1] owner row starts (+ m)
   Csr out;
+  uint32_t *xpos;        // X position of every fragment (processing index)
   uint4 *erec;           // member records (processing order)
   uint32_t *ctrl;        // [6] some sort key >= 2^32
 };
@@ -700,15 +709,33 @@ __global__ void __launch_bounds__(64 * XC_WAVES) k_nw_xchunk(XChunkArgs a) {
       a.out.pk[q] = make_uint2((uint32_t)xc, len);
       a.out.nbd[q] = nbd_code_nw(xc, a.max_x);
       a.out.state[q] = ST_UNKNOWN;
+      a.xpos[k] = q;
     }
   }
 }
 
-// Y states: X hits sit in the Y lists (commonFunctions.cpp:59), X misses query them
-__global__ void k_nw_fill_y(const uint32_t *__restrict__ ent, const uint8_t *__restrict__ xhit,
+// X hits as a bitmask by processing index, a wave per 64 fragments (their X
+// positions are a narrow window of the X axis: the state reads stay local)
+__global__ void k_nw_x_bits(const uint32_t *__restrict__ xpos, const uint8_t *__restrict__ xstate,
+                            uint32_t m, uint32_t *__restrict__ bits) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k - lane < m;
+       k += gridDim.x * blockDim.x) {
+    const bool hit = k < m && xstate[xpos[k]] == ST_HIT;
+    const uint64_t b = __ballot(hit);
+    if (lane == 0) bits[k >> 5] = (uint32_t)b;
+    if (lane == 32 && k < m) bits[k >> 5] = (uint32_t)(b >> 32);
+  }
+}
+
+// Y states: X hits sit in the Y lists (commonFunctions.cpp:59), X misses query
+// them; the 6-MB bitmask (cfg3) is served from L2 / Infinity Cache
+__global__ void k_nw_fill_y(const uint32_t *__restrict__ ent, const uint32_t *__restrict__ bits,
                             uint8_t *__restrict__ state, uint32_t m) {
-  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += gridDim.x * blockDim.x)
-    state[q] = xhit[ent[q]] ? ST_ACTIVE : ST_UNKNOWN;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < m; q += gridDim.x * blockDim.x) {
+    const uint32_t e = ent[q];
+    state[q] = (bits[e >> 5] >> (e & 31)) & 1u ? ST_ACTIVE : ST_UNKNOWN;
+  }
 }
 
 // gid of every member (its root's rank among new groups) into its record,
@@ -760,9 +787,18 @@ Digits plan_digits(int bits) {
 
 constexpr int OS_T = 256;
 int nw_shape();
-int items_for(int db) { return db >= 10 ? 12 : db == 8 && nw_shape() == 2 ? 8 : 16; }
+// records per tile of a pass with DB-bit digits (the shape of launch_pass_db)
+uint32_t tile_records(int db) {
+  if (db != 8) return OS_T * (db >= 10 ? 12 : 16);
+  switch (nw_shape()) {
+    case 2: return 256 * 8;
+    case 3: return 256 * 12;
+    case 5: return 512 * 16;
+    default: return 4096;  // 0, 1: 256 x 16; 4: 512 x 8
+  }
+}
 uint32_t tiles_for(uint32_t n, int db) {
-  const uint32_t tile = OS_T * items_for(db);
+  const uint32_t tile = tile_records(db);
   return (n + tile - 1) / tile;
 }
 
@@ -807,40 +843,47 @@ uint32_t resident_blocks(K kernel, int threads) {
   return (uint32_t)b;
 }
 
-// RK_NW_SHAPE (measurements): 0 = one tile of 4096 records per block
-// (default), 1 = persistent blocks, next tile's loads behind the look-back,
-// 2 = one tile of 2048 records per block (more resident blocks)
+// RK_NW_SHAPE (measurements; 8-bit digits): 0 = 256 threads x 16 records per
+// block, one tile each; 1 = the same, persistent blocks, the next tile's loads
+// issued before the look-back; 2 = 256 x 8; 3 = 256 x 12; 4 = 512 x 8
+// (default); 5 = 512 x 16.  cfg3 step, two streams: 13.75 / - / 14.39 / - /
+// 13.28 / 13.49 ms (shape 1 was slower: the look-back's loads queue behind the
+// next tile's in the same wave's memory counter)
 int nw_shape() {
   static const int v = [] {
     const char *e = getenv("RK_NW_SHAPE");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 4;
   }();
   return v;
 }
 
-template <int ITEMS, int DB, bool PERSIST, class Src, class Dst>
+template <int T, int ITEMS, int DB, bool PERSIST, class Src, class Dst>
 void launch_shape(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
                   uint32_t *status, uint32_t *ctr, hipStream_t st) {
-  const uint32_t tiles = (n + OS_T * ITEMS - 1) / (OS_T * ITEMS);
-  auto kern = k_onesweep<OS_T, ITEMS, DB, PERSIST, Src, Dst>;
+  const uint32_t tiles = (n + T * ITEMS - 1) / (T * ITEMS);
+  auto kern = k_onesweep<T, ITEMS, DB, PERSIST, Src, Dst>;
   uint32_t grid = tiles;
   if (PERSIST) {
-    static const uint32_t resident = resident_blocks(kern, OS_T);
+    static const uint32_t resident = resident_blocks(kern, T);
     grid = tiles < resident ? tiles : resident;
   }
-  kern<<<grid, OS_T, 0, st>>>(src, dst, n, tiles, shift, ghist, status, ctr, trace_slot(tiles));
+  kern<<<grid, T, 0, st>>>(src, dst, n, tiles, shift, ghist, status, ctr, trace_slot(tiles));
 }
 template <int DB, class Src, class Dst>
 void launch_pass_db(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
                     uint32_t *status, uint32_t *ctr, hipStream_t st) {
   constexpr int ITEMS = DB >= 10 ? 12 : 16;
-  const int shape = DB == 8 ? nw_shape() : 0;
-  if (shape == 1)
-    launch_shape<ITEMS, DB, true>(src, dst, n, shift, ghist, status, ctr, st);
-  else if (shape == 2)
-    launch_shape<8, DB, false>(src, dst, n, shift, ghist, status, ctr, st);
-  else
-    launch_shape<ITEMS, DB, false>(src, dst, n, shift, ghist, status, ctr, st);
+  if constexpr (DB == 8) {
+    switch (nw_shape()) {
+      case 1: launch_shape<OS_T, 16, 8, true>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 2: launch_shape<256, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 3: launch_shape<256, 12, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 4: launch_shape<512, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 5: launch_shape<512, 16, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      default: break;
+    }
+  }
+  launch_shape<OS_T, ITEMS, DB, false>(src, dst, n, shift, ghist, status, ctr, st);
 }
 template <class Src, class Dst>
 void launch_pass(const Src &src, const Dst &dst, uint32_t n, int shift, int db,
@@ -1008,27 +1051,35 @@ void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t
 }
 
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
-                 const uint32_t *xoff, Csr cx, uint4 *erec, uint32_t *ctrl, uint32_t W,
-                 hipStream_t st) {
+                 const uint32_t *xoff, Csr cx, uint32_t *xpos, uint4 *erec, uint32_t *ctrl,
+                 uint32_t W, hipStream_t st) {
   if (!m) return;
   uint32_t lgW = 0;
   while ((1u << lgW) < W) ++lgW;
   const uint32_t nch = nw_chunks(nbx, W);
-  XChunkArgs a{R, m, W, lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx, erec, ctrl};
+  XChunkArgs a{R, m, W, lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx, xpos, erec, ctrl};
   kt_begin(st);
   k_nw_xchunk<<<(nch + XC_WAVES - 1) / XC_WAVES, 64 * XC_WAVES,
                 XC_WAVES * 2 * W * sizeof(uint32_t), st>>>(a);
-  // records in (+ halo), X entries (key, id, packed record, code, state) and
-  // member records out
-  kt_end(st, KID_NW_XCHUNK, 16.0 * m + 18.0 * m + 16.0 * m);
+  // records in (+ halo), X entries (key, id, packed record, code, state), their
+  // positions by fragment and member records out
+  kt_end(st, KID_NW_XCHUNK, 16.0 * m + 22.0 * m + 16.0 * m);
 }
 
-void nw_fill_y(const uint32_t *ent, const uint8_t *xhit, uint8_t *state, uint32_t m,
+void nw_x_bits(const uint32_t *xpos, const uint8_t *xstate, uint32_t m, uint32_t *bits,
                hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_nw_fill_y<<<grid_for(m, 256), 256, 0, st>>>(ent, xhit, state, m);
-  kt_end(st, KID_NW_FILLY, 6.0 * m);
+  k_nw_x_bits<<<grid_for(m, 256), 256, 0, st>>>(xpos, xstate, m, bits);
+  kt_end(st, KID_NW_XBITS, 5.0 * m);
+}
+
+void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32_t m,
+               hipStream_t st) {
+  if (!m) return;
+  kt_begin(st);
+  k_nw_fill_y<<<grid_for(m, 256), 256, 0, st>>>(ent, bits, state, m);
+  kt_end(st, KID_NW_FILLY, 5.0 * m);
 }
 
 void nw_assign(const uint32_t *par, const uint32_t *newrank, uint4 *erec, uint32_t m,

@@ -111,10 +111,7 @@ __device__ __forceinline__ void store_state(uint8_t *s, uint8_t v) { *s = v; }
 // winner, or i itself -- a new group (:63-76).
 __device__ __forceinline__ void record_decision(const Axis &ax, uint32_t i, uint8_t st,
                                                 uint32_t win) {
-  if (ax.xhit) {  // record pipeline: one X-hit byte per fragment
-    ax.xhit[i] = st == ST_HIT;
-    if (st == ST_HIT) ax.par[i] = win;
-  } else if (ax.xres) {
+  if (ax.xres) {
     ax.xres[4 * (size_t)i + 3] = st == ST_HIT ? win : NONE;
     if (st == ST_HIT) ax.par[i] = win;
   } else {

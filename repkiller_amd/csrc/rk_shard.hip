@@ -924,7 +924,7 @@ uint32_t sweep_axis(Shard &S, const AxisIn &a, const Csr &c, const rk_params &p)
   if (a.is_x) csr_fill_x(c, a.rec, n, a.max_index, S.st);
   else csr_fill_y(c, a.rec, a.ylenhi, n, a.max_index, S.st);
   S.launched("axis csr");
-  Axis ax{c.key, c.ent, c.cen, c.len, c.state, a.xres, nullptr, a.par, c.pk, c.nbd,
+  Axis ax{c.key, c.ent, c.cen, c.len, c.state, a.xres, a.par, c.pk, c.nbd,
           S.take<uint32_t>(SL_RLEN, n), S.take<uint32_t>(SL_RBEG, n), n, a.max_index,
           p.len_ratio, p.pos_ratio};
   SweepScratch sc{S.take<uint32_t>(SL_RUNS, runs_scratch_words(n)),
