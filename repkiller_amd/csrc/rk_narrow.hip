@@ -57,9 +57,11 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 // through that tile, stop), then publish this tile's inclusive prefix.  Tile
 // ids come from an atomic counter in dispatch order, so every earlier tile is
 // resident or done and publishes its AGG before it waits on anything.
-// The walk reads LB_BATCH predecessors per round trip: with hundreds of tiles
-// resident, the nearest INC is often hundreds of tiles back, and one
-// dependent load per tile made the look-back the slowest part of a pass.
+// The walk reads LB_BATCH predecessors per round trip (hundreds of tiles are
+// resident; the nearest INC is often dozens back).  Measured per tile at cfg3
+// (RK_NW_TRACE): the look-back is ~9-10 us of ~16 us at 32; 64 reads per round
+// trip made it 13 us (the status traffic itself), a wave per digit reading 64
+// tiles per load (status[digit][tile]) 36-47 us.
 constexpr uint32_t LB_BATCH = 32;
 __device__ __forceinline__ uint32_t look_back(uint32_t *status, uint32_t tile, uint32_t stride,
                                               uint32_t slot, uint32_t mine) {
@@ -299,12 +301,13 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
         rec[r] = i < ncnt ? src.load(n0 + i) : make_uint4(0, 0, 0, 0);
       }
     }
-    if (owner)
+    if (owner) {
 #pragma unroll
       for (int j = 0; j < DPT; ++j) {
         const uint32_t d = threadIdx.x * DPT + j;
         gpos[d] = gbase[d] + (tile ? look_back(status, tile, RADIX, d, run[j]) : 0u);
       }
+    }
     __syncthreads();
     const uint64_t tr2 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     // 4: write-out (the next iteration's LDS writes follow its first barrier,
