@@ -8,15 +8,15 @@ flag and output order in HBM (the reference's generate_fragment_groups +
 generate_diagonal_func + sort_groups + repeat flag, commonFunctions.cpp:41-177).
 
 Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one process per GPU.
-`value` (default `--mode replicas`): every rank classifies its OWN independent
-50M-fragment set -- independent comparisons share nothing, so there is no
-data-path collective (weak scaling).  The same run then measures the `sharded`
-leg: ONE fragment set of 50M x N fragments over the 3 Gbp genome (rank r holds
-rows [r*50M, (r+1)*50M); at N=4 this is cfg4's 200M) classified by
-rk_classify_sharded with RCCL all-to-alls over xGMI (xStart/10 slices, X/Y
-halo exchange, cross-slice roots, gid-range member sort; DESIGN.md
-"Multi-GPU").  `--mode sharded` makes that leg the `value`.  A gloo barrier
-brackets every timed region and the max time over ranks is reported.
+`value` at N>1 (default `--mode auto`): ONE fragment set of 50M x N fragments
+over the 3 Gbp genome (rank r holds rows [r*50M, (r+1)*50M), each block seeded
+3+r) classified by rk_classify_sharded with RCCL all-to-alls over xGMI
+(xStart/10 slices, X/Y halo exchange, cross-slice roots, gid-range member sort;
+DESIGN.md "Multi-GPU") -- weak scaling.  The same run first measures
+`replicas`: every rank classifies its own independent 50M set (no data-path
+collective), reported beside the value (and as the value if the sharded leg
+fails, with the error).  A gloo barrier brackets every timed region and the
+max time over ranks is reported.
 
 Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the kernel with the
 most device time per step (algorithmic bytes per launch / HIP-event launch time
@@ -153,18 +153,22 @@ def cpu_baseline(cfg: dict, seconds_hint: float) -> dict | None:
                       f"generate_diagonal_func + sort_groups ({hot:.2f} s); host: {cpu}"}
 
 
-def load_traffic(kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py)."""
+def load_traffic(kernel: str, config: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (tools/pmc_run.sh -> profiles/traffic.json), only when they were measured on
+    this run's config; otherwise None (not measured for this workload)."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as fh:
             t = json.load(fh)
-        return t.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    if t.get("config") != config:
+        return None
+    return t.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
 
 
-def roofline_of(kt: dict, steps: int):
+def roofline_of(kt: dict, steps: int, config: str):
     """Per-kernel HIP-event timing (inside the timed steps, on the library's
     stream) -> the `kernels` table and the roofline of the kernel with the most
     device time per step."""
@@ -183,7 +187,7 @@ def roofline_of(kt: dict, steps: int):
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic(dom), "kernel": dom,
+                "traffic": load_traffic(dom, config), "kernel": dom,
                 "algorithmic_bytes_per_launch": round(bytes_per_launch),
                 "launch_ms": round(launch_ms, 4),
                 "launches_per_step": round(d["launches"] / steps, 2),
@@ -239,7 +243,8 @@ def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
     frags_total, dt_max = aggregate(world, n, dt)
     st = rk.shard_stats(ctx)
     sent = allsum(world, float(st["bytes_sent"]))
-    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps)
+    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps,
+                                    f"{args.config}-sharded-x{world}")
     comm.close()
     value = frags_total * args.steps / dt_max
     n_all = int(frags_total)
@@ -248,7 +253,9 @@ def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
         "ms_per_step": round(dt_max / args.steps * 1e3, 3),
         "scaling": "strong" if total else "weak",
         "workload": (f"ONE {n_all}-fragment set over a {L} bp genome, sharded over {world} GPUs"
-                     + ("" if total else f" ({n} fragments per GPU; N=4 is cfg4's 200M)")),
+                     + (f" ({world} independently seeded blocks of ~{n} rows, cfg's size and "
+                        f"genome; not the single-seed set of the one-GPU {args.config} run)"
+                        if total else f" ({n} fragments per GPU; N=4 is cfg4's size)")),
         "fragments_total": n_all, "comm": args.comm,
         "hbm_algorithmic_GBps": round(50 * value / 1e9, 3),
         "roofline": roofline, "kernels": kernels,
@@ -314,7 +321,7 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
     frags_total, dt_max = aggregate(world, n, dt)
     phases = ctx.phases()
     st = ctx.stats()
-    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps)
+    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps, args.config)
 
     # host-to-host rate (host SoA in, host results out: rk_classify), reported
     # beside value, never as it (SURVEY.md §8d's PCIe-inclusive timed region)
@@ -361,10 +368,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--len-ratio", type=float, default=0.3)
     ap.add_argument("--pos-ratio", type=float, default=0.3)
-    ap.add_argument("--mode", default="replicas", choices=["replicas", "sharded"],
-                    help="what `value` measures at N>1 (N=1 is always the single-GPU path "
-                         "unless --mode sharded)")
-    ap.add_argument("--no-sharded", action="store_true", help="skip the sharded leg at N>1")
+    ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "sharded"],
+                    help="auto: N=1 the single-GPU path, N>1 one fragment set sharded over the "
+                         "GPUs (independent replicas beside it, and the value if the sharded "
+                         "leg fails); replicas / sharded: that leg only")
     ap.add_argument("--sharded-timeout", type=float, default=240.0,
                     help="seconds the sharded leg may take before the line is printed without it")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
@@ -379,9 +386,8 @@ def main():
     torch.cuda.set_device(dev)
     ctx = rk.Context(local)
 
-    if args.mode == "sharded":
-        sh = bench_sharded(args, cfg, rank, world, local, dev, ctx)
-        line = {"metric": METRIC, "value": sh["value"], "unit": "fragments/s", "n_gpus": world,
+    def sharded_line(sh: dict) -> dict:
+        return {"metric": METRIC, "value": sh["value"], "unit": "fragments/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": sh["ms_per_step"],
                 "higher_is_better": True, "scaling": sh["scaling"], "vs_baseline": None,
                 "dtype": "u64/f64",
@@ -391,14 +397,19 @@ def main():
                            "fragments_per_gpu": sh["fragments_total"] // world,
                            "genome_bp": cfg["genome_len"], "len_ratio": args.len_ratio,
                            "pos_ratio": args.pos_ratio,
-                           "parallelism": f"sharded x{world} ({args.comm})"},
+                           "parallelism": f"sharded x{world} ({args.comm}): xStart/10 slices"},
                 "hbm_algorithmic_GBps": sh["hbm_algorithmic_GBps"],
                 "roofline": sh["roofline"], "sharded": sh}
+
+    if args.mode == "sharded":
+        line = sharded_line(bench_sharded(args, cfg, rank, world, local, dev, ctx))
     else:
         line = bench_single(args, cfg, rank, world, dev, ctx)
-        if world > 1 and not args.no_sharded:
-            # every rank arms the same watchdog: a stuck collective must not cost the
-            # contract line measured above
+        if world > 1 and args.mode == "auto":
+            # N > 1: the value is ONE comparison sharded over the GPUs (xStart/10
+            # slices, RCCL exchanges); the independent replicas measured above
+            # stay beside it.  Every rank arms the same watchdog: a stuck
+            # collective must not cost the line.
             import threading
 
             def give_up():
@@ -411,10 +422,18 @@ def main():
             dog.daemon = True
             dog.start()
             try:
-                line["sharded"] = bench_sharded(args, cfg, rank, world, local, dev, ctx)
-            except Exception as e:  # noqa: BLE001 -- reported, the contract line stands
-                line["sharded"] = {"error": repr(e)}
+                sh = bench_sharded(args, cfg, rank, world, local, dev, ctx)
+            except Exception as e:  # noqa: BLE001 -- reported; the replicas line stands
+                sh = {"error": repr(e)}
             dog.cancel()
+            if "error" in sh:
+                line["sharded"] = sh
+            else:
+                replicas = {k: line[k] for k in ("value", "ms_per_step", "scaling", "roofline",
+                                                 "phases_ms", "data")}
+                replicas["parallelism"] = line["config"]["parallelism"]
+                line = sharded_line(sh)
+                line["replicas"] = replicas
     if rank != 0:
         return
     if not args.no_cpu and world == 1:

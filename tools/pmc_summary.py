@@ -27,7 +27,13 @@ def load(d):
     return agg
 
 def main():
-    args = [a for a in sys.argv[1:] if a != "--write"]
+    config = "cfg3"  # the bench config the PMC passes ran (bench.py --config)
+    argv = sys.argv[1:]
+    if "--config" in argv:
+        i = argv.index("--config")
+        config = argv[i + 1]
+        del argv[i:i + 2]
+    args = [a for a in argv if a != "--write"]
     d = args[0] if args else "gpurun_out/pmc"
     agg = load(d)
     out = {}
@@ -58,7 +64,8 @@ def main():
                           "streaming read)",
                 "command": " ".join(args[1:]) or "python3 bench.py --no-cpu --steps 3 --warmup 1"}
         with open("profiles/traffic.json", "w") as f:
-            json.dump({"meta": meta, "kernels": out}, f, indent=1, sort_keys=True)
+            json.dump({"meta": meta, "config": config, "kernels": out}, f, indent=1,
+                      sort_keys=True)
 
 if __name__ == "__main__":
     main()
