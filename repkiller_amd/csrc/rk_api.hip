@@ -523,12 +523,13 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     ctx->stats.n_groups = G;
     const rk::NwDigits ed = rk::nw_plan(rk::bit_length(G ? G - 1 : 0));
     HIPCHK(ctx, hipMemsetAsync(w.ehist, 0, 4096 * sizeof(uint32_t), st));
-    rk::nw_assign(w.par, w.newrank, w.erec, m, ed, w.ehist, st);
+    // gids into isnew's words (dead after the scan)
+    rk::nw_assign(w.par, w.newrank, w.isnew, m, ed, w.ehist, st);
 
     // members (stable by gid => processing order), in-group order, flags
     if (prof) mark(ctx, RK_PH_MEMBERS);
-    rk::nw_member_sort(w.erec, w.Ra, w.Rb, m, ed, w.ehist, w.astatus, w.sgid, w.reckey, w.tag,
-                       w.mrow, st);
+    rk::nw_member_sort(w.erec, w.isnew, w.Ra, w.Rb, m, ed, w.ehist, w.astatus, w.sgid, w.reckey,
+                       w.tag, w.mrow, st);
     rk::group_offsets(w.sgid, m, G, w.goff, st);
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
     rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,

@@ -257,10 +257,10 @@ void nw_x_bits(const uint32_t *xpos, const uint8_t *xstate, uint32_t m, uint32_t
                hipStream_t st);
 void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32_t m,
                hipStream_t st);
-void nw_assign(const uint32_t *par, const uint32_t *newrank, uint4 *erec, uint32_t m,
+void nw_assign(const uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uint32_t m,
                const NwDigits &e, uint32_t *ehist, hipStream_t st);
-void nw_member_sort(const uint4 *erec, uint4 *t0, uint4 *t1, uint32_t m, const NwDigits &e,
-                    const uint32_t *ehist, uint32_t *status, uint32_t *sgid, uint64_t *key,
-                    uint32_t *tag, uint32_t *mrow, hipStream_t st);
+void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1, uint32_t m,
+                    const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint32_t *sgid,
+                    uint64_t *key, uint32_t *tag, uint32_t *mrow, hipStream_t st);
 
 }  // namespace rk

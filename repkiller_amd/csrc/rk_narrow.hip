@@ -348,6 +348,16 @@ struct SrcRec {
   }
   __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
 };
+// ... with the key word from a separate array (the member records' gid)
+struct SrcRecKey {
+  const uint4 *in;
+  const uint32_t *key0;
+  __device__ __forceinline__ uint4 load(uint32_t i) const {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(in + i));
+    return make_uint4(__builtin_nontemporal_load(key0 + i), v.y, v.z, v.w);
+  }
+  __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
+};
 // Dst::wave(rec, live): called by every lane of a wave for consecutive
 // sorted slots of the tile (kWave = false: not at all)
 #define RK_NO_WAVE                   \
@@ -745,14 +755,14 @@ __global__ void k_nw_fill_y(const uint32_t *__restrict__ ent, const uint32_t *__
 // and the member sort's digit histograms
 __global__ void __launch_bounds__(256) k_nw_assign(const uint32_t *__restrict__ par,
                                                    const uint32_t *__restrict__ newrank,
-                                                   uint4 *__restrict__ erec, uint32_t m, Digits D,
-                                                   uint32_t *__restrict__ ghist) {
+                                                   uint32_t *__restrict__ gidp, uint32_t m,
+                                                   Digits D, uint32_t *__restrict__ ghist) {
   __shared__ HistLds L;
   hist_init(L);
   __syncthreads();
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
     const uint32_t g = newrank[par[k]];
-    reinterpret_cast<uint32_t *>(erec)[4 * (size_t)k] = g;
+    gidp[k] = g;  // (a word per fragment: the member records take it in the sort's first pass)
     hist_add(L, D, g);
   }
   __syncthreads();
@@ -998,7 +1008,7 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
 template <class Final>
 static void nw_sort_records(const uint4 *in, uint4 *t0, uint4 *t1, uint32_t m, const NwDigits &dg,
                             const uint32_t *ghist, uint32_t *status, const Final &fin,
-                            double final_bytes, hipStream_t st) {
+                            double final_bytes, hipStream_t st, const uint32_t *key0 = nullptr) {
   const Digits D = to_digits(dg);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
@@ -1008,13 +1018,23 @@ static void nw_sort_records(const uint4 *in, uint4 *t0, uint4 *t1, uint32_t m, c
     (void)hipMemsetAsync(status, 0, status_bytes, st);
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
+    // key0: the first pass takes every record's key from its own array
+    const double kb = p == 0 && key0 ? 4.0 * m : 0.0;
     if (p == D.passes - 1) {
-      launch_pass(SrcRec{src}, fin, m, D.shift[p], D.db[p], gh, status, ctr, st,
-                  16.0 * m + final_bytes);
+      if (p == 0 && key0)
+        launch_pass(SrcRecKey{src, key0}, fin, m, D.shift[p], D.db[p], gh, status, ctr, st,
+                    16.0 * m + kb + final_bytes);
+      else
+        launch_pass(SrcRec{src}, fin, m, D.shift[p], D.db[p], gh, status, ctr, st,
+                    16.0 * m + final_bytes);
     } else {
       uint4 *out = p % 2 == 0 ? t0 : t1;
-      launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], gh, status, ctr,
-                  st, 32.0 * m);
+      if (p == 0 && key0)
+        launch_pass(SrcRecKey{src, key0}, DstRec{out}, m, D.shift[p], D.db[p], gh, status, ctr,
+                    st, 32.0 * m + kb);
+      else
+        launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], gh, status, ctr, st,
+                    32.0 * m);
       src = out;
     }
   }
@@ -1027,11 +1047,11 @@ void nw_y_sort(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y, con
                   DstCsr{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y}, 17.0 * m, st);
 }
 
-void nw_member_sort(const uint4 *erec, uint4 *t0, uint4 *t1, uint32_t m, const NwDigits &e,
-                    const uint32_t *ehist, uint32_t *status, uint32_t *sgid, uint64_t *key,
-                    uint32_t *tag, uint32_t *mrow, hipStream_t st) {
+void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1, uint32_t m,
+                    const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint32_t *sgid,
+                    uint64_t *key, uint32_t *tag, uint32_t *mrow, hipStream_t st) {
   nw_sort_records(erec, t0, t1, m, e, ehist, status, DstMembers{sgid, tag, mrow, key}, 20.0 * m,
-                  st);
+                  st, gidp);
 }
 
 uint32_t nw_chunk_width(uint32_t m, uint32_t nbx) {
@@ -1085,11 +1105,11 @@ void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32
   kt_end(st, KID_NW_FILLY, 5.0 * m);
 }
 
-void nw_assign(const uint32_t *par, const uint32_t *newrank, uint4 *erec, uint32_t m,
+void nw_assign(const uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uint32_t m,
                const NwDigits &e, uint32_t *ehist, hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_nw_assign<<<grid_for(m, 256, 2048), 256, 0, st>>>(par, newrank, erec, m, to_digits(e),
+  k_nw_assign<<<grid_for(m, 256, 2048), 256, 0, st>>>(par, newrank, gidp, m, to_digits(e),
                                                       ehist);
   kt_end(st, KID_NW_ASSIGN, 12.0 * m);
 }
