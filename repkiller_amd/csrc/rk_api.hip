@@ -464,7 +464,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   // the Y axis sorts on the second stream while the X axis is built and resolved
   HIPCHK(ctx, hipEventRecord(ctx->fork, st));
   HIPCHK(ctx, hipStreamWaitEvent(st2, ctx->fork, 0));
-  rk::nw_y_sort(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y, st2);
+  rk::nw_y_sort_head(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, st2);
   HIPCHK(ctx, hipEventRecord(ctx->join, st2));
   mark(ctx, RK_PH_GATHER);
   rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, w.xoff, w.cx, w.xpos, w.erec, w.ctrl, cc.W,
@@ -487,9 +487,13 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if ((rc = rk::resolve_axis(ctx, ax, sc, true, &sweeps))) return rc;
     ctx->stats.x_sweeps = sweeps;
     if (prof) mark(ctx, RK_PH_SWEEP_Y);
-    if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
     rk::nw_x_bits(w.xpos, w.cx.state, m, w.xbits, st);
-    rk::nw_fill_y(w.cy.ent, w.xbits, w.cy.state, m, st);
+    if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
+    if (q == 0)  // the Y sort's last pass writes the CSR and the Y states
+      rk::nw_y_sort_tail(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y,
+                         w.xbits, st);
+    else  // later ratio pairs: the same CSR, new X results
+      rk::nw_fill_y(w.cy.ent, w.xbits, w.cy.state, m, st);
     rk::Axis ay{w.cy.key, w.cy.ent, nullptr, nullptr, w.cy.state, nullptr, w.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};

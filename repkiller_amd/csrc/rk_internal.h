@@ -246,8 +246,11 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
                    const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
                    hipStream_t st);
 void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st);
-void nw_y_sort(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y, const uint32_t *yhist,
-               uint32_t *status, Csr cy, uint32_t nby, uint64_t max_y, hipStream_t st);
+void nw_y_sort_head(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
+                    const uint32_t *yhist, uint32_t *status, hipStream_t st);
+void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDigits &y,
+                    const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
+                    uint64_t max_y, const uint32_t *xbits, hipStream_t st);
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
                  const uint32_t *xoff, Csr cx, uint32_t *xpos, uint4 *erec, uint32_t *ctrl,
                  uint32_t W, hipStream_t st);

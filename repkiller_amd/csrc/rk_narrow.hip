@@ -431,7 +431,12 @@ struct DstCsr {
     const uint64_t base = (uint64_t)b * 100;
     const uint64_t c = base + (uint32_t)(r.z - (uint32_t)base);  // centre from bucket + low bits
     nbd[pos] = nbd_code_nw(c, max_index);
+    // with the X results (bitmask by processing index): the Y states -- X hits
+    // sit in the Y lists (commonFunctions.cpp:59), X misses query them
+    if (xbits) state[pos] = (xbits[r.y >> 5] >> (r.y & 31)) & 1u ? ST_ACTIVE : ST_UNKNOWN;
   }
+  const uint32_t *xbits;  // null: the states are filled later (k_nw_fill_y)
+  uint8_t *state;
 };
 
 // --- group members, last pass: gid order (stable: processing order inside) -
@@ -951,6 +956,8 @@ NwDigits nw_plan(int bits) {
   return o;
 }
 
+static const uint32_t *ghist_of(const uint32_t *h, int pass) { return h + pass * 1024; }
+
 static Digits to_digits(const NwDigits &o) {
   Digits D{};
   D.passes = o.passes;
@@ -1040,11 +1047,40 @@ static void nw_sort_records(const uint4 *in, uint4 *t0, uint4 *t1, uint32_t m, c
   }
 }
 
-void nw_y_sort(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y, const uint32_t *yhist,
-               uint32_t *status, Csr cy, uint32_t nby, uint64_t max_y, hipStream_t st) {
-  // intermediates alternate tmp, yrec (yrec is free once the first pass read it)
-  nw_sort_records(yrec, tmp, const_cast<uint4 *>(yrec), m, y, yhist, status,
-                  DstCsr{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y}, 17.0 * m, st);
+// The Y axis sort in two parts: every pass but the last (on the second stream,
+// beside the X axis), then the last one, which writes the CSR arrays and --
+// given the X-hit bitmask -- the Y states (no separate fill pass).  Pass p
+// reads yrec (p = 0) or the previous pass' output; intermediates alternate
+// tmp, yrec (yrec is free once the first pass read it).
+void nw_y_sort_head(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
+                    const uint32_t *yhist, uint32_t *status, hipStream_t st) {
+  const Digits D = to_digits(y);
+  const size_t sw = nw_status_words(m);
+  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  const uint4 *src = yrec;
+  for (int p = 0; p + 1 < D.passes; ++p) {
+    const size_t status_bytes = (size_t)tiles_for(m, D.db[p]) * ((size_t)1 << D.db[p]) * 4;
+    (void)hipMemsetAsync(status, 0, status_bytes, st);
+    uint4 *out = p % 2 == 0 ? tmp : const_cast<uint4 *>(yrec);
+    launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], ghist_of(yhist, p),
+                status, status + sw - 64 + p, st, 32.0 * m);
+    src = out;
+  }
+}
+void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDigits &y,
+                    const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
+                    uint64_t max_y, const uint32_t *xbits, hipStream_t st) {
+  const Digits D = to_digits(y);
+  const size_t sw = nw_status_words(m);
+  const int p = D.passes - 1;
+  const uint4 *src = p == 0 ? yrec : (p - 1) % 2 == 0 ? tmp : yrec;
+  const size_t status_bytes = (size_t)tiles_for(m, D.db[p]) * ((size_t)1 << D.db[p]) * 4;
+  (void)hipMemsetAsync(status, 0, status_bytes, st);
+  if (p == 0) (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);
+  launch_pass(SrcRec{src},
+              DstCsr{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, xbits, cy.state}, m,
+              D.shift[p], D.db[p], ghist_of(yhist, p), status, status + sw - 64 + p, st,
+              16.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0));
 }
 
 void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1, uint32_t m,
