@@ -27,7 +27,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librepkiller_amd.so")
+# RK_LIB=<path>: load another build of the library (A/B measurements)
+LIB_PATH = os.environ.get("RK_LIB") or os.path.join(_HERE, "librepkiller_amd.so")
 CLI_PATH = os.path.join(_HERE, "bin", "rk_repkiller")
 
 RK_OK = 0

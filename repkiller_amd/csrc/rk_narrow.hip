@@ -176,7 +176,11 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
   constexpr int DPT = RADIX >= T ? RADIX / T : 1, OWNERS = RADIX / DPT;
   static_assert(RADIX % T == 0 || T % RADIX == 0, "whole digits per thread");
   const bool owner = (int)threadIdx.x < OWNERS;
-  __shared__ uint4 srec[TILE];
+  // sorted records staged in LDS, LSLOTS slots at a time (tiles above 4096
+  // records are placed and written out in rounds: 64 KB of LDS per block)
+  constexpr int LSLOTS = TILE < 4096 ? TILE : 4096;
+  static_assert(!PERSIST || LSLOTS == TILE, "persistent tiles reload rec[] before the write-out");
+  __shared__ uint4 srec[LSLOTS];
   __shared__ uint32_t wcnt[NW][RADIX];  // per-wave digit counters, then per-wave starts
   __shared__ uint32_t lbase[RADIX];     // tile-local start of digit d
   __shared__ uint32_t gbase[RADIX];     // global start of digit d (all tiles)
@@ -284,11 +288,13 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
         for (int j = 0; j < DPT; ++j) lbase[threadIdx.x * DPT + j] = at, at += run[j];
     }
     __syncthreads();
+    // sorted slot of every record (round 0's placed at once)
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       if (rk[r] == 0xFFFFFFFFu) continue;
       const uint32_t d = (src.key(rec[r]) >> shift) & (RADIX - 1);
-      srec[lbase[d] + mycnt[d] + rk[r]] = rec[r];
+      rk[r] += lbase[d] + mycnt[d];
+      if (LSLOTS == TILE || rk[r] < (uint32_t)LSLOTS) srec[rk[r]] = rec[r];
     }
     // 3: the next tile's loads, then the look-back
     const uint32_t next = PERSIST ? s_tile[(it + 1) & 1] : tiles;
@@ -312,15 +318,25 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     const uint64_t tr2 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     // 4: write-out (the next iteration's LDS writes follow its first barrier,
     // which every thread reaches only after this loop)
-    for (uint32_t j0 = 0; j0 < cnt; j0 += T) {  // wave-uniform trip count (Dst::wave)
-      const uint32_t j = j0 + threadIdx.x;
-      const bool live = j < cnt;
-      const uint4 r = live ? srec[j] : make_uint4(0, 0, 0, 0);
-      if (live) {
-        const uint32_t d = (src.key(r) >> shift) & (RADIX - 1);
-        dst.store(gpos[d] + (j - lbase[d]), r);
+    for (uint32_t h0 = 0; h0 < cnt; h0 += LSLOTS) {
+      if (LSLOTS < TILE && h0 > 0) {  // the next round of sorted slots
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r)
+          if (rk[r] != 0xFFFFFFFFu && rk[r] - h0 < (uint32_t)LSLOTS) srec[rk[r] - h0] = rec[r];
+        __syncthreads();
       }
-      if (Dst::kWave) dst.wave(r, live);
+      const uint32_t h1 = cnt - h0 < (uint32_t)LSLOTS ? cnt : h0 + LSLOTS;
+      for (uint32_t j0 = h0; j0 < h1; j0 += T) {  // wave-uniform trip count (Dst::wave)
+        const uint32_t j = j0 + threadIdx.x;
+        const bool live = j < h1;
+        const uint4 r = live ? srec[j - h0] : make_uint4(0, 0, 0, 0);
+        if (live) {
+          const uint32_t d = (src.key(r) >> shift) & (RADIX - 1);
+          dst.store(gpos[d] + (j - lbase[d]), r);
+        }
+        if (Dst::kWave) dst.wave(r, live);
+      }
     }
     if (trace && threadIdx.x == 0) {  // RK_NW_TRACE: phase timestamps of this tile
       uint32_t xcc;
@@ -811,7 +827,9 @@ uint32_t tile_records(int db) {
   switch (nw_shape()) {
     case 2: return 256 * 8;
     case 3: return 256 * 12;
-    case 5: return 512 * 16;
+    case 5: case 6: return 512 * 16;
+    case 7: return 512 * 12;
+    case 8: return 1024 * 8;
     default: return 4096;  // 0, 1: 256 x 16; 4: 512 x 8
   }
 }
@@ -863,14 +881,19 @@ uint32_t resident_blocks(K kernel, int threads) {
 
 // RK_NW_SHAPE (measurements; 8-bit digits): 0 = 256 threads x 16 records per
 // block, one tile each; 1 = the same, persistent blocks, the next tile's loads
-// issued before the look-back; 2 = 256 x 8; 3 = 256 x 12; 4 = 512 x 8
-// (default); 5 = 512 x 16.  cfg3 step, two streams: 13.75 / - / 14.39 / - /
-// 13.28 / 13.49 ms (shape 1 was slower: the look-back's loads queue behind the
-// next tile's in the same wave's memory counter)
+// issued before the look-back; 2 = 256 x 8; 3 = 256 x 12; 4 = 512 x 8; 5, 6 =
+// 512 x 16; 7 = 512 x 12 (default); 8 = 1024 x 8.  Tiles above 4096 records
+// are staged through LDS in rounds of 4096 sorted slots, so a 6144-record tile
+// keeps two blocks per CU (125 VGPRs, 2 x ~75 KB of LDS) and pays one look-back
+// per 6144 records.  cfg3 step, two streams: 13.75 / - / 14.39 / - / 13.28 /
+// 13.49 ms (round 2, earlier code: 5 had 128 KB of LDS, one block per CU;
+// shape 1 was slower: the look-back's loads queue behind the next tile's in the
+// same wave's memory counter); now 4 / 6 / 7 / 8: 12.78 / 13.01 / 12.27 / 12.59
+// ms (6: 158 VGPRs, one block per CU; 8: one 1024-thread block per CU)
 int nw_shape() {
   static const int v = [] {
     const char *e = getenv("RK_NW_SHAPE");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 7;
   }();
   return v;
 }
@@ -897,7 +920,9 @@ void launch_pass_db(const Src &src, const Dst &dst, uint32_t n, int shift, const
       case 2: launch_shape<256, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
       case 3: launch_shape<256, 12, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
       case 4: launch_shape<512, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
-      case 5: launch_shape<512, 16, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 5: case 6: launch_shape<512, 16, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 7: launch_shape<512, 12, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 8: launch_shape<1024, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
       default: break;
     }
   }

@@ -485,6 +485,15 @@ __device__ __forceinline__ void foreign_scan32(const Axis &ax, uint32_t g0, int 
 #define RK_OWN_U 4
 #endif
 constexpr int OWN_U = RK_OWN_U;
+#ifdef RK_SWEEP_PROF
+// measurement build only: per-phase shader cycles of the first window sweep
+__device__ unsigned long long g_sweep_prof[16];
+#define SP_T(k) const uint64_t _t##k = __builtin_amdgcn_s_memtime()
+#define SP_ADD(slot, v) do { if (lflag && lane == 0) atomicAdd(&g_sweep_prof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define SP_T(k)
+#define SP_ADD(slot, v)
+#endif
 // One window (64 positions) of the 32-bit sweep; LDS scratch of the calling
 // wavefront in pk / ent / key.  Returns (wave-uniformly) whether the window
 // still owns undecided entries, and records that in wpend[w].
@@ -492,6 +501,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
                                                uint8_t *lflag, uint2 *pk,
                                                uint32_t *ent, uint32_t *key, int lane) {
   bool pending = false;
+  SP_T(0);
   {
     const uint32_t base = w * 64, m = ax.m;
     uint64_t S0, S1;
@@ -539,6 +549,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
       st0[s] = st[s];
     }
     wave_sync_lds();
+    SP_T(1);
     // matching candidates: own run (bit j = entry rs + j), owned neighbour run
     // (bit j = entry nbs + j); a foreign neighbour run is summarised in fs
     uint64_t rown[2], rnb[2];
@@ -570,6 +581,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
         rown[s] |= b4 << j;
       }
     }
+    SP_T(2);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (!open[s] || !nd[s]) continue;
@@ -625,8 +637,15 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     // UNKNOWN set left after that, pending hits whose candidates are all
     // decided become final.  Rounds stop when nothing changes or nothing is
     // left open.
+    SP_T(3);
     uint64_t A0, A1;
+#ifdef RK_SWEEP_PROF
+    uint32_t nrounds = 0;
+#endif
     for (;;) {
+#ifdef RK_SWEEP_PROF
+      ++nrounds;
+#endif
       A0 = __ballot(own[0] && st[0] == ST_ACTIVE);
       A1 = __ballot(own[1] && st[1] == ST_ACTIVE);
       const uint64_t U0 = __ballot(own[0] && st[0] == ST_UNKNOWN);
@@ -653,6 +672,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
       }
       if (!__ballot(changed) || !__ballot(left)) break;
     }
+    SP_T(4);
     A0 = __ballot(own[0] && st[0] == ST_ACTIVE);
     A1 = __ballot(own[1] && st[1] == ST_ACTIVE);
     // winners: the first strict maximum in scan order among the matching
@@ -700,6 +720,20 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     }
     const bool wp = __ballot(pending) != 0;
     if (lane == 0) wpend[w] = wp;
+#ifdef RK_SWEEP_PROF
+    SP_T(5);
+    SP_ADD(0, _t1 - _t0);
+    SP_ADD(1, _t2 - _t1);
+    SP_ADD(2, _t3 - _t2);
+    SP_ADD(3, _t4 - _t3);
+    SP_ADD(4, _t5 - _t4);
+    SP_ADD(5, nrounds);
+    SP_ADD(6, 1);
+    SP_ADD(7, __ballot(own[1]) != 0);
+    SP_ADD(8, __popcll(__ballot(open[0] || open[1])));
+    SP_ADD(9, __popcll(__ballot(own[0] && (st0[0] == ST_UNKNOWN) && rs[0] == 64 * 0 + lane && !nd[0])));
+    SP_ADD(10, __ballot(fs[0].any_unknown || fs[1].any_unknown || fs[0].any_active || fs[1].any_active) != 0);
+#endif
     return wp;
   }
 }
@@ -1263,6 +1297,13 @@ __global__ void __launch_bounds__(256) k_run_bounds(Axis ax, uint32_t nwin, uint
 
 }  // namespace
 
+#ifdef RK_SWEEP_PROF
+static void *g_sweep_prof_ptr() {
+  void *p = nullptr;
+  (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_sweep_prof));
+  return p;
+}
+#endif
 size_t runs_scratch_words(uint32_t m) { return (size_t)m / (LONG_RUN + 1) + 64; }
 
 void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host_words,
@@ -1300,6 +1341,17 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
       k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
     kt_end(st, rl.fast32 ? (first ? KID_SWEEP_FAST : KID_SWEEP_MORE) : KID_SWEEP_TILE,
            first ? (rl.fast32 ? 26.0 : 30.0) * ax.m : (double)rl.nwin);
+#ifdef RK_SWEEP_PROF
+    if (rl.fast32 && first) {
+      unsigned long long h[16];
+      (void)hipStreamSynchronize(st);
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sweep_prof), sizeof h);
+      const double w = h[6] ? (double)h[6] : 1.0;
+      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f open/win %.1f trivial/win %.1f foreignwin %.3f\n",
+              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w, h[9] / w, h[10] / w);
+      (void)hipMemsetAsync(g_sweep_prof_ptr(), 0, sizeof h, st);
+    }
+#endif
   }
   if (rl.fast32) {  // the long-run count lives on the device: a fixed grid reads it
     kt_begin(st);
