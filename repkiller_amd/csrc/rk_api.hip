@@ -50,14 +50,14 @@ void collect_kernel_timing(rk_ctx *ctx) {
   if (ctx->kt.tier_counts) {  // the group-sort tiers' algorithmic bytes
     const uint32_t nb = ctx->kt.tier_nblk;
     std::vector<uint32_t> h((size_t)KernelTimer::TIERS * nb);
-    if (hipMemcpy(h.data(), ctx->kt.tier_counts, (size_t)7 * nb * 4, hipMemcpyDeviceToHost) ==
-        hipSuccess) {
-      for (int u = 0; u < 7; ++u) {
+    if (hipMemcpy(h.data(), ctx->kt.tier_counts, (size_t)GS_NTIER * nb * 4,
+                  hipMemcpyDeviceToHost) == hipSuccess) {
+      for (int u = 0; u < GS_NTIER; ++u) {
         double mem = 0;
         for (uint32_t b = 0; b < nb; ++b) mem += h[(size_t)u * nb + b];
         const int sl = ctx->kt.tier_slot[u];
         if (sl >= 0 && sl < ctx->kt.n) ctx->kt.bytes[sl] = 16.0 * mem;
-        const int s2 = u == 6 ? ctx->kt.tier_slot[7] : -1;  // the large tier's phase B
+        const int s2 = u == GS_NTIER - 1 ? ctx->kt.tier_slot[GS_NTIER] : -1;  // phase B
         if (s2 >= 0 && s2 < ctx->kt.n) ctx->kt.bytes[s2] = 16.0 * mem;
       }
     }

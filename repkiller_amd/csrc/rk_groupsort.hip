@@ -33,6 +33,7 @@
 // In every tier the result goes to `otag` (member order, group-major).
 #include "rk_internal.h"
 
+#include <cstdlib>
 #include <vector>
 
 namespace rk {
@@ -429,22 +430,30 @@ struct TierLists {
   }
 };
 
-// Register tier: one wavefront per group of 17..64 members, no LDS.  The
-// group lives in registers (lane x = member x), the introsort runs there and
+// Register tiers: groups of 17..64 members in registers, no LDS -- PACK
+// groups per wavefront (lanes [64/PACK * j, 64/PACK * (j+1)) hold group j of
+// the wave's PACK consecutive list entries; reg_sort_core keeps every lane's
+// own segment, so the groups never mix).  The introsort runs there and
 // __final_insertion_sort is the stable rank inside each leaf (<= 16 lanes,
 // by shuffles); heap-sorted ranges are already in order.
+template <int PACK>
 __global__ void __launch_bounds__(256) k_sort_groups_reg(TierLists tl, int tier,
                                                          const uint32_t *goff, uint64_t *key,
                                                          uint32_t *tag, uint32_t *otag) {
+  constexpr int SPAN = 64 / PACK;
   const uint32_t lane = threadIdx.x & 63;
+  const int j = (int)lane / SPAN;
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
-  for (uint32_t w = lo + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); w < hi;
-       w += (gridDim.x * blockDim.x) >> 6) {
-    const uint32_t g = tl.list[w];
-    const uint32_t b = goff[g], n = goff[g + 1] - b;
-    const GView v{key + b, tag + b, nullptr, nullptr, nullptr};
-    reg_batch<true, GView>(v, lane < n, 0, 0, (int)n, 2 * (31 - __clz((int)n)), lane, otag + b);
+  const GView v{key, tag, nullptr, nullptr, nullptr};
+  for (uint32_t w = lo + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * PACK; w < hi;
+       w += ((gridDim.x * blockDim.x) >> 6) * PACK) {
+    const bool has = w + j < hi;
+    const uint32_t g = has ? tl.list[w + j] : 0u;
+    const uint32_t b = has ? goff[g] : 0u, n = has ? goff[g + 1] - b : 0u;
+    const int bl = j * SPAN;
+    reg_batch<true, GView>(v, (int)lane - bl < (int)n, bl, b, (int)n,
+                           n ? 2 * (31 - __clz((int)n)) : 0, lane, otag);
   }
 }
 
@@ -724,44 +733,43 @@ __global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, ui
   }
 }
 
-// groups of 1..16 members: insertion sort == stable rank; one thread per member
-// groups of 1..16 members (tier 0): insertion sort == stable rank; one thread
-// per group, the keys in registers
-__global__ void __launch_bounds__(256) k_sort_small(TierLists tl, const uint32_t *goff,
-                                                    const uint64_t *key, const uint32_t *tag,
-                                                    uint32_t *otag) {
-  uint32_t lo, hi;
-  tl.range(0, lo, hi);
-  for (uint32_t w = lo + blockIdx.x * blockDim.x + threadIdx.x; w < hi;
-       w += gridDim.x * blockDim.x) {
-    const uint32_t g = tl.list[w];
+// Groups of 1..16 members (tier 0, not listed): __final_insertion_sort alone
+// sorts them, so a member's final slot is its stable rank inside the group.
+// One lane per member slot over the whole member array: a singleton copies
+// its tag; a member of a group of 2..16 compares its key with the group's
+// (independent loads, served by L1/L2: the group's lanes read the same line).
+__global__ void __launch_bounds__(256) k_sort_small(const uint32_t *sgid, const uint32_t *goff,
+                                                    uint32_t m, const uint64_t *key,
+                                                    const uint32_t *tag, uint32_t *otag) {
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
+    const uint32_t g = sgid[x];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
-    if (n == 1) {
-      otag[b] = tag[b];
-      continue;
-    }
-    uint64_t k[THRESH];
+    if (n > (uint32_t)THRESH) continue;
+    uint32_t r = 0;
+    if (n > 1) {
+      const uint64_t kx = key[x];
+      const uint32_t i = x - b;
 #pragma unroll
-    for (int i = 0; i < THRESH; ++i) k[i] = i < (int)n ? key[b + i] : 0ull;
-#pragma unroll
-    for (int i = 0; i < THRESH; ++i) {
-      if (i < (int)n) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int j = 0; j < THRESH; ++j)
-          r += j < (int)n && (k[j] < k[i] || (k[j] == k[i] && j < i));
-        otag[b + r] = tag[b + i];
+      for (uint32_t j = 0; j < (uint32_t)THRESH; ++j) {
+        if (j < n) {
+          const uint64_t kj = key[b + j];
+          r += kj < kx || (kj == kx && j < i);
+        }
       }
     }
+    otag[b + r] = tag[x];
   }
 }
 
-// Tiers by group size: 0 = 1..16 members (k_sort_small), 1 = 17..64
-// (registers), 2..5 = up to LDS_CAPS[t-2] (LDS), 6 = larger (global memory).
-// Small LDS caps keep many wavefronts resident per CU (a 65..128-member group
-// needs ~3 KB of LDS, a 2048-member one ~30 KB).
-constexpr int NTIER = 7;
+// Tiers by group size: 0 = 1..16 members (k_sort_small, not listed), 1 =
+// 17..32 (registers, two groups per wavefront), 2 = 33..64 (registers), 3..6
+// = up to LDS_CAPS[t-3] (LDS), 7 = larger (global memory).  Small LDS caps
+// keep many wavefronts resident per CU (a 65..128-member group needs ~3 KB of
+// LDS, a 2048-member one ~30 KB).
+constexpr int NTIER = GS_NTIER;
 constexpr int NLDS = 4;
+constexpr int TIER_LDS0 = 3;
+static_assert(TIER_LDS0 + NLDS + 1 == NTIER, "tier layout");
 struct Caps {
   uint32_t c[NLDS];
 };
@@ -770,10 +778,11 @@ __host__ __device__ constexpr Caps lds_caps() { return Caps{{128, 256, 512, 2048
 __device__ __forceinline__ int tier_of(uint32_t n) {
   constexpr Caps caps = lds_caps();
   if (n <= (uint32_t)THRESH) return 0;
-  if (n <= 64) return 1;
+  if (n <= 32) return 1;
+  if (n <= 64) return 2;
 #pragma unroll
   for (int j = 0; j < NLDS; ++j)
-    if (n <= caps.c[j]) return 2 + j;
+    if (n <= caps.c[j]) return TIER_LDS0 + j;
   return NTIER - 1;
 }
 
@@ -826,7 +835,7 @@ __global__ void __launch_bounds__(256) k_tier_lists(const uint32_t *goff, uint32
       if (lane == 0) wc[wv][u] = (uint32_t)__popcll(b);
     }
     __syncthreads();
-    if (g < g1) {
+    if (g < g1 && t != 0) {  // tier 0 is served by a dense pass, not a list
       uint32_t before = 0;
       for (int k = 0; k < wv; ++k) before += wc[k][t];
 #pragma unroll
@@ -899,26 +908,40 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     (void)hipStreamWaitEvent(s2, ev_fork, 0);
   }
   kt_begin(s2);
-  k_sort_small<<<4096, 256, 0, s2>>>(tl, goff, key, tag, otag);
+  // one slot per thread: the three dependent loads of a slot overlap across waves
+  k_sort_small<<<(m + 255) / 256, 256, 0, s2>>>(gid_sorted, goff, m, key, tag, otag);
   kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
   tier_slot(0);
   kt_begin(s2);
-  k_sort_groups_reg<<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
+  k_sort_groups_reg<2><<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
   kt_end(s2, KID_SORT_REG, 0.0);
   tier_slot(1);
-  if (side) (void)hipEventRecord(ev_join, s2);
-  for (int j = 0; j < NLDS; ++j) {
-    const uint32_t cap = caps.c[j];
-    const uint32_t grid = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
-    kt_begin(st);
-    if (narrow_keys)
-      k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), st>>>(tl, 2 + j, goff, key, tag,
-                                                                       otag, cap);
-    else
-      k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), st>>>(tl, 2 + j, goff, key, tag,
-                                                                       otag, cap);
-    kt_end(st, KID_SORT_LDS, 0.0);
-    tier_slot(2 + j);
+  kt_begin(s2);
+  k_sort_groups_reg<1><<<4096, 256, 0, s2>>>(tl, 2, goff, key, tag, otag);
+  kt_end(s2, KID_SORT_REG, 0.0);
+  tier_slot(2);
+  // the first `lds_side` LDS tiers also run on `side` (RK_GS_SIDE, measurements)
+  static const int lds_side = [] {
+    const char *e = getenv("RK_GS_SIDE");
+    return e ? atoi(e) : 0;
+  }();
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1 && side) (void)hipEventRecord(ev_join, s2);
+    for (int j = 0; j < NLDS; ++j) {
+      if ((j < lds_side) != (pass == 0)) continue;
+      hipStream_t sj = pass == 0 ? s2 : st;
+      const uint32_t cap = caps.c[j];
+      const uint32_t grid = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
+      kt_begin(sj);
+      if (narrow_keys)
+        k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), sj>>>(tl, TIER_LDS0 + j, goff,
+                                                                         key, tag, otag, cap);
+      else
+        k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), sj>>>(tl, TIER_LDS0 + j, goff,
+                                                                         key, tag, otag, cap);
+      kt_end(sj, KID_SORT_LDS, 0.0);
+      tier_slot(TIER_LDS0 + j);
+    }
   }
   // phase A marks the final segments' starts in bnd (cleared first); both
   // kernels return at once when no group is that large

@@ -62,6 +62,9 @@ enum KernelId : int {
   KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_NW_XBITS, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
+// group-sort tiers (rk_groupsort.hip tier_of): <=16, <=32, <=64, four LDS caps, larger
+constexpr int GS_NTIER = 8;
+
 struct KernelTimer {
   static constexpr int MAX = 256;
   hipEvent_t ev[2 * MAX];
@@ -70,7 +73,7 @@ struct KernelTimer {
   int n;
   // group-sort tiers: their member counts exist on the device only; they are
   // read back when the call's timings are collected (no sync inside the call)
-  static constexpr int TIERS = 8;
+  static constexpr int TIERS = GS_NTIER + 1;  // + the large tier's phase B
   const uint32_t *tier_counts;  // [tier][nblk] members per block, or null
   uint32_t tier_nblk;
   int tier_slot[TIERS];         // timer slot of each tier's launch (-1: none)
