@@ -494,56 +494,66 @@ __device__ unsigned long long g_sweep_prof[16];
 #define SP_T(k)
 #define SP_ADD(slot, v)
 #endif
+// Window masks (bit P = window position P, two 64-bit words) of a per-lane
+// predicate.  NSLOT == 2: lane l holds positions l (slot 0) and 64 + l (slot
+// 1).  NSLOT == 1: lanes below t hold positions 64 + lane -- the tail of the
+// window's last run --, the others position `lane` (t <= the first run start
+// f of the window, and lanes [t, f) own nothing, so no position is doubled).
+template <int NSLOT>
+__device__ __forceinline__ void win_ballot(bool c0, bool c1, uint64_t lowt, uint64_t &lo,
+                                           uint64_t &hi) {
+  if (NSLOT == 2) {
+    lo = __ballot(c0);
+    hi = __ballot(c1);
+  } else {
+    const uint64_t b = __ballot(c0);
+    lo = b & ~lowt;
+    hi = b & lowt;
+  }
+}
+
 // One window (64 positions) of the 32-bit sweep; LDS scratch of the calling
-// wavefront in pk / ent / key.  Returns (wave-uniformly) whether the window
-// still owns undecided entries, and records that in wpend[w].
-__device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8_t *wpend,
-                                               uint8_t *lflag, uint2 *pk,
-                                               uint32_t *ent, uint32_t *key, int lane) {
+// wavefront in pk / ent / key; the window's keys are already in `key` and its
+// run starts in S0 / S1.  Returns (wave-uniformly) whether the window still
+// owns undecided entries, and records that in wpend[w].  NSLOT == 1 serves
+// the windows whose last run's tail fits in the lanes before the first run
+// start (most windows): every slot's code runs once instead of twice.
+template <int NSLOT>
+__device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t *wpend,
+                                             uint8_t *lflag, uint2 *pk, uint32_t *ent,
+                                             uint32_t *key, int lane, uint64_t S0, uint64_t S1,
+                                             int t, uint2 pk0, uint32_t ent0, uint8_t st00,
+                                             uint8_t nd00) {
   bool pending = false;
   SP_T(0);
   {
     const uint32_t base = w * 64, m = ax.m;
-    uint64_t S0, S1;
-    // slot-0 records are loaded with the keys (one memory round trip for
-    // nearly everything; slot 1 only holds the tail of the last run)
-    const uint32_t p0 = base + lane;
-    uint2 pk0 = make_uint2(0, 0);
-    uint32_t ent0 = 0;
-    uint8_t st00 = ST_HIT, nd00 = 0;
-    if (p0 < m) pk0 = ax.pk[p0], ent0 = ax.ent[p0], st00 = ax.state[p0], nd00 = ax.nbd[p0];
-    {
-      const uint32_t p1 = base + 64 + lane;
-      const uint32_t k0 = p0 < m ? ax.key[p0] : NONE, k1 = p1 < m ? ax.key[p1] : NONE;
-      const uint32_t q0 = p0 < m && p0 > 0 ? ax.key[p0 - 1] : NONE;
-      const uint32_t q1 = p1 < m ? ax.key[p1 - 1] : NONE;
-      key[lane] = k0;
-      key[64 + lane] = k1;
-      S0 = __ballot(p0 >= m || p0 == 0 || q0 != k0);
-      S1 = __ballot(p1 >= m || q1 != k1);
-    }
+    const uint64_t lowt = NSLOT == 1 ? (1ull << t) - 1ull : 0ull;  // t < 64 here
+    int P[2];
     bool own[2];
     int rs[2];
     uint8_t st[2], st0[2], nd[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int P = 64 * s + lane;
-      rs[s] = hs_le(S0, S1, P);
-      const int re = ls_gt(S0, S1, P);
-      own[s] = base + P < m && rs[s] >= 0 && rs[s] < 64 && re - rs[s] <= (int)LONG_RUN;
+    for (int s = 0; s < NSLOT; ++s) {
+      P[s] = NSLOT == 2 ? 64 * s + lane : (lane < t ? 64 + lane : lane);
+      rs[s] = hs_le(S0, S1, P[s]);
+      const int re = ls_gt(S0, S1, P[s]);
+      own[s] = base + P[s] < m && rs[s] >= 0 && rs[s] < 64 && re - rs[s] <= (int)LONG_RUN;
       if (s == 0 && lflag) {  // first sweep: flag a long run that starts here
-        const bool lng = base + P < m && rs[0] == P && re - P > (int)LONG_RUN;
+        const bool lng = base + P[s] < m && rs[0] == P[s] && re - P[s] > (int)LONG_RUN;
         const uint64_t bb = __ballot(lng);
         if (lane == 0) lflag[w] = bb != 0;
       }
       st[s] = ST_HIT;
       nd[s] = 0;
       if (own[s]) {
-        const uint32_t p = base + P;
-        if (s == 0) {
-          pk[P] = pk0, ent[P] = ent0, st[s] = st00, nd[s] = nd00;
+        // slot-0 records came with the keys (positions below 64); the tail of
+        // the last run is loaded now
+        if (P[s] < 64) {
+          pk[P[s]] = pk0, ent[P[s]] = ent0, st[s] = st00, nd[s] = nd00;
         } else {
-          pk[P] = ax.pk[p], ent[P] = ax.ent[p], st[s] = ax.state[p], nd[s] = ax.nbd[p];
+          const uint32_t p = base + P[s];
+          pk[P[s]] = ax.pk[p], ent[P[s]] = ax.ent[p], st[s] = ax.state[p], nd[s] = ax.nbd[p];
         }
       }
       st0[s] = st[s];
@@ -558,17 +568,16 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     Q32 qs[2];
     bool open[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NSLOT; ++s) {
       rown[s] = rnb[s] = 0;
       nbs[s] = 0;
       fs[s] = Scan{0.0, NONE, 0, false, false};
       open[s] = own[s] && (st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING);
       if (!open[s]) continue;
-      const int P = 64 * s + lane;
-      const uint2 me = pk[P];
+      const uint2 me = pk[P[s]];
       const Q32 q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
       qs[s] = q;
-      const int n = P - rs[s];
+      const int n = P[s] - rs[s];
       // OWN_U independent LDS reads per step (pk is padded past position 127)
       for (int j = 0; j < n; j += OWN_U) {
         uint2 o[OWN_U];
@@ -583,12 +592,11 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     }
     SP_T(2);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NSLOT; ++s) {
       if (!open[s] || !nd[s]) continue;
-      const int P = 64 * s + lane;
       const Q32 q = qs[s];
       const int dir = nd[s] == 1 ? -1 : 1;
-      const uint32_t i = ent[P], k = key[P];
+      const uint32_t i = ent[P[s]], k = key[P[s]];
       uint32_t g0 = 0;  // first position of a foreign neighbour scan
       bool foreign = false;
       int nb = -1, ne = -1;
@@ -604,7 +612,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
           foreign = true, g0 = base - 1;  // the key test happens in the scan
         }
       } else {
-        const int q2 = ls_gt(S0, S1, P);
+        const int q2 = ls_gt(S0, S1, P[s]);
         const uint32_t gq = base + q2;
         if (gq < m) {
           const uint32_t kq = q2 < 128 ? key[q2] : k + 1;  // q2 == 128: tested in the scan
@@ -626,7 +634,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     // is two ANDs per ballot word
     M128 cm[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NSLOT; ++s) {
       const M128 o = shl128(rown[s], rs[s]), q = shl128(rnb[s], nbs[s]);
       cm[s] = M128{o.lo | q.lo, o.hi | q.hi};
     }
@@ -638,6 +646,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     // decided become final.  Rounds stop when nothing changes or nothing is
     // left open.
     SP_T(3);
+#define RK_SLOT_IS(s, v) ((s) < NSLOT && own[(s) < NSLOT ? (s) : 0] && st[(s) < NSLOT ? (s) : 0] == (v))
     uint64_t A0, A1;
 #ifdef RK_SWEEP_PROF
     uint32_t nrounds = 0;
@@ -646,24 +655,23 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
 #ifdef RK_SWEEP_PROF
       ++nrounds;
 #endif
-      A0 = __ballot(own[0] && st[0] == ST_ACTIVE);
-      A1 = __ballot(own[1] && st[1] == ST_ACTIVE);
-      const uint64_t U0 = __ballot(own[0] && st[0] == ST_UNKNOWN);
-      const uint64_t U1 = __ballot(own[1] && st[1] == ST_UNKNOWN);
+      uint64_t U0, U1;
+      win_ballot<NSLOT>(RK_SLOT_IS(0, ST_ACTIVE), RK_SLOT_IS(1, ST_ACTIVE), lowt, A0, A1);
+      win_ballot<NSLOT>(RK_SLOT_IS(0, ST_UNKNOWN), RK_SLOT_IS(1, ST_UNKNOWN), lowt, U0, U1);
       bool changed = false;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < NSLOT; ++s) {
         if (!own[s] || st[s] != ST_UNKNOWN) continue;
         const bool has_act = ((A0 & cm[s].lo) | (A1 & cm[s].hi)) != 0 || fs[s].any_active;
         const bool has_unk = ((U0 & cm[s].lo) | (U1 & cm[s].hi)) != 0 || fs[s].any_unknown;
         if (has_act) st[s] = ST_HIT_PENDING, changed = true;
         else if (!has_unk) st[s] = ST_ACTIVE, changed = true;
       }
-      const uint64_t V0 = __ballot(own[0] && st[0] == ST_UNKNOWN);
-      const uint64_t V1 = __ballot(own[1] && st[1] == ST_UNKNOWN);
+      uint64_t V0, V1;
+      win_ballot<NSLOT>(RK_SLOT_IS(0, ST_UNKNOWN), RK_SLOT_IS(1, ST_UNKNOWN), lowt, V0, V1);
       bool left = false;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < NSLOT; ++s) {
         if (!own[s]) continue;
         if (st[s] == ST_HIT_PENDING && ((V0 & cm[s].lo) | (V1 & cm[s].hi)) == 0 &&
             !fs[s].any_unknown)
@@ -673,17 +681,17 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
       if (!__ballot(changed) || !__ballot(left)) break;
     }
     SP_T(4);
-    A0 = __ballot(own[0] && st[0] == ST_ACTIVE);
-    A1 = __ballot(own[1] && st[1] == ST_ACTIVE);
+    win_ballot<NSLOT>(RK_SLOT_IS(0, ST_ACTIVE), RK_SLOT_IS(1, ST_ACTIVE), lowt, A0, A1);
+#undef RK_SLOT_IS
     // winners: the first strict maximum in scan order among the matching
     // ACTIVE candidates (own run newest first, then the neighbour run); a
     // single candidate needs no deviation
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NSLOT; ++s) {
       if (!own[s]) continue;
       pending |= st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING;
       if (st[s] == st0[s]) continue;
-      const uint32_t p = base + 64 * s + lane;
+      const uint32_t p = base + P[s];
       if (st[s] == ST_HIT) {
         const uint64_t ao = bits_from(A0, A1, rs[s]) & rown[s];
         const uint64_t an = rnb[s] ? bits_from(A0, A1, nbs[s]) & rnb[s] : 0;
@@ -692,8 +700,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
           win = ao ? ent[rs[s] + 63 - __clzll(ao)]
                    : an ? ent[nbs[s] + 63 - __clzll(an)] : fs[s].win;
         } else {
-          const int P = 64 * s + lane;
-          const Q32 q = make_q32(pk[P].x, pk[P].y, ax.len_ratio, ax.pos_ratio);
+          const Q32 q = make_q32(pk[P[s]].x, pk[P[s]].y, ax.len_ratio, ax.pos_ratio);
           double best = 0.0;
           win = NONE;
           uint64_t b = ao;
@@ -712,9 +719,9 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
           }
           if (fs[s].any_active && fs[s].best > best) win = fs[s].win;
         }
-        record_decision(ax, ent[64 * s + lane], ST_HIT, win);
+        record_decision(ax, ent[P[s]], ST_HIT, win);
       } else if (st[s] == ST_ACTIVE) {
-        record_decision(ax, ent[64 * s + lane], ST_ACTIVE, NONE);
+        record_decision(ax, ent[P[s]], ST_ACTIVE, NONE);
       }
       store_state(&ax.state[p], st[s]);
     }
@@ -722,6 +729,7 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     if (lane == 0) wpend[w] = wp;
 #ifdef RK_SWEEP_PROF
     SP_T(5);
+    const uint64_t o1 = __ballot(NSLOT == 2 && own[NSLOT - 1]);
     SP_ADD(0, _t1 - _t0);
     SP_ADD(1, _t2 - _t1);
     SP_ADD(2, _t3 - _t2);
@@ -729,13 +737,50 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     SP_ADD(4, _t5 - _t4);
     SP_ADD(5, nrounds);
     SP_ADD(6, 1);
-    SP_ADD(7, __ballot(own[1]) != 0);
-    SP_ADD(8, __popcll(__ballot(open[0] || open[1])));
-    SP_ADD(9, __popcll(__ballot(own[0] && (st0[0] == ST_UNKNOWN) && rs[0] == 64 * 0 + lane && !nd[0])));
-    SP_ADD(10, __ballot(fs[0].any_unknown || fs[1].any_unknown || fs[0].any_active || fs[1].any_active) != 0);
+    SP_ADD(7, o1 != 0);
+    SP_ADD(8, NSLOT == 1);
 #endif
     return wp;
   }
+}
+
+// One window: the keys and slot-0 records in one memory round trip, the run
+// starts, then the one-slot core when the last run's tail (t entries past
+// position 63) fits in the lanes before the window's first run start f.
+__device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8_t *wpend,
+                                               uint8_t *lflag, uint2 *pk,
+                                               uint32_t *ent, uint32_t *key, int lane) {
+  const uint32_t base = w * 64, m = ax.m;
+  uint64_t S0, S1;
+  const uint32_t p0 = base + lane;
+  uint2 pk0 = make_uint2(0, 0);
+  uint32_t ent0 = 0;
+  uint8_t st00 = ST_HIT, nd00 = 0;
+  if (p0 < m) pk0 = ax.pk[p0], ent0 = ax.ent[p0], st00 = ax.state[p0], nd00 = ax.nbd[p0];
+  {
+    const uint32_t p1 = base + 64 + lane;
+    const uint32_t k0 = p0 < m ? ax.key[p0] : NONE, k1 = p1 < m ? ax.key[p1] : NONE;
+    const uint32_t q0 = p0 < m && p0 > 0 ? ax.key[p0 - 1] : NONE;
+    const uint32_t q1 = p1 < m ? ax.key[p1 - 1] : NONE;
+    key[lane] = k0;
+    key[64 + lane] = k1;
+    S0 = __ballot(p0 >= m || p0 == 0 || q0 != k0);
+    S1 = __ballot(p1 >= m || q1 != k1);
+  }
+  // f: first run start of the window; t: how far the last run that starts in
+  // the window reaches past position 63 (0 when it does not, or is long)
+  const int f = S0 ? __builtin_ctzll(S0) : 64;
+  int t = 0;
+  if (S0) {
+    const int L = 63 - __clzll(S0);
+    const int re = S1 ? 64 + __builtin_ctzll(S1) : 128;
+    if (re > 64 && re - L <= (int)LONG_RUN && base + L < m) t = re - 64;
+  }
+  if (t <= f && t < 64)
+    return sweep_core32<1>(ax, w, wpend, lflag, pk, ent, key, lane, S0, S1, t, pk0, ent0, st00,
+                           nd00);
+  return sweep_core32<2>(ax, w, wpend, lflag, pk, ent, key, lane, S0, S1, t, pk0, ent0, st00,
+                         nd00);
 }
 
 // first sweep: one wavefront per window
@@ -1347,8 +1392,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
       (void)hipStreamSynchronize(st);
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sweep_prof), sizeof h);
       const double w = h[6] ? (double)h[6] : 1.0;
-      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f open/win %.1f trivial/win %.1f foreignwin %.3f\n",
-              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w, h[9] / w, h[10] / w);
+      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f one-slot windows %.3f\n",
+              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w);
       (void)hipMemsetAsync(g_sweep_prof_ptr(), 0, sizeof h, st);
     }
 #endif
