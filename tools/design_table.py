@@ -11,7 +11,7 @@ BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
 BENCH, CFG5 = "r2_bench.json", "r2_bench_cfg5.json"
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
-    ("k_onesweep", "one LSD pass over 16-B records: ballot ranks, LDS placement, decoupled look-back, digit-segment write-out (4 processing-order passes, 4 Y, 3 member)", "32 (pass 1: 41; last order pass: 57)"),
+    ("k_onesweep", "one LSD pass over 16-B records, 6144 per tile: ballot ranks, LDS placement in rounds of 4096 slots, decoupled look-back, digit-segment write-out (4 processing-order passes, 4 Y, 3 member)", "32 (pass 1: 41; last order pass: 57)"),
     ("k_nw_xcount", "entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
     ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "54"),
     ("k_sweep_fast", "occupancy decisions, first sweep: a wavefront per 64-position window, ballot rounds, 32-bit candidate tests", "26"),
@@ -22,8 +22,8 @@ JOBS = [
     ("k_jump", "chase parent chains to the root", "16"),
     ("k_nw_assign", "gid from the root's rank into each member record; member-sort histograms", "12"),
     ("k_group_offsets", "group bounds", "4"),
-    ("k_sort_small", "exact libstdc++ introsort, <= 16 members: stable rank (second stream)", "16 per member"),
-    ("k_sort_groups_reg", "17..64 members in registers by one wavefront (second stream)", "16 per member"),
+    ("k_sort_small", "groups of <= 16 members (insertion sort == stable rank): one dense pass over the member slots, singletons copy their tag (second stream)", "16 per member"),
+    ("k_sort_groups_reg", "17..64 members in registers (17..32: two groups per wavefront; second stream)", "16 per member"),
     ("k_sort_groups_lds", "65..2048 members in LDS, register-finished segments", "16 per member"),
     ("k_sort_groups_split", "groups above 2048: block-wide partitions down to 512-member segments", "16 per member"),
     ("k_sort_segments", "those segments, one LDS wavefront each", "16 per member"),
