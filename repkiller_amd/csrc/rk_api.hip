@@ -942,6 +942,8 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
   } else {
     bool narrow = true;
     for (uint32_t x = 0; x < m; ++x) narrow &= (keys[x] >> 32) == 0;
+    // one-element segments are not written by the group sort: their slot stays
+    (void)hipMemcpyAsync(dot, dt, M * 4, hipMemcpyDeviceToDevice, st);
     rk::sort_groups_exact(dg, doff, nseg, m, dk, dt, dot, dgs, rk::ScanScratch{dsc, sc},
                           ctx->host + 128, narrow, st);
     if (hipGetLastError() != hipSuccess ||

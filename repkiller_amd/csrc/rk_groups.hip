@@ -221,8 +221,10 @@ __global__ void k_emit(const uint32_t *otag, const uint32_t *sgid, const uint32_
                        uint32_t *out_order) {
   GRID_STRIDE(t, m) {
     const uint32_t g = sgid[t];
+    const uint32_t o = otag[t];  // issued beside the bounds (unwritten for a singleton)
     const uint32_t b = goff[g], e = goff[g + 1];
-    out_order[t] = mrow[otag[t]];
+    // a one-member group is not written by the group sort: its slot is itself
+    out_order[t] = mrow[e - b == 1 ? t : o];
     out_gid[t] = g;
     out_rep[t] = e - b == 1 ? 0 : (t == b ? 1 : 2);
   }

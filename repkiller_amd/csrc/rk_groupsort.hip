@@ -733,35 +733,36 @@ __global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, ui
   }
 }
 
-// Groups of 1..16 members (tier 0, not listed): __final_insertion_sort alone
-// sorts them, so a member's final slot is its stable rank inside the group.
-// One lane per member slot over the whole member array: a singleton copies
-// its tag; a member of a group of 2..16 compares its key with the group's
-// (independent loads, served by L1/L2: the group's lanes read the same line).
-__global__ void __launch_bounds__(256) k_sort_small(const uint32_t *sgid, const uint32_t *goff,
-                                                    uint32_t m, const uint64_t *key,
-                                                    const uint32_t *tag, uint32_t *otag) {
-  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
-    const uint32_t g = sgid[x];
+// Groups of 2..16 members (tier 0): __final_insertion_sort alone sorts them,
+// so a member's final slot is its stable rank inside the group.  Sixteen
+// lanes per group, four groups per wavefront: lane l loads member l (the
+// group's members are contiguous), ranks itself against the other lanes of
+// its segment by width-16 shuffles and writes its tag at its rank.
+// Singletons are not listed and not written: emit_result takes a one-member
+// group's slot as it is (tag[x] == x for every caller).
+__global__ void __launch_bounds__(256) k_sort_small(TierLists tl, const uint32_t *goff,
+                                                    const uint64_t *key, const uint32_t *tag,
+                                                    uint32_t *otag) {
+  uint32_t lo, hi;
+  tl.range(0, lo, hi);
+  const uint32_t l = threadIdx.x & 15;
+  for (uint32_t w = lo + ((blockIdx.x * blockDim.x + threadIdx.x) >> 4); w - lo < hi - lo;
+       w += (gridDim.x * blockDim.x) >> 4) {
+    const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
-    if (n > (uint32_t)THRESH) continue;
+    const bool in = l < n;
+    const uint64_t k = in ? key[b + l] : ~0ull;
     uint32_t r = 0;
-    if (n > 1) {
-      const uint64_t kx = key[x];
-      const uint32_t i = x - b;
 #pragma unroll
-      for (uint32_t j = 0; j < (uint32_t)THRESH; ++j) {
-        if (j < n) {
-          const uint64_t kj = key[b + j];
-          r += kj < kx || (kj == kx && j < i);
-        }
-      }
+    for (int j = 0; j < THRESH; ++j) {
+      const uint64_t kj = __shfl(k, j, 16);
+      r += (uint32_t)j < n && (kj < k || (kj == k && (uint32_t)j < l));
     }
-    otag[b + r] = tag[x];
+    if (in) otag[b + r] = tag[b + l];
   }
 }
 
-// Tiers by group size: 0 = 1..16 members (k_sort_small, not listed), 1 =
+// Tiers by group size (singletons: none): 0 = 2..16 members (k_sort_small), 1 =
 // 17..32 (registers, two groups per wavefront), 2 = 33..64 (registers), 3..6
 // = up to LDS_CAPS[t-3] (LDS), 7 = larger (global memory).  Small LDS caps
 // keep many wavefronts resident per CU (a 65..128-member group needs ~3 KB of
@@ -777,6 +778,7 @@ __host__ __device__ constexpr Caps lds_caps() { return Caps{{128, 256, 512, 2048
 
 __device__ __forceinline__ int tier_of(uint32_t n) {
   constexpr Caps caps = lds_caps();
+  if (n <= 1) return NTIER;  // a singleton: nothing to sort, nothing listed
   if (n <= (uint32_t)THRESH) return 0;
   if (n <= 32) return 1;
   if (n <= 64) return 2;
@@ -835,7 +837,7 @@ __global__ void __launch_bounds__(256) k_tier_lists(const uint32_t *goff, uint32
       if (lane == 0) wc[wv][u] = (uint32_t)__popcll(b);
     }
     __syncthreads();
-    if (g < g1 && t != 0) {  // tier 0 is served by a dense pass, not a list
+    if (g < g1 && t < NTIER) {  // singletons are not listed
       uint32_t before = 0;
       for (int k = 0; k < wv; ++k) before += wc[k][t];
 #pragma unroll
@@ -908,8 +910,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     (void)hipStreamWaitEvent(s2, ev_fork, 0);
   }
   kt_begin(s2);
-  // one slot per thread: the three dependent loads of a slot overlap across waves
-  k_sort_small<<<(m + 255) / 256, 256, 0, s2>>>(gid_sorted, goff, m, key, tag, otag);
+  k_sort_small<<<2048, 256, 0, s2>>>(tl, goff, key, tag, otag);
   kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
   tier_slot(0);
   kt_begin(s2);

@@ -207,7 +207,8 @@ void build_records(uint32_t *gmem, const ulonglong2 *hrec, uint32_t m, uint64_t 
                    uint32_t *tag, hipStream_t st);
 // ------------------------------------------------------- rk_groupsort.hip --
 size_t groupsort_scratch_bytes(uint32_t n);
-// libstdc++ std::sort of every group's (key, tag) records; sorted tags -> otag.
+// libstdc++ std::sort of every group's (key, tag) records; sorted tags -> otag
+// (groups of one member are left unwritten: their slot holds its own tag).
 // gid_sorted: group id of every record; host_words: >= 16 pinned words;
 // narrow_keys: every key fits 32 bits (LDS tiers stage 4-byte keys).
 // side (optional): a second stream for the tiers of <= 64 members, forked
