@@ -107,7 +107,8 @@ int resolve_axis(rk_ctx *ctx, const Axis &ax, SweepScratch sc, bool fast32, uint
   RunList rl{sc.runs, sc.wpend, 0, 0, fast32};
   build_runs(ax, rl, sc.dev_count, ctx->host + 128, ctx->stream);
   HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));
+  // the 32-bit path's first sweep sets the open flag of every long run itself
+  if (!fast32) HIPCHK(ctx, hipMemsetAsync(rpend, 1, ax.m, ctx->stream));
   *sweeps = 0;
   for (;;) {
     if (*sweeps > ax.m + 2) {

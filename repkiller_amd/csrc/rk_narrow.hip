@@ -647,7 +647,7 @@ int nw_shape() {
 
 template <int T, int ITEMS, int DB, bool PERSIST, class Src, class Dst>
 void launch_shape(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
-                  uint32_t *status, uint32_t *ctr, hipStream_t st) {
+                  uint32_t *status, uint32_t *ctr, hipStream_t st, uint32_t *clear_next) {
   const uint32_t tiles = (n + T * ITEMS - 1) / (T * ITEMS);
   auto kern = k_onesweep<T, ITEMS, DB, PERSIST, Src, Dst>;
   uint32_t grid = tiles;
@@ -655,36 +655,37 @@ void launch_shape(const Src &src, const Dst &dst, uint32_t n, int shift, const u
     static const uint32_t resident = resident_blocks(kern, T);
     grid = tiles < resident ? tiles : resident;
   }
-  kern<<<grid, T, 0, st>>>(src, dst, n, tiles, shift, ghist, status, ctr, trace_slot(tiles));
+  kern<<<grid, T, 0, st>>>(src, dst, n, tiles, shift, ghist, status, ctr, trace_slot(tiles),
+                           clear_next);
 }
 template <int DB, class Src, class Dst>
 void launch_pass_db(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
-                    uint32_t *status, uint32_t *ctr, hipStream_t st) {
+                    uint32_t *status, uint32_t *ctr, hipStream_t st, uint32_t *clear_next) {
   constexpr int ITEMS = DB >= 10 ? 12 : 16;
   if constexpr (DB == 8) {
     switch (nw_shape()) {
-      case 1: launch_shape<OS_T, 16, 8, true>(src, dst, n, shift, ghist, status, ctr, st); return;
-      case 2: launch_shape<256, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
-      case 3: launch_shape<256, 12, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
-      case 4: launch_shape<512, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
-      case 5: case 6: launch_shape<512, 16, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
-      case 7: launch_shape<512, 12, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
-      case 8: launch_shape<1024, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st); return;
+      case 1: launch_shape<OS_T, 16, 8, true>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
+      case 2: launch_shape<256, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
+      case 3: launch_shape<256, 12, 8, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
+      case 4: launch_shape<512, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
+      case 5: case 6: launch_shape<512, 16, 8, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
+      case 7: launch_shape<512, 12, 8, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
+      case 8: launch_shape<1024, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
       default: break;
     }
   }
-  launch_shape<OS_T, ITEMS, DB, false>(src, dst, n, shift, ghist, status, ctr, st);
+  launch_shape<OS_T, ITEMS, DB, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next);
 }
 template <class Src, class Dst>
 void launch_pass(const Src &src, const Dst &dst, uint32_t n, int shift, int db,
                  const uint32_t *ghist, uint32_t *status, uint32_t *ctr, hipStream_t st,
-                 double bytes) {
+                 double bytes, uint32_t *clear_next = nullptr) {
   if (!n) return;
   kt_begin(st);
   switch (db) {
-    case 8: launch_pass_db<8>(src, dst, n, shift, ghist, status, ctr, st); break;
-    case 9: launch_pass_db<9>(src, dst, n, shift, ghist, status, ctr, st); break;
-    default: launch_pass_db<10>(src, dst, n, shift, ghist, status, ctr, st); break;
+    case 8: launch_pass_db<8>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
+    case 9: launch_pass_db<9>(src, dst, n, shift, ghist, status, ctr, st, nullptr); break;
+    default: launch_pass_db<10>(src, dst, n, shift, ghist, status, ctr, st, nullptr); break;
   }
   kt_end(st, KID_ONESWEEP, bytes);
 }
@@ -737,6 +738,33 @@ static Digits to_digits(const NwDigits &o) {
   return D;
 }
 
+// Status words of one sort.  With 8-bit digits in every pass the buffer is
+// used as two halves: pass p publishes into half p & 1 and zeroes, tile by
+// tile, the other half for pass p + 1 (k_onesweep's clear_next), so a sort
+// needs one memset instead of one per pass; otherwise one buffer, cleared
+// before each pass.
+struct PassStatus {
+  uint32_t *base;
+  size_t half;
+  bool ahead;
+  uint32_t *use(int p) const { return ahead ? base + (size_t)(p & 1) * half : base; }
+  uint32_t *next(int p, int passes) const {
+    return ahead && p + 1 < passes ? base + (size_t)((p + 1) & 1) * half : nullptr;
+  }
+  // before pass p: the memset it still needs (none after a clear-ahead pass)
+  void prepare(int p, uint32_t n, const Digits &D, hipStream_t st) const {
+    if (ahead && p > 0) return;
+    const size_t words = ahead ? half : (size_t)tiles_for(n, D.db[p]) * ((size_t)1 << D.db[p]);
+    (void)hipMemsetAsync(use(p), 0, words * 4, st);
+  }
+};
+static PassStatus pass_status(uint32_t *status, uint32_t n, const Digits &D) {
+  bool all8 = true;
+  for (int p = 0; p < D.passes; ++p) all8 &= D.db[p] == 8;
+  const size_t half = (size_t)tiles_for(n, 8) * 256;
+  return PassStatus{status, half, all8 && 2 * half + 64 <= nw_status_words(n)};
+}
+
 void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
                    uint32_t nby, const NwDigits &a, const NwDigits &y, uint32_t *ghist,
                    uint32_t *yhist, uint32_t *ctrl, hipStream_t st) {
@@ -757,12 +785,13 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
   const Digits D = to_digits(a);
   const size_t sw = nw_status_words(n);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  const PassStatus ps = pass_status(status, n, D);
   // the final pass lands in Ra
   for (int p = 0; p < D.passes; ++p) {
     uint4 *out = ((D.passes - 1 - p) % 2 == 0) ? Ra : Rb;
     const uint4 *src = ((D.passes - p) % 2 == 0) ? Ra : Rb;  // the previous pass' output
-    const size_t status_bytes = (size_t)tiles_for(n, D.db[p]) * ((size_t)1 << D.db[p]) * 4;
-    (void)hipMemsetAsync(status, 0, status_bytes, st);
+    ps.prepare(p, n, D, st);
+    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     const bool last = p == D.passes - 1;
@@ -770,15 +799,15 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
     if (p == 0) {
       SrcFile sf{in.x_start, in.y_start, in.length, in.strand, vsize};
       if (last)
-        launch_pass(sf, dp, n, D.shift[p], D.db[p], gh, status, ctr, st, 25.0 * n + 32.0 * n);
+        launch_pass(sf, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 25.0 * n + 32.0 * n, nxt);
       else
-        launch_pass(sf, DstRec{out}, n, D.shift[p], D.db[p], gh, status, ctr, st,
-                    25.0 * n + 16.0 * n);
+        launch_pass(sf, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st,
+                    25.0 * n + 16.0 * n, nxt);
     } else if (last) {
-      launch_pass(SrcRec{src}, dp, n, D.shift[p], D.db[p], gh, status, ctr, st, 48.0 * n);
+      launch_pass(SrcRec{src}, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 48.0 * n, nxt);
     } else {
-      launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, status, ctr, st,
-                  32.0 * n);
+      launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st,
+                  32.0 * n, nxt);
     }
   }
 }
@@ -791,29 +820,30 @@ static void nw_sort_records(const uint4 *in, uint4 *t0, uint4 *t1, uint32_t m, c
   const Digits D = to_digits(dg);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  const PassStatus ps = pass_status(status, m, D);
   const uint4 *src = in;
   for (int p = 0; p < D.passes; ++p) {
-    const size_t status_bytes = (size_t)tiles_for(m, D.db[p]) * ((size_t)1 << D.db[p]) * 4;
-    (void)hipMemsetAsync(status, 0, status_bytes, st);
+    ps.prepare(p, m, D, st);
+    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     // key0: the first pass takes every record's key from its own array
     const double kb = p == 0 && key0 ? 4.0 * m : 0.0;
     if (p == D.passes - 1) {
       if (p == 0 && key0)
-        launch_pass(SrcRecKey{src, key0}, fin, m, D.shift[p], D.db[p], gh, status, ctr, st,
-                    16.0 * m + kb + final_bytes);
+        launch_pass(SrcRecKey{src, key0}, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st,
+                    16.0 * m + kb + final_bytes, nxt);
       else
-        launch_pass(SrcRec{src}, fin, m, D.shift[p], D.db[p], gh, status, ctr, st,
-                    16.0 * m + final_bytes);
+        launch_pass(SrcRec{src}, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st,
+                    16.0 * m + final_bytes, nxt);
     } else {
       uint4 *out = p % 2 == 0 ? t0 : t1;
       if (p == 0 && key0)
-        launch_pass(SrcRecKey{src, key0}, DstRec{out}, m, D.shift[p], D.db[p], gh, status, ctr,
-                    st, 32.0 * m + kb);
+        launch_pass(SrcRecKey{src, key0}, DstRec{out}, m, D.shift[p], D.db[p], gh, stp, ctr,
+                    st, 32.0 * m + kb, nxt);
       else
-        launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], gh, status, ctr, st,
-                    32.0 * m);
+        launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
+                    32.0 * m, nxt);
       src = out;
     }
   }
@@ -829,13 +859,13 @@ void nw_y_sort_head(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y
   const Digits D = to_digits(y);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  const PassStatus ps = pass_status(status, m, D);  // the tail pass' half is cleared here
   const uint4 *src = yrec;
   for (int p = 0; p + 1 < D.passes; ++p) {
-    const size_t status_bytes = (size_t)tiles_for(m, D.db[p]) * ((size_t)1 << D.db[p]) * 4;
-    (void)hipMemsetAsync(status, 0, status_bytes, st);
+    ps.prepare(p, m, D, st);
     uint4 *out = p % 2 == 0 ? tmp : const_cast<uint4 *>(yrec);
     launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], ghist_of(yhist, p),
-                status, status + sw - 64 + p, st, 32.0 * m);
+                ps.use(p), status + sw - 64 + p, st, 32.0 * m, ps.next(p, D.passes));
     src = out;
   }
 }
@@ -846,12 +876,12 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
   const size_t sw = nw_status_words(m);
   const int p = D.passes - 1;
   const uint4 *src = p == 0 ? yrec : (p - 1) % 2 == 0 ? tmp : yrec;
-  const size_t status_bytes = (size_t)tiles_for(m, D.db[p]) * ((size_t)1 << D.db[p]) * 4;
-  (void)hipMemsetAsync(status, 0, status_bytes, st);
+  const PassStatus ps = pass_status(status, m, D);
+  ps.prepare(p, m, D, st);  // a no-op after the head's clear-ahead
   if (p == 0) (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);
   launch_pass(SrcRec{src},
               DstCsr{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, xbits, cy.state}, m,
-              D.shift[p], D.db[p], ghist_of(yhist, p), status, status + sw - 64 + p, st,
+              D.shift[p], D.db[p], ghist_of(yhist, p), ps.use(p), status + sw - 64 + p, st,
               16.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0));
 }
 

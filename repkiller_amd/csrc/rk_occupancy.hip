@@ -520,7 +520,8 @@ __device__ __forceinline__ void win_ballot(bool c0, bool c1, uint64_t lowt, uint
 // start (most windows): every slot's code runs once instead of twice.
 template <int NSLOT>
 __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t *wpend,
-                                             uint8_t *lflag, uint2 *pk, uint32_t *ent,
+                                             uint8_t *lflag, uint8_t *rpend, uint2 *pk,
+                                             uint32_t *ent,
                                              uint32_t *key, int lane, uint64_t S0, uint64_t S1,
                                              int t, uint2 pk0, uint32_t ent0, uint8_t st00,
                                              uint8_t nd00) {
@@ -543,6 +544,7 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
         const bool lng = base + P[s] < m && rs[0] == P[s] && re - P[s] > (int)LONG_RUN;
         const uint64_t bb = __ballot(lng);
         if (lane == 0) lflag[w] = bb != 0;
+        if (lng) rpend[base + P[s]] = 1;  // the long-run kernel's "still open" flag
       }
       st[s] = ST_HIT;
       nd[s] = 0;
@@ -748,7 +750,7 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
 // starts, then the one-slot core when the last run's tail (t entries past
 // position 63) fits in the lanes before the window's first run start f.
 __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8_t *wpend,
-                                               uint8_t *lflag, uint2 *pk,
+                                               uint8_t *lflag, uint8_t *rpend, uint2 *pk,
                                                uint32_t *ent, uint32_t *key, int lane) {
   const uint32_t base = w * 64, m = ax.m;
   uint64_t S0, S1;
@@ -777,22 +779,24 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     if (re > 64 && re - L <= (int)LONG_RUN && base + L < m) t = re - 64;
   }
   if (t <= f && t < 64)
-    return sweep_core32<1>(ax, w, wpend, lflag, pk, ent, key, lane, S0, S1, t, pk0, ent0, st00,
-                           nd00);
-  return sweep_core32<2>(ax, w, wpend, lflag, pk, ent, key, lane, S0, S1, t, pk0, ent0, st00,
-                         nd00);
+    return sweep_core32<1>(ax, w, wpend, lflag, rpend, pk, ent, key, lane, S0, S1, t, pk0, ent0,
+                           st00, nd00);
+  return sweep_core32<2>(ax, w, wpend, lflag, rpend, pk, ent, key, lane, S0, S1, t, pk0, ent0,
+                         st00, nd00);
 }
 
-// first sweep: one wavefront per window
+// first sweep: one wavefront per window, every window (wpend and rpend are
+// written here, not read)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint8_t *lflag) {
+k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint8_t *lflag,
+             uint8_t *rpend) {
   __shared__ uint2 s_pk[4][128 + OWN_U];  // {centre low 32 bits, length}; read padding
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t w = blockIdx.x * 4 + wv;
   bool pending = false;
-  if (w < nwin && wpend[w])
-    pending = sweep_window32(ax, w, wpend, lflag, s_pk[wv], s_ent[wv], s_key[wv], lane);
+  if (w < nwin)
+    pending = sweep_window32(ax, w, wpend, lflag, rpend, s_pk[wv], s_ent[wv], s_key[wv], lane);
   count_pending(counters, pending && lane == 0);
 }
 
@@ -810,7 +814,7 @@ __global__ void __launch_bounds__(256) k_sweep_fast_more(Axis ax, uint8_t *wpend
       const int b = __builtin_ctzll(todo);
       todo &= todo - 1;
       wave_sync_lds();  // the previous window's LDS reads are done
-      pending |= sweep_window32(ax, w0 + b, wpend, nullptr, s_pk[wv], s_ent[wv],
+      pending |= sweep_window32(ax, w0 + b, wpend, nullptr, nullptr, s_pk[wv], s_ent[wv],
                                 s_key[wv], lane);
     }
   }
@@ -1356,8 +1360,8 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
   rl.nbig = 0;
   rl.nwin = (ax.m + 63) / 64;
   if (!ax.m) return;
+  if (rl.fast32) return;  // the first sweep flags the long runs and the windows itself
   (void)hipMemsetAsync(rl.wpend, 1, rl.nwin, st);
-  if (rl.fast32) return;  // the first sweep flags the long runs itself
   (void)hipMemsetAsync(dev_count, 0, 4, st);
   kt_begin(st);
   k_run_bounds<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.nwin, rl.big, dev_count);
@@ -1378,7 +1382,7 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     kt_begin(st);
     if (rl.fast32 && first)
       k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters,
-                                                      reinterpret_cast<uint8_t *>(rl.big));
+                                                      reinterpret_cast<uint8_t *>(rl.big), rpend);
     else if (rl.fast32)
       k_sweep_fast_more<<<((rl.nwin + 63) / 64 + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin,
                                                                        counters);

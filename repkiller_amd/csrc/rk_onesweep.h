@@ -80,7 +80,8 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
                                                 int shift, const uint32_t *__restrict__ ghist,
                                                 uint32_t *__restrict__ status,
                                                 uint32_t *__restrict__ tile_ctr,
-                                                uint64_t *__restrict__ trace) {
+                                                uint64_t *__restrict__ trace,
+                                                uint32_t *__restrict__ clear_next) {
   // thread t < RADIX / DPT owns digits [t*DPT, (t+1)*DPT)
   constexpr int RADIX = 1 << DB, NW = T / 64, TILE = T * ITEMS;
   constexpr int DPT = RADIX >= T ? RADIX / T : 1, OWNERS = RADIX / DPT;
@@ -140,6 +141,10 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     const uint32_t tile0 = tile * (uint32_t)TILE;
     const uint32_t cnt = n - tile0 < (uint32_t)TILE ? n - tile0 : (uint32_t)TILE;
     if (PERSIST && threadIdx.x == 0) s_tile[(it + 1) & 1] = atomicAdd(tile_ctr, 1u);
+    // the next pass' status row of this tile (same tiles, same radix), zeroed
+    // here instead of by a memset between the passes
+    if (clear_next)
+      for (uint32_t d = threadIdx.x; d < (uint32_t)RADIX; d += T) clear_next[(size_t)tile * RADIX + d] = 0;
     // 1: rank (the wave's own counter row: no block barrier before it)
     for (uint32_t d = lane; d < RADIX; d += 64) mycnt[d] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
