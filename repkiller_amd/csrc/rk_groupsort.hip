@@ -33,6 +33,7 @@
 // In every tier the result goes to `otag` (member order, group-major).
 #include "rk_internal.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -343,11 +344,26 @@ struct Frame {
   int d;
 };
 
+#ifdef RK_GS_PROF
+// measurement build only: shader cycles per phase of the LDS tiers' sort
+__device__ unsigned long long g_gs_prof[8];
+#define GS_T(k) const uint64_t _g##k = __builtin_amdgcn_s_memtime()
+#define GS_ADD(slot, v) do { if (lane == 0) atomicAdd(&g_gs_prof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define GS_T(k)
+#define GS_ADD(slot, v)
+#endif
+
 // the whole libstdc++ std::sort of one group [0, n) of view v, then stable
 // leaf ranks written to out[0..n) (tags only)
 template <bool GLOBAL, class V>
 __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stack,
-                              Frame *smallq, Frame *heapq, uint32_t lane, int d0) {
+                              Frame *smallq, Frame *heapq, uint32_t lane, int d0,
+                              uint32_t reg_max) {
+  GS_T(0);
+#ifdef RK_GS_PROF
+  uint64_t part_cyc = 0, nparts = 0;
+#endif
   for (uint32_t x = lane; x < n; x += 64) v.B[x] = 0;
   int sp = 0, nsmall = 0, nheap = 0;
   if (lane == 0) stack[0] = {0u, n, d0};
@@ -365,14 +381,21 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
         final_leaf = false;
         break;
       }
-      if (l - f <= 64) {  // small: finished in registers (reg_batch)
+      if (l - f <= reg_max) {  // small: finished in registers (reg_batch)
         if (lane == 0) smallq[nsmall] = {f, l, d};
         ++nsmall;
         final_leaf = false;
         break;
       }
       --d;
+#ifdef RK_GS_PROF
+      const uint64_t _p0 = __builtin_amdgcn_s_memtime();
+#endif
       const uint32_t cut = wave_partition<GLOBAL, V>(v, f, l, lane);
+#ifdef RK_GS_PROF
+      part_cyc += __builtin_amdgcn_s_memtime() - _p0;
+      ++nparts;
+#endif
       if (lane == 0) stack[sp] = {cut, l, d};
       ++sp;
       l = cut;
@@ -380,8 +403,15 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
     if (final_leaf && lane == 0) v.B[f] = 1;
     sync_mem<GLOBAL>();
   }
+  GS_T(1);
+#ifdef RK_GS_PROF
+  uint64_t nbatch = 0;
+#endif
   // small segments, packed up to three per 64-lane batch
   for (int q0 = 0; q0 < nsmall;) {
+#ifdef RK_GS_PROF
+    ++nbatch;
+#endif
     int tot = 0, q1 = q0;
     while (q1 < nsmall && tot + (int)(smallq[q1].l - smallq[q1].f) <= 64)
       tot += (int)(smallq[q1].l - smallq[q1].f), ++q1;
@@ -393,28 +423,55 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
     q0 = q1;
   }
   sync_mem<GLOBAL>();
+  GS_T(2);
   for (int q = (int)lane; q < nheap; q += 64) heap_sort_segment(v, heapq[q].f, heapq[q].l);
   sync_mem<GLOBAL>();
   // __final_insertion_sort == stable sort inside every leaf (segments
-  // finished in registers are already written, B == 3)
-  for (uint32_t x = lane; x < n; x += 64) {
-    if (v.B[x] == 3) continue;
-    if (v.B[x] == 2) {
-      out[x] = v.T[x];
-      continue;
+  // finished in registers are already written, B == 3).  A leaf is a B == 1
+  // start followed by B == 0 positions (at most 16); its bounds come from one
+  // ballot over this chunk's B and one over the next chunk's, and the rank
+  // reads are independent (one LDS round trip).
+  uint32_t carry = 0;  // start of the leaf still open at the end of the previous chunk
+  for (uint32_t c = 0; c < n; c += 64) {
+    const uint32_t x = c + lane;
+    const uint8_t b = x < n ? v.B[x] : 1;
+    const uint8_t bn = x + 64 < n ? v.B[x + 64] : 1;
+    const uint64_t bd = __ballot(b != 0), bdn = __ballot(bn != 0);
+    const uint64_t upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
+    const uint64_t le = bd & upto, gt = bd & ~upto;
+    const uint32_t s = le ? c + 63 - (uint32_t)__clzll(le) : carry;
+    const uint32_t e = gt ? c + (uint32_t)__builtin_ctzll(gt)
+                          : bdn ? c + 64 + (uint32_t)__builtin_ctzll(bdn) : c + 128;
+    if (bd) carry = c + 63 - (uint32_t)__clzll(bd);
+    if (x < n && b != 3) {
+      if (b == 2) {
+        out[x] = v.T[x];
+      } else {
+        const typename V::key_t kx = v.K[x];
+        typename V::key_t ky[THRESH];
+#pragma unroll
+        for (int j = 0; j < THRESH; ++j) ky[j] = v.K[s + j < e ? s + j : x];
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < THRESH; ++j)
+          r += s + j < e && (ky[j] < kx || (ky[j] == kx && s + j < x));
+        out[s + r] = v.T[x];
+      }
     }
-    uint32_t s = x;
-    while (v.B[s] == 0) --s;
-    uint32_t e = x + 1;
-    while (e < n && v.B[e] == 0) ++e;
-    const typename V::key_t kx = v.K[x];
-    uint32_t r = 0;
-    for (uint32_t y = s; y < e; ++y) {
-      const typename V::key_t ky = v.K[y];
-      r += (ky < kx) || (ky == kx && y < x);
-    }
-    out[s + r] = v.T[x];
   }
+#ifdef RK_GS_PROF
+  GS_T(3);
+  if (!GLOBAL) {
+    GS_ADD(0, _g1 - _g0 - part_cyc);  // init + stack walk outside the partitions
+    GS_ADD(1, part_cyc);
+    GS_ADD(2, _g2 - _g1);             // register batches
+    GS_ADD(3, _g3 - _g2);             // heap + final insertion pass
+    GS_ADD(4, nparts);
+    GS_ADD(5, nbatch);
+    GS_ADD(6, 1);
+    GS_ADD(7, n);
+  }
+#endif
 }
 
 // The listed tiers' groups, tier-major in one array: tier u (1..6) owns
@@ -467,7 +524,7 @@ template <class KT>
 __global__ void __launch_bounds__(64) k_sort_groups_lds(TierLists tl, int tier,
                                                         const uint32_t *goff, const uint64_t *key,
                                                         const uint32_t *tag, uint32_t *otag,
-                                                        uint32_t cap) {
+                                                        uint32_t cap, uint32_t reg_max) {
   extern __shared__ __align__(16) uint8_t smem[];
   const uint32_t lane = threadIdx.x;
   const uint32_t nfr = cap / (THRESH + 1) + 2;
@@ -490,7 +547,8 @@ __global__ void __launch_bounds__(64) k_sort_groups_lds(TierLists tl, int tier,
       T[x] = tag[b + x];
     }
     wave_sync();
-    wave_std_sort<false>(v, n, otag + b, stack, smallq, heapq, lane, 2 * (31 - __clz((int)n)));
+    wave_std_sort<false>(v, n, otag + b, stack, smallq, heapq, lane, 2 * (31 - __clz((int)n)),
+                         reg_max);
     wave_sync();
   }
 }
@@ -697,7 +755,7 @@ template <class KT>
 __global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, uint32_t m,
                                                       const uint8_t *bnd, const uint32_t *head,
                                                       const uint64_t *key, const uint32_t *tag,
-                                                      uint32_t *otag) {
+                                                      uint32_t *otag, uint32_t reg_max) {
   {
     uint32_t lo, hi;
     tl.range(tier, lo, hi);
@@ -727,7 +785,7 @@ __global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, ui
         T[y] = tag[x + y];
       }
       wave_sync();
-      wave_std_sort<false>(v, n, otag + x, stack, smallq, heapq, lane, (int)(h >> 16));
+      wave_std_sort<false>(v, n, otag + x, stack, smallq, heapq, lane, (int)(h >> 16), reg_max);
       wave_sync();
     }
   }
@@ -921,6 +979,14 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   k_sort_groups_reg<1><<<4096, 256, 0, s2>>>(tl, 2, goff, key, tag, otag);
   kt_end(s2, KID_SORT_REG, 0.0);
   tier_slot(2);
+  // segments of 17..reg_max members inside the LDS tiers would be finished in
+  // registers (reg_batch); by default (0) the LDS partitions go down to the
+  // leaves, which the vectorised final pass ranks -- LDS tiers 1.29 -> 1.25
+  // ms at cfg3 (RK_GS_REGMAX=64 restores the register batches)
+  static const uint32_t reg_max = [] {
+    const char *e = getenv("RK_GS_REGMAX");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
   // the first `lds_side` LDS tiers also run on `side` (RK_GS_SIDE, measurements)
   static const int lds_side = [] {
     const char *e = getenv("RK_GS_SIDE");
@@ -936,14 +1002,29 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
       kt_begin(sj);
       if (narrow_keys)
         k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), sj>>>(tl, TIER_LDS0 + j, goff,
-                                                                         key, tag, otag, cap);
+                                                                         key, tag, otag, cap,
+                                                                         reg_max);
       else
         k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), sj>>>(tl, TIER_LDS0 + j, goff,
-                                                                         key, tag, otag, cap);
+                                                                         key, tag, otag, cap,
+                                                                         reg_max);
       kt_end(sj, KID_SORT_LDS, 0.0);
       tier_slot(TIER_LDS0 + j);
     }
   }
+#ifdef RK_GS_PROF
+  {
+    unsigned long long h[8];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_gs_prof), sizeof h);
+    const double g = h[6] ? (double)h[6] : 1.0;
+    fprintf(stderr, "GSPROF groups=%llu members/group %.1f cyc/group: stack %.0f partitions %.0f batches %.0f final %.0f | partitions/group %.2f batches/group %.2f\n",
+            h[6], h[7] / g, h[0] / g, h[1] / g, h[2] / g, h[3] / g, h[4] / g, h[5] / g);
+    void *p = nullptr;
+    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_gs_prof));
+    (void)hipMemsetAsync(p, 0, sizeof h, st);
+  }
+#endif
   // phase A marks the final segments' starts in bnd (cleared first); both
   // kernels return at once when no group is that large
   k_clear_if_tier<<<1024, 256, 0, st>>>(tl, NTIER - 1, bnd, m);
@@ -954,10 +1035,10 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   kt_begin(st);
   if (narrow_keys)
     k_sort_segments<uint32_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 4), st>>>(
-        tl, NTIER - 1, m, bnd, pl, key, tag, otag);
+        tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max);
   else
     k_sort_segments<uint64_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 8), st>>>(
-        tl, NTIER - 1, m, bnd, pl, key, tag, otag);
+        tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max);
   kt_end(st, KID_SORT_SEGS, 0.0);
   tier_slot(NTIER);
   if (side) (void)hipStreamWaitEvent(st, ev_join, 0);
