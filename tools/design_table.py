@@ -22,9 +22,9 @@ JOBS = [
     ("k_jump", "chase parent chains to the root", "16"),
     ("k_nw_assign", "gid from the root's rank into each member record; member-sort histograms", "12"),
     ("k_group_offsets", "group bounds", "4"),
-    ("k_sort_small", "groups of <= 16 members (insertion sort == stable rank): one dense pass over the member slots, singletons copy their tag (second stream)", "16 per member"),
+    ("k_sort_small", "groups of 2..16 members (insertion sort == stable rank): 16 lanes per group from the tier list, width-16 shuffles; singletons are not touched (second stream)", "16 per member"),
     ("k_sort_groups_reg", "17..64 members in registers (17..32: two groups per wavefront; second stream)", "16 per member"),
-    ("k_sort_groups_lds", "65..2048 members in LDS, register-finished segments", "16 per member"),
+    ("k_sort_groups_lds", "65..2048 members in LDS: partitions down to the leaves, then the final insertion pass with ballot-found leaf bounds", "16 per member"),
     ("k_sort_groups_split", "groups above 2048: block-wide partitions down to 512-member segments", "16 per member"),
     ("k_sort_segments", "those segments, one LDS wavefront each", "16 per member"),
     ("k_emit", "gid, flag, output order", "29"),
