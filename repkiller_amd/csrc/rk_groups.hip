@@ -189,13 +189,16 @@ __global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, u
       p.par[k] = k;
     }
     if (isnew) isnew[k] = a == k;
-    for (int step = 0; step < 32; ++step) {
+    int step = 0;
+    for (; step < 32; ++step) {
       const uint32_t b = p.par[a];
       if (b == a) break;
       a = b;
     }
     if (a != a0) p.par[k] = a;
-    if (p.par[a] != a) ch = true;
+    // a root stays a root (only non-roots' parents are rewritten), so a chain
+    // that ended on one is final; 32 jumps without reaching one need a round more
+    if (step == 32) ch = true;
   }
   if (ch) *changed = 1u;
 }
@@ -280,7 +283,7 @@ void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t
                 hipStream_t st) {
   if (!m) return;
   kt_begin(st);
-  k_jump<<<grid_for(m, 256), 256, 0, st>>>(p, m, changed, isnew, err);
+  k_jump<<<grid_for(m, 256, (size_t)1 << 20), 256, 0, st>>>(p, m, changed, isnew, err);
   kt_end(st, KID_JUMP, (isnew ? 16.0 : 12.0) * m);  // parent, root, parent written (+ new flag)
 }
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {
