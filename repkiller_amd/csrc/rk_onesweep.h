@@ -22,11 +22,18 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 // ids come from an atomic counter in dispatch order, so every earlier tile is
 // resident or done and publishes its AGG before it waits on anything.
 // The walk reads LB_BATCH predecessors per round trip (hundreds of tiles are
-// resident; the nearest INC is often dozens back).  Measured per tile at cfg3
+// resident; the nearest INC is often dozens back; fewer words per trip keep
+// the status traffic down).  Measured per tile at cfg3
 // (RK_NW_TRACE): the look-back is ~9-10 us of ~16 us at 32; 64 reads per round
 // trip made it 13 us (the status traffic itself), a wave per digit reading 64
 // tiles per load (status[digit][tile]) 36-47 us.
-constexpr uint32_t LB_BATCH = 32;
+// RK_LB_BATCH (compile time): predecessors read per round trip.  With
+// 6144-record tiles, cfg3 step 8 / 12 / 16 / 24 / 32 / 48: 12.00-12.03 /
+// 12.04-12.10 / 12.00-12.08 / 12.05-12.21 / 12.29-12.32 / 12.51-12.54 ms
+#ifndef RK_LB_BATCH
+#define RK_LB_BATCH 16
+#endif
+constexpr uint32_t LB_BATCH = RK_LB_BATCH;
 __device__ __forceinline__ uint32_t look_back(uint32_t *status, uint32_t tile, uint32_t stride,
                                               uint32_t slot, uint32_t mine) {
   uint32_t acc = 0;
