@@ -33,6 +33,11 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 #ifndef RK_LB_BATCH
 #define RK_LB_BATCH 16
 #endif
+// RK_LB_SLEEP: s_sleep units between polls of unpublished tiles (0 / 1 / 4:
+// 12.09-12.10 / 12.12-12.14 / 12.10-12.18 ms, neutral)
+#ifndef RK_LB_SLEEP
+#define RK_LB_SLEEP 1
+#endif
 constexpr uint32_t LB_BATCH = RK_LB_BATCH;
 __device__ __forceinline__ uint32_t look_back(uint32_t *status, uint32_t tile, uint32_t stride,
                                               uint32_t slot, uint32_t mine) {
@@ -57,7 +62,7 @@ __device__ __forceinline__ uint32_t look_back(uint32_t *status, uint32_t tile, u
     }
     if (done) break;
     j -= k;
-    if (k < cnt) __builtin_amdgcn_s_sleep(1);
+    if (RK_LB_SLEEP && k < cnt) __builtin_amdgcn_s_sleep(RK_LB_SLEEP);
   }
   sw_store(&status[(size_t)tile * stride + slot], SW_INC | (acc + mine));
   return acc;
