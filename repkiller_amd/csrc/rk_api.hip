@@ -534,7 +534,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     // members (stable by gid => processing order), in-group order, flags
     if (prof) mark(ctx, RK_PH_MEMBERS);
     rk::nw_member_sort(w.erec, w.isnew, w.Ra, w.Rb, m, ed, w.ehist, w.astatus, w.sgid, w.reckey,
-                       w.tag, w.mrow, st);
+                       w.tag, w.mrow, narrow_keys, st);
     rk::group_offsets(w.sgid, m, G, w.goff, st);
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
     rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,

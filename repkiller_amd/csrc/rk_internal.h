@@ -268,6 +268,7 @@ void nw_assign(const uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uin
                const NwDigits &e, uint32_t *ehist, hipStream_t st);
 void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1, uint32_t m,
                     const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint32_t *sgid,
-                    uint64_t *key, uint32_t *tag, uint32_t *mrow, hipStream_t st);
+                    uint64_t *key, uint32_t *tag, uint32_t *mrow, bool narrow_keys,
+                    hipStream_t st);
 
 }  // namespace rk

@@ -120,15 +120,48 @@ struct SrcRecKey {
   }
   __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
 };
+// 12-B records (the Y axis' records, and the member records when every sort
+// key fits 32 bits), key = .x
+struct SrcRec12 {
+  using rec_t = uint3;
+  const uint3 *in;
+  __device__ __forceinline__ uint3 load(uint32_t i) const {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
+    return make_uint3(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
+                      __builtin_nontemporal_load(p + 2));
+  }
+  __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
+};
+// the member records of the X chunk kernel {0, row, key lo, key hi} with the
+// gid from its own array, as 12-B records {gid, row, key}
+struct SrcMem12 {
+  using rec_t = uint3;
+  const uint4 *in;
+  const uint32_t *key0;
+  __device__ __forceinline__ uint3 load(uint32_t i) const {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(in + i));
+    return make_uint3(__builtin_nontemporal_load(key0 + i), v.y, v.z);
+  }
+  __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
+};
 // Dst::wave(rec, live): called by every lane of a wave for consecutive
 // sorted slots of the tile (kWave = false: not at all)
 #define RK_NO_WAVE                   \
   static constexpr bool kWave = false; \
-  __device__ __forceinline__ void wave(const uint4 &, bool) const {}
+  template <class R_>                  \
+  __device__ __forceinline__ void wave(const R_ &, bool) const {}
 struct DstRec {
   RK_NO_WAVE
   uint4 *out;
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const { out[pos] = r; }
+};
+struct DstRec12 {
+  RK_NO_WAVE
+  uint3 *out;
+  __device__ __forceinline__ void store(uint32_t pos, const uint3 &r) const {
+    uint32_t *p = reinterpret_cast<uint32_t *>(out + pos);
+    p[0] = r.x, p[1] = r.y, p[2] = r.z;
+  }
 };
 
 // arr[v] += the length of every run of equal v != NONE over consecutive lanes
@@ -165,16 +198,19 @@ struct SrcFile {
 };
 // --- processing order, last pass: the records, and the Y axis' input -------
 // Yrec: {strand * nby + centre/100, processing index, centre low 32, length}
+// 12-B Yrec: {strand * nby + centre/100, processing index, length (24) |
+// centre % 100 (7) << 24}; the centre is the bucket * 100 + the remainder
 struct DstProc {
   RK_NO_WAVE
-  uint4 *out, *yrec;
+  uint4 *out;
+  uint3 *yrec;
   uint32_t nby;
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const {
     out[pos] = r;
     const uint64_t ys = rec_y(r);
     const uint32_t len = rec_len(r), s = rec_strand(r);
     const uint64_t yc = ys + len / 2;
-    yrec[pos] = make_uint4(s * nby + (uint32_t)(yc / 100), pos, (uint32_t)yc, len);
+    yrec[pos] = make_uint3(s * nby + (uint32_t)(yc / 100), pos, len | (uint32_t)(yc % 100) << 24);
   }
 };
 
@@ -186,13 +222,12 @@ struct DstCsr {
   uint8_t *nbd;
   uint32_t nb;
   uint64_t max_index;
-  __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const {
+  __device__ __forceinline__ void store(uint32_t pos, const uint3 &r) const {
     key[pos] = r.x;
     ent[pos] = r.y;
-    pk[pos] = make_uint2(r.z, r.w);
     const uint32_t b = r.x >= nb ? r.x - nb : r.x;
-    const uint64_t base = (uint64_t)b * 100;
-    const uint64_t c = base + (uint32_t)(r.z - (uint32_t)base);  // centre from bucket + low bits
+    const uint64_t c = (uint64_t)b * 100 + (r.z >> 24);  // centre = bucket * 100 + remainder
+    pk[pos] = make_uint2((uint32_t)c, r.z & 0xFFFFFFu);
     nbd[pos] = nbd_code_nw(c, max_index);
     // with the X results (bitmask by processing index): the Y states -- X hits
     // sit in the Y lists (commonFunctions.cpp:59), X misses query them
@@ -213,6 +248,12 @@ struct DstMembers {
     sgid[pos] = r.x;
     mrow[pos] = r.y;
     key[pos] = (uint64_t)r.w << 32 | r.z;
+    tag[pos] = pos;
+  }
+  __device__ __forceinline__ void store(uint32_t pos, const uint3 &r) const {
+    sgid[pos] = r.x;
+    mrow[pos] = r.y;
+    key[pos] = r.z;
     tag[pos] = pos;
   }
 };
@@ -567,6 +608,14 @@ Digits plan_digits(int bits) {
 }
 
 constexpr int OS_T = 256;
+// 12-B record passes (the Y axis; the members when every sort key fits 32
+// bits): 512 threads x RK_NW_ITEMS12 records, placed through LDS in rounds of
+// 5461 slots.  14 (7168 per tile, 128 VGPRs: two blocks per CU): cfg3 step
+// 11.54-11.58 ms; 12: 11.59-11.66; 16 (142 VGPRs, one block per CU) not run;
+// the same passes on 16-B records: 12.14-12.16 ms
+#ifndef RK_NW_ITEMS12
+#define RK_NW_ITEMS12 14
+#endif
 int nw_shape();
 // records per tile of a pass with DB-bit digits (the shape of launch_pass_db)
 uint32_t tile_records(int db) {
@@ -662,7 +711,12 @@ template <int DB, class Src, class Dst>
 void launch_pass_db(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
                     uint32_t *status, uint32_t *ctr, hipStream_t st, uint32_t *clear_next) {
   constexpr int ITEMS = DB >= 10 ? 12 : 16;
-  if constexpr (DB == 8) {
+  if constexpr (DB == 8 && sizeof(typename Src::rec_t) == 12) {
+    // 12-B records: RK_NW_ITEMS12 per thread (LDS rounds of 5461 slots)
+    launch_shape<512, RK_NW_ITEMS12, 8, false>(src, dst, n, shift, ghist, status, ctr, st,
+                                               clear_next);
+    return;
+  } else if constexpr (DB == 8) {
     switch (nw_shape()) {
       case 1: launch_shape<OS_T, 16, 8, true>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
       case 2: launch_shape<256, 8, 8, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next); return;
@@ -795,16 +849,16 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     const bool last = p == D.passes - 1;
-    const DstProc dp{out, yrec, nby};
+    const DstProc dp{out, reinterpret_cast<uint3 *>(yrec), nby};
     if (p == 0) {
       SrcFile sf{in.x_start, in.y_start, in.length, in.strand, vsize};
       if (last)
-        launch_pass(sf, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 25.0 * n + 32.0 * n, nxt);
+        launch_pass(sf, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 25.0 * n + 28.0 * n, nxt);
       else
         launch_pass(sf, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st,
                     25.0 * n + 16.0 * n, nxt);
     } else if (last) {
-      launch_pass(SrcRec{src}, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 48.0 * n, nxt);
+      launch_pass(SrcRec{src}, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 44.0 * n, nxt);
     } else {
       launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st,
                   32.0 * n, nxt);
@@ -860,12 +914,13 @@ void nw_y_sort_head(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
   const PassStatus ps = pass_status(status, m, D);  // the tail pass' half is cleared here
-  const uint4 *src = yrec;
+  // 12-B records (DstProc); the buffers are uint4 arrays, large enough
+  const uint3 *src = reinterpret_cast<const uint3 *>(yrec);
   for (int p = 0; p + 1 < D.passes; ++p) {
     ps.prepare(p, m, D, st);
-    uint4 *out = p % 2 == 0 ? tmp : const_cast<uint4 *>(yrec);
-    launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], ghist_of(yhist, p),
-                ps.use(p), status + sw - 64 + p, st, 32.0 * m, ps.next(p, D.passes));
+    uint3 *out = reinterpret_cast<uint3 *>(p % 2 == 0 ? tmp : const_cast<uint4 *>(yrec));
+    launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], ghist_of(yhist, p),
+                ps.use(p), status + sw - 64 + p, st, 24.0 * m, ps.next(p, D.passes));
     src = out;
   }
 }
@@ -875,21 +930,57 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
   const Digits D = to_digits(y);
   const size_t sw = nw_status_words(m);
   const int p = D.passes - 1;
-  const uint4 *src = p == 0 ? yrec : (p - 1) % 2 == 0 ? tmp : yrec;
+  const uint3 *src = reinterpret_cast<const uint3 *>(p == 0 ? yrec : (p - 1) % 2 == 0 ? tmp : yrec);
   const PassStatus ps = pass_status(status, m, D);
   ps.prepare(p, m, D, st);  // a no-op after the head's clear-ahead
   if (p == 0) (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);
-  launch_pass(SrcRec{src},
+  launch_pass(SrcRec12{src},
               DstCsr{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, xbits, cy.state}, m,
               D.shift[p], D.db[p], ghist_of(yhist, p), ps.use(p), status + sw - 64 + p, st,
-              16.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0));
+              12.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0));
 }
 
+// 12-B member records {gid, row, key} when every sort key fits 32 bits
+static void nw_member_sort12(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1,
+                             uint32_t m, const NwDigits &dg, const uint32_t *ghist,
+                             uint32_t *status, const DstMembers &fin, hipStream_t st) {
+  const Digits D = to_digits(dg);
+  const size_t sw = nw_status_words(m);
+  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  const PassStatus ps = pass_status(status, m, D);
+  const uint3 *src = nullptr;
+  for (int p = 0; p < D.passes; ++p) {
+    ps.prepare(p, m, D, st);
+    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
+    uint32_t *ctr = status + sw - 64 + p;
+    const uint32_t *gh = ghist + p * 1024;
+    const bool last = p == D.passes - 1;
+    uint3 *out = reinterpret_cast<uint3 *>(p % 2 == 0 ? t0 : t1);
+    if (p == 0) {
+      const SrcMem12 s0{erec, gidp};
+      if (last)
+        launch_pass(s0, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st, 20.0 * m + 20.0 * m, nxt);
+      else
+        launch_pass(s0, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, 32.0 * m, nxt);
+    } else if (last) {
+      launch_pass(SrcRec12{src}, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st,
+                  12.0 * m + 20.0 * m, nxt);
+    } else {
+      launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
+                  24.0 * m, nxt);
+    }
+    src = out;
+  }
+}
 void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1, uint32_t m,
                     const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint32_t *sgid,
-                    uint64_t *key, uint32_t *tag, uint32_t *mrow, hipStream_t st) {
-  nw_sort_records(erec, t0, t1, m, e, ehist, status, DstMembers{sgid, tag, mrow, key}, 20.0 * m,
-                  st, gidp);
+                    uint64_t *key, uint32_t *tag, uint32_t *mrow, bool narrow_keys,
+                    hipStream_t st) {
+  if (narrow_keys)
+    nw_member_sort12(erec, gidp, t0, t1, m, e, ehist, status, DstMembers{sgid, tag, mrow, key}, st);
+  else
+    nw_sort_records(erec, t0, t1, m, e, ehist, status, DstMembers{sgid, tag, mrow, key}, 20.0 * m,
+                    st, gidp);
 }
 
 uint32_t nw_chunk_width(uint32_t m, uint32_t nbx) {
