@@ -132,17 +132,30 @@ struct SrcRec12 {
   }
   __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
 };
-// the member records of the X chunk kernel {0, row, key lo, key hi} with the
-// gid from its own array, as 12-B records {gid, row, key}
+// the member records of the X chunk kernel ({row, key low} + key high) with
+// the gid from its own array, as 12-B {gid, row, key} or 16-B {gid, row, key
+// low, key high} records
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 struct SrcMem12 {
   using rec_t = uint3;
-  const uint4 *in;
-  const uint32_t *key0;
+  const uint2 *erk;
+  const uint32_t *gid;
   __device__ __forceinline__ uint3 load(uint32_t i) const {
-    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(in + i));
-    return make_uint3(__builtin_nontemporal_load(key0 + i), v.y, v.z);
+    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u *>(erk + i));
+    return make_uint3(__builtin_nontemporal_load(gid + i), v.x, v.y);
   }
   __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
+};
+struct SrcMem16 {
+  using rec_t = uint4;
+  const uint2 *erk;
+  const uint32_t *ehi, *gid;
+  __device__ __forceinline__ uint4 load(uint32_t i) const {
+    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u *>(erk + i));
+    return make_uint4(__builtin_nontemporal_load(gid + i), v.x, v.y,
+                      __builtin_nontemporal_load(ehi + i));
+  }
+  __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
 };
 // Dst::wave(rec, live): called by every lane of a wave for consecutive
 // sorted slots of the tile (kWave = false: not at all)
@@ -401,7 +414,8 @@ struct XChunkArgs {
   const uint32_t *xoff;  // [2 nch] strand-major entry offsets, [nch + 1] owner row starts (+ m)
   Csr out;
   uint32_t *xpos;        // X position of every fragment (processing index)
-  uint4 *erec;           // member records (processing order)
+  uint2 *erk;            // member records (processing order): {file row, sort key low 32}
+  uint32_t *ehi;         // ... and the sort key's high 32 bits
   uint32_t *ctrl;        // [6] some sort key >= 2^32
 };
 
@@ -462,7 +476,8 @@ __global__ void __launch_bounds__(64 * XC_WAVES) k_nw_xchunk(XChunkArgs a) {
           above ? __shfl(ys, (int)__builtin_ctzll(above)) : carry_end;  // all lanes shuffle
       if (live && k >= kO) {
         const uint64_t h = ys > end_ys ? ys - end_ys : end_ys - ys;
-        a.erec[k] = make_uint4(0, r.y, (uint32_t)h, (uint32_t)(h >> 32));
+        a.erk[k] = make_uint2(r.y, (uint32_t)h);
+        a.ehi[k] = (uint32_t)(h >> 32);
         wide |= (h >> 32) != 0;
       }
       carry_key = __shfl(key, 0);
@@ -940,34 +955,34 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
               12.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0));
 }
 
-// 12-B member records {gid, row, key} when every sort key fits 32 bits
-static void nw_member_sort12(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1,
-                             uint32_t m, const NwDigits &dg, const uint32_t *ghist,
-                             uint32_t *status, const DstMembers &fin, hipStream_t st) {
+// The member sort by gid: 12-B records {gid, row, key} when every sort key
+// fits 32 bits, else 16-B {gid, row, key low, key high}; pass 1 reads the X
+// chunk kernel's {row, key low} (+ key high) and the gids.
+template <class Rec, class Src1, class SrcN, class DstN>
+static void nw_member_passes(const Src1 &s1, Rec *t0, Rec *t1, uint32_t m, const NwDigits &dg,
+                             const uint32_t *ghist, uint32_t *status, const DstMembers &fin,
+                             hipStream_t st) {
   const Digits D = to_digits(dg);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
   const PassStatus ps = pass_status(status, m, D);
-  const uint3 *src = nullptr;
+  const double rb = sizeof(Rec), in1 = sizeof(Rec) == 12 ? 12.0 : 16.0;
+  const Rec *src = nullptr;
   for (int p = 0; p < D.passes; ++p) {
     ps.prepare(p, m, D, st);
     uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     const bool last = p == D.passes - 1;
-    uint3 *out = reinterpret_cast<uint3 *>(p % 2 == 0 ? t0 : t1);
+    Rec *out = p % 2 == 0 ? t0 : t1;
+    const double in_b = p == 0 ? in1 : rb, out_b = last ? 20.0 : rb;
     if (p == 0) {
-      const SrcMem12 s0{erec, gidp};
-      if (last)
-        launch_pass(s0, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st, 20.0 * m + 20.0 * m, nxt);
-      else
-        launch_pass(s0, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, 32.0 * m, nxt);
+      if (last) launch_pass(s1, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st, (in_b + out_b) * m, nxt);
+      else launch_pass(s1, DstN{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, (in_b + out_b) * m, nxt);
     } else if (last) {
-      launch_pass(SrcRec12{src}, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st,
-                  12.0 * m + 20.0 * m, nxt);
+      launch_pass(SrcN{src}, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st, (in_b + out_b) * m, nxt);
     } else {
-      launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
-                  24.0 * m, nxt);
+      launch_pass(SrcN{src}, DstN{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, (in_b + out_b) * m, nxt);
     }
     src = out;
   }
@@ -976,11 +991,16 @@ void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t
                     const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint32_t *sgid,
                     uint64_t *key, uint32_t *tag, uint32_t *mrow, bool narrow_keys,
                     hipStream_t st) {
+  const uint2 *erk = reinterpret_cast<const uint2 *>(erec);
+  const uint32_t *ehi = reinterpret_cast<const uint32_t *>(erk + m);
+  const DstMembers fin{sgid, tag, mrow, key};
   if (narrow_keys)
-    nw_member_sort12(erec, gidp, t0, t1, m, e, ehist, status, DstMembers{sgid, tag, mrow, key}, st);
+    nw_member_passes<uint3, SrcMem12, SrcRec12, DstRec12>(
+        SrcMem12{erk, gidp}, reinterpret_cast<uint3 *>(t0), reinterpret_cast<uint3 *>(t1), m, e,
+        ehist, status, fin, st);
   else
-    nw_sort_records(erec, t0, t1, m, e, ehist, status, DstMembers{sgid, tag, mrow, key}, 20.0 * m,
-                    st, gidp);
+    nw_member_passes<uint4, SrcMem16, SrcRec, DstRec>(SrcMem16{erk, ehi, gidp}, t0, t1, m, e,
+                                                      ehist, status, fin, st);
 }
 
 uint32_t nw_chunk_width(uint32_t m, uint32_t nbx) {
@@ -1009,13 +1029,16 @@ void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint3
   uint32_t lgW = 0;
   while ((1u << lgW) < W) ++lgW;
   const uint32_t nch = nw_chunks(nbx, W);
-  XChunkArgs a{R, m, W, lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx, xpos, erec, ctrl};
+  // the member records take the erec buffer (16 B per row) as two arrays
+  uint2 *erk = reinterpret_cast<uint2 *>(erec);
+  XChunkArgs a{R,   m,    W,   lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx, xpos,
+               erk, reinterpret_cast<uint32_t *>(erk + m), ctrl};
   kt_begin(st);
   k_nw_xchunk<<<(nch + XC_WAVES - 1) / XC_WAVES, 64 * XC_WAVES,
                 XC_WAVES * 2 * W * sizeof(uint32_t), st>>>(a);
   // records in (+ halo), X entries (key, id, packed record, code, state), their
   // positions by fragment and member records out
-  kt_end(st, KID_NW_XCHUNK, 16.0 * m + 22.0 * m + 16.0 * m);
+  kt_end(st, KID_NW_XCHUNK, 16.0 * m + 22.0 * m + 12.0 * m);  // records in; X CSR + position out; member records ({row, key lo} + key hi)
 }
 
 void nw_x_bits(const uint32_t *xpos, const uint8_t *xstate, uint32_t m, uint32_t *bits,

@@ -13,7 +13,7 @@ JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
     ("k_onesweep", "one LSD pass over 16-B records, 6144 per tile: ballot ranks, LDS placement in rounds of 4096 slots, decoupled look-back, digit-segment write-out (4 processing-order passes, 4 Y, 3 member)", "32 (pass 1: 41; last order pass: 57)"),
     ("k_nw_xcount", "entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
-    ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "54"),
+    ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "50"),
     ("k_sweep_fast", "occupancy decisions, first sweep: a wavefront per 64-position window, ballot rounds, 32-bit candidate tests", "26"),
     ("k_sweep_fast_more", "later sweeps: one wavefront per 64 windows handles the still-pending ones", "-"),
     ("k_sweep_long32", "runs of more than 64 entries, 64 entries at a time against LDS lists", "-"),
