@@ -109,17 +109,6 @@ struct SrcRec {
   }
   __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
 };
-// ... with the key word from a separate array (the member records' gid)
-struct SrcRecKey {
-  using rec_t = uint4;
-  const uint4 *in;
-  const uint32_t *key0;
-  __device__ __forceinline__ uint4 load(uint32_t i) const {
-    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(in + i));
-    return make_uint4(__builtin_nontemporal_load(key0 + i), v.y, v.z, v.w);
-  }
-  __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
-};
 // 12-B records (the Y axis' records, and the member records when every sort
 // key fits 32 bits), key = .x
 struct SrcRec12 {
@@ -882,41 +871,6 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
 }
 
 // a sort of m 16-B records by .x, the last pass writing through `final`
-template <class Final>
-static void nw_sort_records(const uint4 *in, uint4 *t0, uint4 *t1, uint32_t m, const NwDigits &dg,
-                            const uint32_t *ghist, uint32_t *status, const Final &fin,
-                            double final_bytes, hipStream_t st, const uint32_t *key0 = nullptr) {
-  const Digits D = to_digits(dg);
-  const size_t sw = nw_status_words(m);
-  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
-  const PassStatus ps = pass_status(status, m, D);
-  const uint4 *src = in;
-  for (int p = 0; p < D.passes; ++p) {
-    ps.prepare(p, m, D, st);
-    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
-    uint32_t *ctr = status + sw - 64 + p;
-    const uint32_t *gh = ghist + p * 1024;
-    // key0: the first pass takes every record's key from its own array
-    const double kb = p == 0 && key0 ? 4.0 * m : 0.0;
-    if (p == D.passes - 1) {
-      if (p == 0 && key0)
-        launch_pass(SrcRecKey{src, key0}, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st,
-                    16.0 * m + kb + final_bytes, nxt);
-      else
-        launch_pass(SrcRec{src}, fin, m, D.shift[p], D.db[p], gh, stp, ctr, st,
-                    16.0 * m + final_bytes, nxt);
-    } else {
-      uint4 *out = p % 2 == 0 ? t0 : t1;
-      if (p == 0 && key0)
-        launch_pass(SrcRecKey{src, key0}, DstRec{out}, m, D.shift[p], D.db[p], gh, stp, ctr,
-                    st, 32.0 * m + kb, nxt);
-      else
-        launch_pass(SrcRec{src}, DstRec{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
-                    32.0 * m, nxt);
-      src = out;
-    }
-  }
-}
 
 // The Y axis sort in two parts: every pass but the last (on the second stream,
 // beside the X axis), then the last one, which writes the CSR arrays and --
