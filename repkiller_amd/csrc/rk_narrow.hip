@@ -27,12 +27,13 @@
 //     the same kernel computes each row's in-group sort key
 //     |yStart - diag_func[xStart/10]| (diag_func[b] = yStart of the LAST row
 //     of bucket b, commonFunctions.cpp:161-177) from the bucket runs it holds;
-//   * the Y axis records {bucket key, processing index, centre lo, length} are
-//     written by the last processing-order pass and sorted on the second
+//   * the Y axis records (12 B: {bucket key, processing index, length |
+//     centre%100 << 24}) are written by the last processing-order pass and sorted on the second
 //     stream while X resolves; the X results reach the Y axis through one
 //     byte per fragment (xhit);
 //   * group members {gid, row, sort key} are sorted by gid with the records
-//     carried, straight into the arrays the in-group sort reads.
+//     carried (12 B when every sort key fits 32 bits, else 16 B), straight
+//     into the arrays the in-group sort reads.
 #include <cstdio>
 #include <cstdlib>
 #include <utility>

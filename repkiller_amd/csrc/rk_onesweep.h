@@ -1,6 +1,6 @@
 // rk_onesweep.h -- one-sweep LSD radix pass shared by the record pipeline
-// (rk_narrow.hip: 16-B records) and the key/value pair sort (rk_radix.hip:
-// 8-B pairs).  Included inside namespace rk { namespace { ... } }.
+// (rk_narrow.hip: 12- and 16-B records) and the key/value pair sort
+// (rk_radix.hip: 8-B pairs).  Included inside namespace rk { namespace { ... } }.
 //
 // Src: rec_t (the record type), load(i) -> record i, key(rec) -> the sort key
 // word.  Dst: store(pos, rec); kWave / wave(rec, live) (see rk_narrow.hip).
@@ -29,7 +29,9 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 // tiles per load (status[digit][tile]) 36-47 us.
 // RK_LB_BATCH (compile time): predecessors read per round trip.  With
 // 6144-record tiles, cfg3 step 8 / 12 / 16 / 24 / 32 / 48: 12.00-12.03 /
-// 12.04-12.10 / 12.00-12.08 / 12.05-12.21 / 12.29-12.32 / 12.51-12.54 ms
+// 12.04-12.10 / 12.00-12.08 / 12.05-12.21 / 12.29-12.32 / 12.51-12.54 ms;
+// after the 12-B Y/member passes, 8 / 16 / 24: 11.31-11.36 / 11.32-11.45 /
+// 11.51-11.54 ms (same box).
 #ifndef RK_LB_BATCH
 #define RK_LB_BATCH 16
 #endif
