@@ -424,7 +424,15 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   rk::ScanScratch ss{w.scan, w.scan_cap};
   ctx->stats.n_in = n;
   const rk::NwDigits ad = rk::nw_plan(rk::bit_length(pl.vsize - 1));
-  const rk::NwDigits yd = rk::nw_plan(rk::bit_length(2ull * pl.nby - 1));
+  // the Y sort's widest digit: 9 bits (12-B records, 7168 per tile: 14 per
+  // digit segment) takes the 26-bit cfg3 key in 3 passes instead of 4
+  // (RK_NW_YBITS=8 for measurements)
+  static const int ybits = [] {
+    const char *e = getenv("RK_NW_YBITS");
+    const int b = e ? atoi(e) : 9;
+    return b < 8 ? 8 : b > 9 ? 9 : b;
+  }();
+  const rk::NwDigits yd = rk::nw_plan(rk::bit_length(2ull * pl.nby - 1), ybits);
 
   HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
   HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));

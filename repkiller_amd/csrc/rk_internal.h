@@ -233,7 +233,7 @@ struct NwDigits {
   int passes;
   int shift[4], db[4];
 };
-NwDigits nw_plan(int bits);
+NwDigits nw_plan(int bits, int max_bits = 0);  // max_bits 0: nw_max_bits()
 void nw_trace_dump(hipStream_t st);  // RK_NW_TRACE (measurement only)
 size_t nw_status_words(uint32_t n);
 uint32_t nw_chunk_width(uint32_t m, uint32_t nbx);

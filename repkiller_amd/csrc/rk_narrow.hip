@@ -597,10 +597,10 @@ int nw_max_bits() {
   return v;
 }
 
-Digits plan_digits(int bits) {
+Digits plan_digits(int bits, int max_bits = 0) {
   Digits D{};
   if (bits < 1) bits = 1;
-  const int mb = nw_max_bits();
+  const int mb = max_bits ? max_bits : nw_max_bits();
   D.passes = (bits + mb - 1) / mb;
   int shift = 0;
   for (int p = 0; p < D.passes; ++p) {
@@ -622,8 +622,10 @@ constexpr int OS_T = 256;
 #define RK_NW_ITEMS12 14
 #endif
 int nw_shape();
-// records per tile of a pass with DB-bit digits (the shape of launch_pass_db)
-uint32_t tile_records(int db) {
+// records per tile of a pass with DB-bit digits over rec_bytes-B records (the
+// shape of launch_pass_db)
+uint32_t tile_records(int db, int rec_bytes = 16) {
+  if (rec_bytes == 12 && db <= 9) return 512 * RK_NW_ITEMS12;
   if (db != 8) return OS_T * (db >= 10 ? 12 : 16);
   switch (nw_shape()) {
     case 2: return 256 * 8;
@@ -634,8 +636,8 @@ uint32_t tile_records(int db) {
     default: return 4096;  // 0, 1: 256 x 16; 4: 512 x 8
   }
 }
-uint32_t tiles_for(uint32_t n, int db) {
-  const uint32_t tile = tile_records(db);
+uint32_t tiles_for(uint32_t n, int db, int rec_bytes = 16) {
+  const uint32_t tile = tile_records(db, rec_bytes);
   return (n + tile - 1) / tile;
 }
 
@@ -716,7 +718,11 @@ template <int DB, class Src, class Dst>
 void launch_pass_db(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
                     uint32_t *status, uint32_t *ctr, hipStream_t st, uint32_t *clear_next) {
   constexpr int ITEMS = DB >= 10 ? 12 : 16;
-  if constexpr (DB == 8 && sizeof(typename Src::rec_t) == 12) {
+  if constexpr (DB == 9 && sizeof(typename Src::rec_t) == 12) {
+    launch_shape<512, RK_NW_ITEMS12, 9, false>(src, dst, n, shift, ghist, status, ctr, st,
+                                               clear_next);
+    return;
+  } else if constexpr (DB == 8 && sizeof(typename Src::rec_t) == 12) {
     // 12-B records: RK_NW_ITEMS12 per thread (LDS rounds of 5461 slots)
     launch_shape<512, RK_NW_ITEMS12, 8, false>(src, dst, n, shift, ghist, status, ctr, st,
                                                clear_next);
@@ -743,7 +749,7 @@ void launch_pass(const Src &src, const Dst &dst, uint32_t n, int shift, int db,
   kt_begin(st);
   switch (db) {
     case 8: launch_pass_db<8>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
-    case 9: launch_pass_db<9>(src, dst, n, shift, ghist, status, ctr, st, nullptr); break;
+    case 9: launch_pass_db<9>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
     default: launch_pass_db<10>(src, dst, n, shift, ghist, status, ctr, st, nullptr); break;
   }
   kt_end(st, KID_ONESWEEP, bytes);
@@ -780,8 +786,8 @@ size_t nw_status_words(uint32_t n) {
   return (size_t)((n + 3071) / 3072 + 1) * 1024 + 64;
 }
 
-NwDigits nw_plan(int bits) {
-  const Digits D = plan_digits(bits);
+NwDigits nw_plan(int bits, int max_bits) {
+  const Digits D = plan_digits(bits, max_bits);
   NwDigits o{};
   o.passes = D.passes;
   for (int p = 0; p < 4; ++p) o.shift[p] = D.shift[p], o.db[p] = D.db[p];
@@ -797,15 +803,17 @@ static Digits to_digits(const NwDigits &o) {
   return D;
 }
 
-// Status words of one sort.  With 8-bit digits in every pass the buffer is
-// used as two halves: pass p publishes into half p & 1 and zeroes, tile by
-// tile, the other half for pass p + 1 (k_onesweep's clear_next), so a sort
-// needs one memset instead of one per pass; otherwise one buffer, cleared
-// before each pass.
+// Status words of one sort.  When every pass has the same tiles and no pass
+// has more digits than the one before (8-bit digits, or 9-bit ones over 12-B
+// records), the buffer is used as two halves: pass p publishes into half p & 1
+// and zeroes, tile by tile, its own rows of the other half for pass p + 1
+// (k_onesweep's clear_next), so a sort needs one memset instead of one per
+// pass; otherwise one buffer, cleared before each pass.
 struct PassStatus {
   uint32_t *base;
   size_t half;
   bool ahead;
+  int rec_bytes;
   uint32_t *use(int p) const { return ahead ? base + (size_t)(p & 1) * half : base; }
   uint32_t *next(int p, int passes) const {
     return ahead && p + 1 < passes ? base + (size_t)((p + 1) & 1) * half : nullptr;
@@ -813,15 +821,18 @@ struct PassStatus {
   // before pass p: the memset it still needs (none after a clear-ahead pass)
   void prepare(int p, uint32_t n, const Digits &D, hipStream_t st) const {
     if (ahead && p > 0) return;
-    const size_t words = ahead ? half : (size_t)tiles_for(n, D.db[p]) * ((size_t)1 << D.db[p]);
+    const size_t words =
+        ahead ? half : (size_t)tiles_for(n, D.db[p], rec_bytes) * ((size_t)1 << D.db[p]);
     (void)hipMemsetAsync(use(p), 0, words * 4, st);
   }
 };
-static PassStatus pass_status(uint32_t *status, uint32_t n, const Digits &D) {
-  bool all8 = true;
-  for (int p = 0; p < D.passes; ++p) all8 &= D.db[p] == 8;
-  const size_t half = (size_t)tiles_for(n, 8) * 256;
-  return PassStatus{status, half, all8 && 2 * half + 64 <= nw_status_words(n)};
+static PassStatus pass_status(uint32_t *status, uint32_t n, const Digits &D, int rec_bytes = 16) {
+  const uint32_t tiles = tiles_for(n, D.db[0], rec_bytes);
+  bool same = true;
+  for (int p = 1; p < D.passes; ++p)
+    same &= D.db[p] <= D.db[p - 1] && tiles_for(n, D.db[p], rec_bytes) == tiles;
+  const size_t half = (size_t)tiles << D.db[0];
+  return PassStatus{status, half, same && 2 * half + 64 <= nw_status_words(n), rec_bytes};
 }
 
 void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
@@ -883,7 +894,7 @@ void nw_y_sort_head(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y
   const Digits D = to_digits(y);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
-  const PassStatus ps = pass_status(status, m, D);  // the tail pass' half is cleared here
+  const PassStatus ps = pass_status(status, m, D, 12);  // the tail pass' half is cleared here
   // 12-B records (DstProc); the buffers are uint4 arrays, large enough
   const uint3 *src = reinterpret_cast<const uint3 *>(yrec);
   for (int p = 0; p + 1 < D.passes; ++p) {
@@ -901,7 +912,7 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
   const size_t sw = nw_status_words(m);
   const int p = D.passes - 1;
   const uint3 *src = reinterpret_cast<const uint3 *>(p == 0 ? yrec : (p - 1) % 2 == 0 ? tmp : yrec);
-  const PassStatus ps = pass_status(status, m, D);
+  const PassStatus ps = pass_status(status, m, D, 12);
   ps.prepare(p, m, D, st);  // a no-op after the head's clear-ahead
   if (p == 0) (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);
   launch_pass(SrcRec12{src},
@@ -920,7 +931,7 @@ static void nw_member_passes(const Src1 &s1, Rec *t0, Rec *t1, uint32_t m, const
   const Digits D = to_digits(dg);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
-  const PassStatus ps = pass_status(status, m, D);
+  const PassStatus ps = pass_status(status, m, D, (int)sizeof(Rec));
   const double rb = sizeof(Rec), in1 = sizeof(Rec) == 12 ? 12.0 : 16.0;
   const Rec *src = nullptr;
   for (int p = 0; p < D.passes; ++p) {

@@ -104,7 +104,10 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
   // sorted records staged in LDS, LSLOTS slots at a time (tiles above 64 KB of
   // records are placed and written out in rounds)
   using R = typename Src::rec_t;  // uint4 (16-B records) or uint2 (key, value pairs)
-  constexpr int LSLOTS = TILE < (int)(65536 / sizeof(R)) ? TILE : (int)(65536 / sizeof(R));
+  // (48 KB with 9-bit and wider digits, whose counters take the rest: two
+  // blocks per CU)
+  constexpr int LBYTES = DB >= 9 ? 49152 : 65536;
+  constexpr int LSLOTS = TILE < (int)(LBYTES / sizeof(R)) ? TILE : (int)(LBYTES / sizeof(R));
   static_assert(!PERSIST || LSLOTS == TILE, "persistent tiles reload rec[] before the write-out");
   __shared__ R srec[LSLOTS];
   __shared__ uint32_t wcnt[NW][RADIX];  // per-wave digit counters, then per-wave starts

@@ -11,7 +11,7 @@ BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
 BENCH, CFG5 = "r2_bench.json", "r2_bench_cfg5.json"
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
-    ("k_onesweep", "one LSD pass over 16-B records, 6144 per tile: ballot ranks, LDS placement in rounds of 4096 slots, decoupled look-back, digit-segment write-out (4 processing-order passes, 4 Y, 3 member)", "32 (pass 1: 41; last order pass: 57)"),
+    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (4 processing-order passes), 12-B records 7168 per tile (3 Y passes with 9-bit digits, 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last order pass: 57)"),
     ("k_nw_xcount", "entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
     ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "50"),
     ("k_sweep_fast", "occupancy decisions, first sweep: a wavefront per 64-position window, ballot rounds, 32-bit candidate tests", "26"),
