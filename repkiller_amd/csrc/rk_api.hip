@@ -424,15 +424,15 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   rk::ScanScratch ss{w.scan, w.scan_cap};
   ctx->stats.n_in = n;
   const rk::NwDigits ad = rk::nw_plan(rk::bit_length(pl.vsize - 1));
-  // the Y sort's widest digit: 9 bits (12-B records, 7168 per tile: 14 per
-  // digit segment) takes the 26-bit cfg3 key in 3 passes instead of 4
-  // (RK_NW_YBITS=8 for measurements)
-  static const int ybits = [] {
+  // the widest digit of the 12-B record sorts (Y axis, narrow members): 9
+  // bits (7168 records per tile: 14 per digit segment) takes cfg3's 26-bit Y
+  // key in 3 passes instead of 4 (RK_NW_YBITS=8 for measurements)
+  static const int bits12 = [] {
     const char *e = getenv("RK_NW_YBITS");
     const int b = e ? atoi(e) : 9;
     return b < 8 ? 8 : b > 9 ? 9 : b;
   }();
-  const rk::NwDigits yd = rk::nw_plan(rk::bit_length(2ull * pl.nby - 1), ybits);
+  const rk::NwDigits yd = rk::nw_plan(rk::bit_length(2ull * pl.nby - 1), bits12);
 
   HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
   HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));
@@ -534,7 +534,9 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     const uint32_t G = ctx->host[0];
     out->n_groups = G;
     ctx->stats.n_groups = G;
-    const rk::NwDigits ed = rk::nw_plan(rk::bit_length(G ? G - 1 : 0));
+    // 12-B member records take 9-bit digits too (a 25..27-bit gid in 3
+    // passes); 16-B ones keep 8-bit digits
+    const rk::NwDigits ed = rk::nw_plan(rk::bit_length(G ? G - 1 : 0), narrow_keys ? bits12 : 8);
     HIPCHK(ctx, hipMemsetAsync(w.ehist, 0, 4096 * sizeof(uint32_t), st));
     // gids into isnew's words (dead after the scan)
     rk::nw_assign(w.par, w.newrank, w.isnew, m, ed, w.ehist, st);
