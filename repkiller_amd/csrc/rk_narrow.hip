@@ -597,16 +597,30 @@ int nw_max_bits() {
   return v;
 }
 
+// narrowest radix of a pass (RK_NW_MINBITS=7..8): a pass whose balanced
+// digit width is 7 bits sorts over 128 digits instead of 256 (cfg3's 29-bit
+// processing key: 8 + 7 + 7 + 7) -- one ballot less per record and half the
+// counters and look-back walks per tile
+int nw_min_bits() {
+  static const int v = [] {
+    const char *e = getenv("RK_NW_MINBITS");
+    const int b = e ? atoi(e) : 7;
+    return b < 7 ? 7 : b > 8 ? 8 : b;
+  }();
+  return v;
+}
+
 Digits plan_digits(int bits, int max_bits = 0) {
   Digits D{};
   if (bits < 1) bits = 1;
   const int mb = max_bits ? max_bits : nw_max_bits();
+  const int lo = nw_min_bits();
   D.passes = (bits + mb - 1) / mb;
   int shift = 0;
   for (int p = 0; p < D.passes; ++p) {
     const int left = bits - shift, w0 = (left + (D.passes - p) - 1) / (D.passes - p);
     D.shift[p] = shift;
-    D.db[p] = w0 < 8 ? 8 : w0;
+    D.db[p] = w0 < lo ? lo : w0;
     shift += w0;
   }
   return D;
@@ -626,6 +640,7 @@ int nw_shape();
 // shape of launch_pass_db)
 uint32_t tile_records(int db, int rec_bytes = 16) {
   if (rec_bytes == 12 && db <= 9) return 512 * RK_NW_ITEMS12;
+  if (db == 7) return 512 * 12;
   if (db != 8) return OS_T * (db >= 10 ? 12 : 16);
   switch (nw_shape()) {
     case 2: return 256 * 8;
@@ -718,7 +733,14 @@ template <int DB, class Src, class Dst>
 void launch_pass_db(const Src &src, const Dst &dst, uint32_t n, int shift, const uint32_t *ghist,
                     uint32_t *status, uint32_t *ctr, hipStream_t st, uint32_t *clear_next) {
   constexpr int ITEMS = DB >= 10 ? 12 : 16;
-  if constexpr (DB == 9 && sizeof(typename Src::rec_t) == 12) {
+  if constexpr (DB == 7 && sizeof(typename Src::rec_t) == 12) {
+    launch_shape<512, RK_NW_ITEMS12, 7, false>(src, dst, n, shift, ghist, status, ctr, st,
+                                               clear_next);
+    return;
+  } else if constexpr (DB == 7) {
+    launch_shape<512, 12, 7, false>(src, dst, n, shift, ghist, status, ctr, st, clear_next);
+    return;
+  } else if constexpr (DB == 9 && sizeof(typename Src::rec_t) == 12) {
     launch_shape<512, RK_NW_ITEMS12, 9, false>(src, dst, n, shift, ghist, status, ctr, st,
                                                clear_next);
     return;
@@ -748,6 +770,7 @@ void launch_pass(const Src &src, const Dst &dst, uint32_t n, int shift, int db,
   if (!n) return;
   kt_begin(st);
   switch (db) {
+    case 7: launch_pass_db<7>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
     case 8: launch_pass_db<8>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
     case 9: launch_pass_db<9>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
     default: launch_pass_db<10>(src, dst, n, shift, ghist, status, ctr, st, nullptr); break;
