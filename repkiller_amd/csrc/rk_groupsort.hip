@@ -967,18 +967,6 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     (void)hipEventRecord(ev_fork, st);  // the tier lists are ready
     (void)hipStreamWaitEvent(s2, ev_fork, 0);
   }
-  kt_begin(s2);
-  k_sort_small<<<2048, 256, 0, s2>>>(tl, goff, key, tag, otag);
-  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
-  tier_slot(0);
-  kt_begin(s2);
-  k_sort_groups_reg<2><<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
-  kt_end(s2, KID_SORT_REG, 0.0);
-  tier_slot(1);
-  kt_begin(s2);
-  k_sort_groups_reg<1><<<4096, 256, 0, s2>>>(tl, 2, goff, key, tag, otag);
-  kt_end(s2, KID_SORT_REG, 0.0);
-  tier_slot(2);
   // segments of 17..reg_max members inside the LDS tiers would be finished in
   // registers (reg_batch); by default (0) the LDS partitions go down to the
   // leaves, which the vectorised final pass ranks -- LDS tiers 1.29 -> 1.25
@@ -992,24 +980,48 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     const char *e = getenv("RK_GS_SIDE");
     return e ? atoi(e) : 0;
   }();
+  // the last `lds_big` LDS tiers (the largest groups: few, long wavefronts
+  // that leave the device idle at the end of their own launch) run first on
+  // `side`, under the smaller LDS tiers on `st` (RK_GS_BIG).  cfg3 group-sort
+  // phase with 0 / 1 / 2 / 3 / 4 of them: 1.38-1.39 / 1.26 / 1.23-1.24 /
+  // 1.40-1.41 / 1.57 ms
+  static const int lds_big = [] {
+    const char *e = getenv("RK_GS_BIG");
+    const int b = e ? atoi(e) : 2;
+    return b < 0 ? 0 : b > NLDS ? NLDS : b;
+  }();
+  auto launch_lds = [&](int j, hipStream_t sj) {
+    const uint32_t cap = caps.c[j];
+    const uint32_t grid = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
+    kt_begin(sj);
+    if (narrow_keys)
+      k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), sj>>>(tl, TIER_LDS0 + j, goff, key,
+                                                                       tag, otag, cap, reg_max);
+    else
+      k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), sj>>>(tl, TIER_LDS0 + j, goff, key,
+                                                                       tag, otag, cap, reg_max);
+    kt_end(sj, KID_SORT_LDS, 0.0);
+    tier_slot(TIER_LDS0 + j);
+  };
+  const int big0 = side ? NLDS - lds_big : NLDS;  // tiers [big0, NLDS) go first on side
+  for (int j = NLDS - 1; j >= big0; --j) launch_lds(j, s2);
+  kt_begin(s2);
+  k_sort_small<<<2048, 256, 0, s2>>>(tl, goff, key, tag, otag);
+  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
+  tier_slot(0);
+  kt_begin(s2);
+  k_sort_groups_reg<2><<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
+  kt_end(s2, KID_SORT_REG, 0.0);
+  tier_slot(1);
+  kt_begin(s2);
+  k_sort_groups_reg<1><<<4096, 256, 0, s2>>>(tl, 2, goff, key, tag, otag);
+  kt_end(s2, KID_SORT_REG, 0.0);
+  tier_slot(2);
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1 && side) (void)hipEventRecord(ev_join, s2);
-    for (int j = 0; j < NLDS; ++j) {
+    for (int j = 0; j < big0; ++j) {
       if ((j < lds_side) != (pass == 0)) continue;
-      hipStream_t sj = pass == 0 ? s2 : st;
-      const uint32_t cap = caps.c[j];
-      const uint32_t grid = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
-      kt_begin(sj);
-      if (narrow_keys)
-        k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), sj>>>(tl, TIER_LDS0 + j, goff,
-                                                                         key, tag, otag, cap,
-                                                                         reg_max);
-      else
-        k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), sj>>>(tl, TIER_LDS0 + j, goff,
-                                                                         key, tag, otag, cap,
-                                                                         reg_max);
-      kt_end(sj, KID_SORT_LDS, 0.0);
-      tier_slot(TIER_LDS0 + j);
+      launch_lds(j, pass == 0 ? s2 : st);
     }
   }
 #ifdef RK_GS_PROF
