@@ -1013,10 +1013,21 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   k_sort_groups_reg<2><<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
   kt_end(s2, KID_SORT_REG, 0.0);
   tier_slot(1);
-  kt_begin(s2);
-  k_sort_groups_reg<1><<<4096, 256, 0, s2>>>(tl, 2, goff, key, tag, otag);
-  kt_end(s2, KID_SORT_REG, 0.0);
-  tier_slot(2);
+  // the 33..64-member tier on `st` after its LDS tiers (RK_GS_REG1=1, the
+  // default) or on `side` (0): the two streams' kernel time is then ~1.06 /
+  // ~1.0 ms instead of 0.94 / 1.12 (cfg3 kernel trace); group-sort phase
+  // 1.23-1.24 -> 1.21 ms
+  static const int reg1_main = [] {
+    const char *e = getenv("RK_GS_REG1");
+    return e ? atoi(e) : 1;
+  }();
+  auto launch_reg1 = [&](hipStream_t sj) {
+    kt_begin(sj);
+    k_sort_groups_reg<1><<<4096, 256, 0, sj>>>(tl, 2, goff, key, tag, otag);
+    kt_end(sj, KID_SORT_REG, 0.0);
+    tier_slot(2);
+  };
+  if (!reg1_main || !side) launch_reg1(s2);
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1 && side) (void)hipEventRecord(ev_join, s2);
     for (int j = 0; j < big0; ++j) {
@@ -1024,6 +1035,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
       launch_lds(j, pass == 0 ? s2 : st);
     }
   }
+  if (reg1_main && side) launch_reg1(st);
 #ifdef RK_GS_PROF
   {
     unsigned long long h[8];
