@@ -515,11 +515,19 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     pr.par = w.par;
     bool narrow_keys = true;
     HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
-    uint32_t rounds = 0;
+    uint32_t rounds = 0, G = 0;
     for (;;) {
       HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
       rk::jump_round(pr, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st);
-      if ((rc = readback(ctx, w.ctrl + 5, 2))) return rc;  // + the wide-key flag
+      if (rounds == 0) {
+        // the new-group flags are final after the first round: their scan
+        // (the group count G, in ctrl[32]) shares the round's readback
+        rk::exclusive_scan_u32(w.isnew, w.newrank, (size_t)m + 1, ss, st);
+        HIPCHK(ctx, hipMemcpyAsync(w.ctrl + 32, w.newrank + m, sizeof(uint32_t),
+                                   hipMemcpyDeviceToDevice, st));
+      }
+      if ((rc = readback(ctx, w.ctrl + 5, 28))) return rc;  // + the wide-key flag, G
+      if (rounds == 0) G = ctx->host[27];
       ++rounds;
       narrow_keys = ctx->host[1] == 0;
       if (!ctx->host[0]) break;
@@ -529,9 +537,6 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
       }
     }
     ctx->stats.jump_rounds = rounds;
-    rk::exclusive_scan_u32(w.isnew, w.newrank, (size_t)m + 1, ss, st);
-    if ((rc = readback(ctx, w.newrank + m, 1))) return rc;
-    const uint32_t G = ctx->host[0];
     out->n_groups = G;
     ctx->stats.n_groups = G;
     // 12-B member records take 9-bit digits too (a 25..27-bit gid in 3

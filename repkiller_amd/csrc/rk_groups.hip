@@ -165,10 +165,34 @@ __global__ void k_csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylen
   }
 }
 
-__global__ void k_group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups,
-                                uint32_t *goff) {
+__global__ void k_group_offsets_unaligned(const uint32_t *sgid, uint32_t m, uint32_t ngroups,
+                                          uint32_t *goff) {
   GRID_STRIDE(q, m) {
     if (q == 0 || sgid[q] != sgid[q - 1]) goff[sgid[q]] = q;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) goff[ngroups] = m;
+}
+// the same with four positions per thread (one 16-B load; sgid 16-B aligned):
+// a group starts where the gid differs from the previous position's
+__global__ void __launch_bounds__(256) k_group_offsets(const uint32_t *sgid, uint32_t m,
+                                                        uint32_t ngroups, uint32_t *goff) {
+  const uint32_t nq = (m + 3) / 4;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
+    const uint32_t q0 = t * 4;
+    uint32_t g[4];
+    if (q0 + 4 <= m) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(sgid + q0);
+      g[0] = v.x, g[1] = v.y, g[2] = v.z, g[3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = q0 + j < m ? sgid[q0 + j] : 0u;
+    }
+    uint32_t prev = q0 ? sgid[q0 - 1] : ~0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (q0 + j < m && g[j] != prev) goff[g[j]] = q0 + j;
+      prev = g[j];
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) goff[ngroups] = m;
 }
@@ -276,7 +300,10 @@ void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t 
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st) {
   kt_begin(st);
-  k_group_offsets<<<grid_for(m, 256), 256, 0, st>>>(sgid, m, ngroups, goff);
+  if ((reinterpret_cast<uintptr_t>(sgid) & 15) == 0)
+    k_group_offsets<<<grid_for((m + 3) / 4, 256, 16384), 256, 0, st>>>(sgid, m, ngroups, goff);
+  else
+    k_group_offsets_unaligned<<<grid_for(m, 256), 256, 0, st>>>(sgid, m, ngroups, goff);
   kt_end(st, KID_GROUP_OFFSETS, 4.0 * m + 4.0 * ngroups);
 }
 void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,

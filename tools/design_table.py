@@ -11,7 +11,7 @@ BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
 BENCH, CFG5 = "r2_bench.json", "r2_bench_cfg5.json"
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
-    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (4 processing-order passes), 12-B records 7168 per tile (3 Y passes with 9-bit digits, 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last order pass: 57)"),
+    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (4 processing-order passes, 8 + 7 + 7 + 7-bit digits at cfg3), 12-B records 7168 per tile (3 Y passes with 9-bit digits, 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last order pass: 57)"),
     ("k_nw_xcount", "entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
     ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "50"),
     ("k_sweep_fast", "occupancy decisions, first sweep: a wavefront per 64-position window, ballot rounds, 32-bit candidate tests", "26"),
@@ -23,8 +23,8 @@ JOBS = [
     ("k_nw_assign", "gid from the root's rank into each member record; member-sort histograms", "12"),
     ("k_group_offsets", "group bounds", "4"),
     ("k_sort_small", "groups of 2..16 members (insertion sort == stable rank): 16 lanes per group from the tier list, width-16 shuffles; singletons are not touched (second stream)", "16 per member"),
-    ("k_sort_groups_reg", "17..64 members in registers (17..32: two groups per wavefront; second stream)", "16 per member"),
-    ("k_sort_groups_lds", "65..2048 members in LDS: partitions down to the leaves, then the final insertion pass with ballot-found leaf bounds", "16 per member"),
+    ("k_sort_groups_reg", "17..64 members in registers (17..32: two groups per wavefront, second stream; 33..64: main stream, after its LDS tiers)", "16 per member"),
+    ("k_sort_groups_lds", "65..2048 members in LDS: partitions down to the leaves, then the final insertion pass with ballot-found leaf bounds (257..2048: second stream, first)", "16 per member"),
     ("k_sort_groups_split", "groups above 2048: block-wide partitions down to 512-member segments", "16 per member"),
     ("k_sort_segments", "those segments, one LDS wavefront each", "16 per member"),
     ("k_emit", "gid, flag, output order", "29"),
