@@ -1494,8 +1494,10 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
                      S.take<uint32_t>(SL_RADIX, rw), rw, S.st);
     group_offsets(sgid, mr, Gl, goffs, S.st);
     build_records(gmem, mem, mr, reckey, tag, S.st);
+    // the group-sort tiers on both streams, as in the single-device path
     sort_groups_exact(sgid, goffs, Gl, mr, reckey, tag, otag, gsort,
-                      S.scan_scratch(SL_SCAN, mr + Gl + 2), ctx->host + 128, narrow, S.st);
+                      S.scan_scratch(SL_SCAN, mr + Gl + 2), ctx->host + 128, narrow, S.st,
+                      S.st2 != S.st ? S.st2 : nullptr, ctx->fork, ctx->join);
     emit_result(otag, sgid, goffs, gmem, mr, ogid, orep, oord, S.st);
     if (g0) k_add_u32<<<grid_for(mr, 256), 256, 0, S.st>>>(ogid, mr, g0);
     S.launched("member order");
