@@ -67,10 +67,21 @@ __device__ __forceinline__ uint8_t nbd_code_nw(uint64_t c, uint64_t max_index) {
 
 // largest bucket index get_associated_group touches for centre c
 __device__ __forceinline__ uint64_t probe_max_bucket_nw(uint64_t c, uint64_t max_index) {
+  if (c < (1ull << 32) - 2 && max_index != 0 && max_index < (1ull << 32)) {
+    // the same in 32 bits (no wrap of c + 2 or max_index - 1 here)
+    const uint32_t c32 = (uint32_t)c, m32 = (uint32_t)max_index;
+    uint32_t b = c32 / 100u;
+    if (c32 < m32 && (c32 + 1) / 100u > b) b = (c32 + 1) / 100u;
+    if (c32 < m32 - 1 && (c32 + 2) / 100u > b) b = (c32 + 2) / 100u;
+    return b;
+  }
   uint64_t b = c / 100;
   if (c < max_index && (c + 1) / 100 > b) b = (c + 1) / 100;
   if (c < max_index - 1 && (c + 2) / 100 > b) b = (c + 2) / 100;
   return b;
+}
+__device__ __forceinline__ uint64_t div_small(uint64_t v, uint32_t d) {  // 32-bit when it fits
+  return v < (1ull << 32) ? (uint64_t)((uint32_t)v / d) : v / d;
 }
 
 // digits of one LSD sort: pass p sorts by (key >> shift[p]) & (2^db[p] - 1)
@@ -189,7 +200,7 @@ struct SrcFile {
   __device__ __forceinline__ uint4 load(uint32_t i) const {
     const uint64_t xs = x[i], ys = y[i], L = len[i];
     const uint32_t s = strand[i] != 'f' ? 1u : 0u;
-    const uint64_t pk = xs / 10;
+    const uint64_t pk = div_small(xs, 10);
     const uint32_t key = (uint32_t)(pk < vsize - 1 ? pk : vsize - 1);
     // (rows that do not pack were flagged by k_nw_order_hist: the generic
     // pipeline takes over then)
@@ -290,7 +301,7 @@ __global__ void __launch_bounds__(256) k_nw_order_hist(OrderHistArgs a) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
     const uint64_t xs = a.x[i], ys = a.y[i], L0 = a.len[i];
     const uint32_t s = a.strand[i] != 'f' ? 1u : 0u;
-    const uint64_t pk = xs / 10;
+    const uint64_t pk = div_small(xs, 10);
     ub |= pk >= a.vsize;
     wide |= L0 >= (1ull << 24) || ys >= (1ull << 35);
     const uint32_t key = (uint32_t)(pk < drop ? pk : drop);
@@ -303,7 +314,7 @@ __global__ void __launch_bounds__(256) k_nw_order_hist(OrderHistArgs a) {
     const uint64_t h = len / 2;
     ubc |= probe_max_bucket_nw(xs + h, a.max_x) > a.max_x ||
            probe_max_bucket_nw(ys + h, a.max_y) > a.max_y;
-    hist_add(LY, a.yd, s * a.nby + (uint32_t)((ys + h) / 100));
+    hist_add(LY, a.yd, s * a.nby + (uint32_t)div_small(ys + h, 100));
   }
   for (int off = 32; off > 0; off >>= 1) {
     kept += __shfl_xor(kept, off);
