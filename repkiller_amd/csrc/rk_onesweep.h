@@ -31,7 +31,9 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 // 6144-record tiles, cfg3 step 8 / 12 / 16 / 24 / 32 / 48: 12.00-12.03 /
 // 12.04-12.10 / 12.00-12.08 / 12.05-12.21 / 12.29-12.32 / 12.51-12.54 ms;
 // after the 12-B Y/member passes, 8 / 16 / 24: 11.31-11.36 / 11.32-11.45 /
-// 11.51-11.54 ms (same box).
+// 11.51-11.54 ms (same box); with the 7-bit passes, record passes per step at
+// 4 / 8 / 12 / 16 / 24: 6.09-6.22 / 6.11-6.25 / 6.15-6.29 / 6.18-6.31 /
+// 6.38-6.42 ms (RK_LIB builds, interleaved; the spread is the box's).
 #ifndef RK_LB_BATCH
 #define RK_LB_BATCH 16
 #endif
