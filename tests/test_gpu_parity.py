@@ -355,3 +355,37 @@ def test_wide_length_detected_in_any_lane(pctx, pos):
     f = rk.synth(20_000, 1_000_000, seed=64)
     f.length[pos] = np.uint64(2**31 + 3)
     gpu_vs_oracle(pctx, f, 5_000_000_000, 5_000_000_000)
+
+
+_SWITCH_SCRIPT = r"""
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import repkiller_amd as rk
+f = rk.synth(300_000, 18_000_000, seed=41)
+ctx = rk.Context(0)
+r = ctx.classify(f, 18_000_000, 18_000_000)
+h = hashlib.sha256()
+for a in (r.out_order, r.gid, r.repval):
+    h.update(np.ascontiguousarray(a).tobytes())
+print(h.hexdigest(), r.n_groups)
+"""
+
+
+@pytest.mark.parametrize("env", ["RK_GS_BIG=0", "RK_GS_BIG=4", "RK_GS_REG1=0", "RK_NW_MINBITS=8"])
+def test_schedule_switches_bit_identical(gpu_ctx, env):
+    """The measurement switches only move work between streams or change the
+    radix of a pass: the result must not change.  300k rows at cfg3 density
+    (groups up to ~2000 members: every group-sort tier is used); the switch is
+    read once per process, so the variant runs in a child process."""
+    f = rk.synth(300_000, 18_000_000, seed=41)
+    r = gpu_ctx.classify(f, 18_000_000, 18_000_000)
+    h = hashlib.sha256()
+    for a in (r.out_order, r.gid, r.repval):
+        h.update(np.ascontiguousarray(a).tobytes())
+    k, v = env.split("=")
+    out = subprocess.run(["python", "-c", _SWITCH_SCRIPT, str(ROOT)], capture_output=True,
+                         text=True, timeout=120, env={**os.environ, k: v})
+    assert out.returncode == 0, out.stderr[-2000:]
+    digest, ng = out.stdout.split()
+    assert digest == h.hexdigest() and int(ng) == r.n_groups
