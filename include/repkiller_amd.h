@@ -125,8 +125,8 @@ int rk_get_stats(const rk_ctx *ctx, rk_stats *st);
 
 /* Which device pipeline rk_classify* uses on this context.  AUTO (default):
  * the record pipeline whenever every row packs into its 16-B record (length
- * < 2^24, yStart < 2^35, fewer than 2^30 rows, X chunks within their LDS
- * capacity), else the generic one; GENERIC: always the generic pipeline.
+ * < 2^24, yStart < 2^35) and there are fewer than 2^30 rows, else the
+ * generic one; GENERIC: always the generic pipeline.
  * Both produce the same output. */
 enum { RK_PIPELINE_AUTO = 0, RK_PIPELINE_GENERIC = 1 };
 int rk_set_pipeline(rk_ctx *ctx, int pipeline);

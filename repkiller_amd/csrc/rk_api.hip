@@ -311,9 +311,10 @@ void collect_phases(rk_ctx *ctx) {
 
 // ---------------------------------------------------------------------------
 // The record pipeline (rk_narrow.hip): used when every row packs into a
-// 16-B record; returns with *fallback set when the input turns out not to
-// (a length >= 2^24, a yStart >= 2^35, or an X chunk denser than its LDS
-// capacity) -- the generic pipeline then classifies from scratch.
+// 16-B record; returns with *fallback set when the input turns out not to (a
+// length >= 2^24 or a yStart >= 2^35, found by the upfront pass before the
+// workspace is sized; n >= 2^30 never gets here) -- the generic pipeline then
+// classifies from scratch.
 struct NWork {
   uint32_t *ctrl, *ahist, *yhist, *ehist;
   uint32_t *astatus, *ystatus, *xcnt, *xoff;
@@ -332,10 +333,6 @@ struct NWork {
 size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
   const size_t n = n1 + 1;
   const size_t sw = rk::nw_status_words((uint32_t)n);
-  w.ctrl = c.take<uint32_t>(64 + rk::PEND_WORDS);
-  w.ahist = c.take<uint32_t>(3 * 4096);
-  w.yhist = w.ahist + 4096;
-  w.ehist = w.ahist + 8192;
   w.astatus = c.take<uint32_t>(sw);
   w.ystatus = c.take<uint32_t>(sw);
   // X-chunk counts and their scan (chunks of >= 64 buckets)
@@ -373,6 +370,27 @@ size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
   w.scan_cap = rk::scan_blocks(n + 1) + 64;
   w.scan = c.take<uint32_t>(w.scan_cap);
   return c.off;
+}
+
+// control words and digit histograms (ctrl, ahist / yhist / ehist), size
+// independent of n: the upfront pass that decides whether every row packs
+// writes only these, so an input that falls back never sizes the workspace
+constexpr size_t NW_SMALL_WORDS = 64 + rk::PEND_WORDS + 3 * 4096;
+
+int ensure_nw_small(rk_ctx *ctx, NWork &w) {
+  if (!ctx->nw_small) {
+    const hipError_t e = hipMalloc(&ctx->nw_small, NW_SMALL_WORDS * sizeof(uint32_t));
+    if (e != hipSuccess) {
+      ctx->nw_small = nullptr;
+      ctx->err = std::string("record-pipeline control hipMalloc: ") + hipGetErrorString(e);
+      return e == hipErrorOutOfMemory ? RK_E_NOMEM : RK_E_HIP;
+    }
+  }
+  w.ctrl = static_cast<uint32_t *>(ctx->nw_small);
+  w.ahist = w.ctrl + 64 + rk::PEND_WORDS;
+  w.yhist = w.ahist + 4096;
+  w.ehist = w.ahist + 8192;
+  return RK_OK;
 }
 
 int ensure_nw(rk_ctx *ctx, uint64_t n, uint32_t nbx, NWork &w) {
@@ -418,10 +436,9 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   *fallback = false;
   const uint32_t n = (uint32_t)pl.n;
   NWork w{};
-  int rc = ensure_nw(ctx, pl.n, pl.nbx, w);
+  int rc = ensure_nw_small(ctx, w);
   if (rc) return rc;
   hipStream_t st = ctx->stream, st2 = ctx->stream2;
-  rk::ScanScratch ss{w.scan, w.scan_cap};
   ctx->stats.n_in = n;
   const rk::NwDigits ad = rk::nw_plan(rk::bit_length(pl.vsize - 1));
   // the widest digit of the 12-B record sorts (Y axis, narrow members): 9
@@ -448,6 +465,9 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     ctx->stats.record_fallback = 1;
     return RK_OK;
   }
+  // every row packs: now the workspace (~190 B per row)
+  if ((rc = ensure_nw(ctx, pl.n, pl.nbx, w))) return rc;
+  rk::ScanScratch ss{w.scan, w.scan_cap};
   const uint32_t m = ctx->host[1], maxlen = ctx->host[4];
   ctx->stats.n_proc = m;
   for (uint32_t q = 0; q < npairs; ++q) outs[q].n_out = m, outs[q].n_groups = 0;
@@ -826,6 +846,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->io) (void)hipFree(ctx->io);
   if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
   if (ctx->ws_nw) (void)hipFree(ctx->ws_nw);
+  if (ctx->nw_small) (void)hipFree(ctx->nw_small);
   for (void *p : ctx->pool.ptr)
     if (p) (void)hipFree(p);
   if (ctx->host) (void)hipHostFree(ctx->host);

@@ -36,6 +36,8 @@ struct rk_ctx {
   int pipeline = RK_PIPELINE_AUTO;
   void *ws_nw = nullptr;  // workspace of the record pipeline (rk_narrow.hip)
   size_t ws_nw_cap = 0;
+  void *nw_small = nullptr;  // its control words + digit histograms: allocated once, so
+                             // the pack check runs before the workspace is sized
   uint32_t *host = nullptr;  // pinned readback words
   // device copies for rk_classify (host-buffer entry point)
   void *io = nullptr;

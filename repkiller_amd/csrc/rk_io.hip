@@ -129,16 +129,28 @@ void io_destroy(rk_ctx *ctx) {
   ctx->ioe = nullptr;
 }
 
-static int io_ready(rk_ctx *ctx) {
-  if (ctx->ioe) return RK_OK;
-  auto *e = new IoEngine;
-  ctx->ioe = e;
+// The engine is built aside and published only when every resource exists: a
+// failed pinned allocation returns RK_E_HIP now and is retried by the next
+// call, instead of leaving a half-built engine (null slots / stream) behind.
+static int io_build(rk_ctx *ctx, IoEngine *e) {
   HIPCHK(ctx, hipStreamCreateWithFlags(&e->io, hipStreamNonBlocking));
   for (int k = 0; k < NSLOT; ++k) {
     HIPCHK(ctx, hipHostMalloc((void **)&e->slot[k], SLOT, hipHostMallocDefault));
     HIPCHK(ctx, hipEventCreateWithFlags(&e->ev[k], hipEventDisableTiming));
   }
   e->pool = new HostPool(io_threads());
+  return RK_OK;
+}
+
+static int io_ready(rk_ctx *ctx) {
+  if (ctx->ioe) return RK_OK;
+  auto *e = new IoEngine;
+  const int rc = io_build(ctx, e);
+  if (rc) {
+    delete e;  // the destructor skips the members that were never created
+    return rc;
+  }
+  ctx->ioe = e;
   return RK_OK;
 }
 

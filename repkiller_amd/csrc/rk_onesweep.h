@@ -1,6 +1,7 @@
-// rk_onesweep.h -- one-sweep LSD radix pass shared by the record pipeline
-// (rk_narrow.hip: 12- and 16-B records) and the key/value pair sort
-// (rk_radix.hip: 8-B pairs).  Included inside namespace rk { namespace { ... } }.
+// rk_onesweep.h -- the one-sweep LSD radix pass of the record pipeline
+// (rk_narrow.hip: 12- and 16-B records; its only user -- the generic
+// pipeline's pair sort in rk_radix.hip keeps its three-kernel passes, see
+// DESIGN.md).  Included inside namespace rk { namespace { ... } }.
 //
 // Src: rec_t (the record type), load(i) -> record i, key(rec) -> the sort key
 // word.  Dst: store(pos, rec); kWave / wave(rec, live) (see rk_narrow.hip).

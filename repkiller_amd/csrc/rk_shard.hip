@@ -46,6 +46,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -821,6 +822,14 @@ struct Shard {
   }
 };
 
+// Test hook: RK_TEST_FAULT=<stage> in one rank's environment makes that rank
+// fail locally at <stage> (as an allocation failure would), so the tests can
+// check that every peer still leaves the call with RK_E_PEER.
+bool fault_here(rk_ctx *, const char *stage) {
+  const char *e = std::getenv("RK_TEST_FAULT");
+  return e && std::strcmp(e, stage) == 0;
+}
+
 uint32_t owner_of_host(const Bounds &B, uint64_t key) {
   uint32_t q = 0;
   while (q + 1 < B.P && B.b[q + 1] <= key) ++q;
@@ -1435,15 +1444,25 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
     uint32_t nq = 0;
     uint64_t from[MAXP];
     const uint32_t *rqs = S.exchange<uint32_t>(rq.req, pp, SL_RQ, &nq, from);
-    uint2 *resp = S.take<uint2>(SL_RESP, nq + 1);
-    if (nq) {
-      k_respond<<<grid_for(nq, 256), 256, 0, S.st>>>(rqs, nq, poff, m, lpar, lab, cur, resp,
-                                                      S.ctrl);
-      S.launched("k_respond");
+    // the response all-to-all needs its own agreement point: both buffers are
+    // sized by skewed counts and the launch can fail on one rank alone
+    uint2 *resp = nullptr, *back = nullptr;
+    int rrc = RK_OK;
+    try {
+      resp = S.take<uint2>(SL_RESP, nq + 1);
+      back = S.take<uint2>(SL_BACK, pp.total + 1);
+      if (fault_here(ctx, "k_respond")) throw (int)RK_E_NOMEM;
+      if (nq) {
+        k_respond<<<grid_for(nq, 256), 256, 0, S.st>>>(rqs, nq, poff, m, lpar, lab, cur, resp,
+                                                        S.ctrl);
+        S.launched("k_respond");
+      }
+    } catch (int code) {
+      rrc = code;
     }
+    S.agree(rrc);
     uint64_t sb[MAXP], rb[MAXP];
     for (uint32_t q = 0; q < P; ++q) sb[q] = from[q] * sizeof(uint2), rb[q] = pp.cnt[q] * sizeof(uint2);
-    uint2 *back = S.take<uint2>(SL_BACK, pp.total + 1);
     S.run_a2a(resp, sb, back, rb);
     k_apply<<<grid_for((uint32_t)pp.total, 256), 256, 0, S.st>>>(back, rq.src, (uint32_t)pp.total,
                                                                   lab, cur);

@@ -15,6 +15,9 @@ and output digests, no reference source).
        (24.2 GB per 50M), more than this container has, so the
        restatement (pinned at cfg3 above and on every fixture) supplies the
        array digest.
+  cfg5q (250M, 3.75 Gbp, seed 5, repeat-rich) -- cfg5's shape (long bucket
+       runs, groups of 10^4-10^5 members) at a quarter of its size; the
+       restatement supplies the array digest, as for cfg4.
 
 Digests
   input_arrays_sha256   sha256(x_start | y_start | length | strand), the
@@ -24,7 +27,7 @@ Digests
   result_sha256         sha256(out_order u32 | gid u32 | repval u8), output
                         order, little-endian
 
-  python tests/golden/make_golden_large.py [cfg3] [cfg4]     (repo root)
+  python tests/golden/make_golden_large.py [cfg3] [cfg4] [cfg5q]   (repo root)
 """
 from __future__ import annotations
 
@@ -48,6 +51,11 @@ OUT = os.path.join(HERE, "large_hashes.json")
 CONFIGS = {
     "cfg3": dict(n=50_000_000, genome_len=3_000_000_000, seed=3),
     "cfg4": dict(n=200_000_000, genome_len=3_000_000_000, seed=4),
+    # cfg5's repeat-rich shape (95 % family fragments, 100..600 copies per
+    # family, cfg5's 0.067 fragments per bp) at a quarter of its size: the
+    # largest set the restatement classifies in this container's 64 GB
+    "cfg5q": dict(n=250_000_000, genome_len=3_750_000_000, seed=5, family_frac=0.95,
+                  copies=(100, 600)),
 }
 
 

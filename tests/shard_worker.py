@@ -54,12 +54,16 @@ def worker(rank, world, port, cases, q, comm_kind="host"):
             lr = case.get("lr", 0.3)
             if case.get("bad_rank") == rank:
                 lr = -1.0  # this rank alone fails its argument check
+            if case.get("fault_rank") == rank:  # rk_shard.hip fault_here(): fail at that stage
+                os.environ["RK_TEST_FAULT"] = case["fault"]
             try:
                 out = rk.classify_sharded(ctx, comm, x, y, ln, s, lx, ly, lr,
                                           case.get("pr", 0.3), case.get("lead_in", -1))
             except rk.RkError as e:
                 q.put((ci, rank, "error", e.code))
                 continue
+            finally:
+                os.environ.pop("RK_TEST_FAULT", None)
             r = out.result
             q.put((ci, rank, "ok", (out.out_offset, out.n_out_total, out.n_groups,
                                     r.out_order, r.gid, r.repval, rk.shard_stats(ctx))))

@@ -176,6 +176,27 @@ def test_sharded_one_rank_fails(gpu_ctx):
     assert np.array_equal(gid, want.gid) and np.array_equal(rep, want.repval)
 
 
+def test_sharded_fault_before_response_exchange(gpu_ctx):
+    """A rank that fails between the cross-slice root requests and the response
+    all-to-all (its response buffers are sized by skewed counts) must not leave
+    its peers inside the all-to-all: the response exchange has its own
+    agreement point, so the failing rank returns RK_E_NOMEM, the others
+    RK_E_PEER, and the next call on the same comm is bit-exact."""
+    base = dict(kind="synth", n=200_000, L=20_000_000, seed=34)
+    world = 3
+    cases = [dict(base, fault_rank=2, fault="k_respond"), base]
+    got = run_ranks(world, cases)
+    for r in range(world):
+        kind, code = got[(0, r)]
+        assert kind == "error", (r, kind, code)
+        assert code == (-6 if r == 2 else -11), (r, code)
+    order, gid, rep, ng, stats = assemble(got, 1, world)
+    assert sum(s["root_rounds"] for s in stats) > 0  # the response exchange ran
+    want, *_ = reference(gpu_ctx, base)
+    assert ng == want.n_groups and np.array_equal(order, want.out_order)
+    assert np.array_equal(gid, want.gid) and np.array_equal(rep, want.repval)
+
+
 def test_sharded_rccl_single_rank(gpu_ctx):
     cases = [dict(kind="synth", n=100_000, L=10_000_000, seed=31)]
     got = run_ranks(1, cases, comm_kind="rccl")
