@@ -598,6 +598,14 @@ class Comm:
                                                   ctypes.byref(h)))
         return cls(h, rank, size, keep=(ag, a2a, ops))
 
+    @classmethod
+    def local(cls, size: int) -> list["Comm"]:
+        """``size`` ranks inside this process (one thread per rank,
+        rk_comm_create_local): device blocks move by device copies."""
+        hs = (ctypes.c_void_p * size)()
+        _check(load_library().rk_comm_create_local(size, hs), "rk_comm_create_local")
+        return [cls(ctypes.c_void_p(hs[r]), r, size) for r in range(size)]
+
     def last_error(self) -> str:
         return load_library().rk_comm_last_error(self._h).decode()
 
@@ -646,6 +654,63 @@ def classify_sharded(ctx: "Context", comm: Comm, x, y, length, strand, len_x_hdr
         out = ClassifyResult(gid, rep, order, int(res.n_groups))
     return ShardOutput(out, int(res.out_offset), int(res.n_out), int(res.n_out_total),
                        int(res.n_groups), res)
+
+
+def classify_sharded_threads(f: Frags, ranks: int, len_x_hdr: int, len_y_hdr: int,
+                             len_ratio: float = 0.3, pos_ratio: float = 0.3,
+                             devices: list[int] | None = None) -> ClassifyResult:
+    """ONE host fragment set over ``ranks`` ranks of this process (the CLI's
+    ``--gpus P`` path, rk_cli.cpp): rank r holds the file-order rows
+    [n r / P, n (r + 1) / P), runs rk_classify_sharded_host on its own context
+    (device ``devices[r]``, default 0 for every rank) and copies its output
+    share into the whole result at its offset."""
+    import threading
+    lib = load_library()
+    n = f.n
+    devices = devices or [0] * ranks
+    comms = Comm.local(ranks)
+    order, gid, rep = np.empty(n, np.uint32), np.empty(n, np.uint32), np.empty(n, np.uint8)
+    status, errs, totals = [0] * ranks, [""] * ranks, [None] * ranks
+    prm = Params(len_x_hdr, len_y_hdr, len_ratio, pos_ratio)
+
+    def rank_body(r):
+        h = ctypes.c_void_p()
+        status[r] = lib.rk_create(ctypes.byref(h), devices[r])
+        if status[r]:
+            errs[r] = f"rk_create(device {devices[r]})"
+            lib.rk_comm_abandon(comms[r]._h, status[r])
+            return
+        try:
+            a, b = n * r // ranks, n * (r + 1) // ranks
+            soa = FragsSoA(*[int(c.ctypes.data) + a * c.itemsize
+                             for c in (f.x_start, f.y_start, f.length, f.strand)], b - a)
+            res = ShardResult()
+            status[r] = lib.rk_classify_sharded_host(h, comms[r]._h, ctypes.byref(soa),
+                                                     ctypes.byref(prm), -1, ctypes.byref(res))
+            if not status[r]:
+                o = int(res.out_offset)
+                status[r] = lib.rk_shard_copy_result(
+                    h, ctypes.byref(res), order.ctypes.data + 4 * o, gid.ctypes.data + 4 * o,
+                    rep.ctypes.data + o)
+                totals[r] = (int(res.n_out_total), int(res.n_groups))
+            if status[r]:
+                errs[r] = lib.rk_last_error(h).decode()
+        finally:
+            lib.rk_destroy(h)
+
+    threads = [threading.Thread(target=rank_body, args=(r,)) for r in range(ranks)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for c in comms:
+        c.close()
+    for r in range(ranks):
+        if status[r]:
+            raise RkError(status[r], f"rank {r}: {errs[r]}")
+    n_out, ng = totals[0]
+    assert all(t == totals[0] for t in totals), totals
+    return ClassifyResult(gid[:n_out], rep[:n_out], order[:n_out], ng)
 
 
 def shard_stats(ctx: "Context") -> dict:

@@ -491,10 +491,16 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   rk::exclusive_scan_u32(w.xcnt, w.xoff, (size_t)3 * cc.nch + 1, ss, st);
   HIPCHK(ctx, hipGetLastError());
   // the Y axis sorts on the second stream while the X axis is built and resolved
+  // (RK_Y_SERIAL=1: on the main stream, before it)
+  static const bool y_serial = [] {
+    const char *e = getenv("RK_Y_SERIAL");
+    return e && e[0] == '1';
+  }();
+  const hipStream_t sty = y_serial ? st : st2;
   HIPCHK(ctx, hipEventRecord(ctx->fork, st));
-  HIPCHK(ctx, hipStreamWaitEvent(st2, ctx->fork, 0));
-  rk::nw_y_sort_head(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, st2);
-  HIPCHK(ctx, hipEventRecord(ctx->join, st2));
+  HIPCHK(ctx, hipStreamWaitEvent(sty, ctx->fork, 0));
+  rk::nw_y_sort_head(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, sty);
+  HIPCHK(ctx, hipEventRecord(ctx->join, sty));
   mark(ctx, RK_PH_GATHER);
   rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, w.xoff, w.cx, w.xpos, w.erec, w.ctrl, cc.W,
                   st);
