@@ -249,15 +249,35 @@ void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint6
 void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
                    const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
                    hipStream_t st);
-void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st);
+// (halo, G): the sharded driver's G lead-in records ahead of R (R holds m - G)
+void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st,
+                const uint4 *halo = nullptr, uint32_t G = 0);
+// arrival_ids: the first pass numbers the entries by position (the sharded
+// driver's received Y records), instead of keeping their processing index;
+// src0: the first pass reads these records instead of yrec (which then only
+// takes the intermediates, with tmp)
 void nw_y_sort_head(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
-                    const uint32_t *yhist, uint32_t *status, hipStream_t st);
+                    const uint32_t *yhist, uint32_t *status, hipStream_t st,
+                    bool arrival_ids = false, const uint4 *src0 = nullptr);
 void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDigits &y,
                     const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
-                    uint64_t max_y, const uint32_t *xbits, hipStream_t st);
+                    uint64_t max_y, const uint32_t *xbits, hipStream_t st,
+                    bool arrival_ids = false, const uint4 *src0 = nullptr);
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
                  const uint32_t *xoff, Csr cx, uint32_t *xpos, uint4 *erec, uint32_t *ctrl,
-                 uint32_t W, hipStream_t st);
+                 uint32_t W, hipStream_t st, const uint4 *halo = nullptr, uint32_t G = 0);
+// the sharded driver (rk_shard_nw.h): the processing order of received 16-B
+// records (Y records numbered from `base`), digit histograms of records whose
+// key is their first word (minus sub), the member sort of received records
+void nw_order_sort_recs(const uint4 *in, uint32_t m, uint32_t nby, uint32_t base,
+                        const NwDigits &a, const uint32_t *ghist, uint32_t *status, uint4 *Ra,
+                        uint4 *Rb, uint4 *yrec, hipStream_t st);
+void nw_rec_hist(const void *recs, int rec_bytes, uint32_t n, uint32_t sub, const NwDigits &d,
+                 uint32_t *ghist, hipStream_t st);
+void nw_member_sort_recv(const void *recs, bool narrow_keys, uint32_t m, uint32_t g0,
+                         const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint4 *t0,
+                         uint4 *t1, uint32_t *sgid, uint64_t *key, uint32_t *tag, uint32_t *mrow,
+                         hipStream_t st);
 // X hits as a bitmask by processing index, from the resolved X axis (xpos[k] =
 // X position of fragment k); then the Y states: X hits sit in the Y lists
 void nw_x_bits(const uint32_t *xpos, const uint8_t *xstate, uint32_t m, uint32_t *bits,

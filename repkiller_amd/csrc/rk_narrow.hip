@@ -219,14 +219,66 @@ struct DstProc {
   uint4 *out;
   uint3 *yrec;
   uint32_t nby;
+  uint32_t base;  // processing index of position 0 (the sharded driver's slice offset)
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const {
     out[pos] = r;
     const uint64_t ys = rec_y(r);
     const uint32_t len = rec_len(r), s = rec_strand(r);
     const uint64_t yc = ys + len / 2;
-    yrec[pos] = make_uint3(s * nby + (uint32_t)(yc / 100), pos, len | (uint32_t)(yc % 100) << 24);
+    yrec[pos] = make_uint3(s * nby + (uint32_t)(yc / 100), base + pos,
+                           len | (uint32_t)(yc % 100) << 24);
   }
 };
+
+// --- sharded driver: records as received from other ranks -------------------
+// the Y records in arrival order: the entry id becomes the arrival index (the
+// global processing index stays in the received array)
+struct SrcIdx12 {
+  using rec_t = uint3;
+  const uint3 *in;
+  __device__ __forceinline__ uint3 load(uint32_t i) const {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
+    return make_uint3(__builtin_nontemporal_load(p), i, __builtin_nontemporal_load(p + 2));
+  }
+  __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
+};
+// member records {gid, row, key ...} with the gid made local to the rank's range
+struct SrcSub12 {
+  using rec_t = uint3;
+  const uint3 *in;
+  uint32_t sub;
+  __device__ __forceinline__ uint3 load(uint32_t i) const {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
+    return make_uint3(__builtin_nontemporal_load(p) - sub, __builtin_nontemporal_load(p + 1),
+                      __builtin_nontemporal_load(p + 2));
+  }
+  __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
+};
+struct SrcSub16 {
+  using rec_t = uint4;
+  const uint4 *in;
+  uint32_t sub;
+  __device__ __forceinline__ uint4 load(uint32_t i) const {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(in + i));
+    return make_uint4(v.x - sub, v.y, v.z, v.w);
+  }
+  __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
+};
+
+// digit histograms of every pass of a sort over records whose key is their
+// first word (minus `sub`); STRIDE = record size in words
+template <int STRIDE>
+__global__ void __launch_bounds__(256) k_nw_rec_hist(const uint32_t *__restrict__ recs, uint32_t n,
+                                                     uint32_t sub, Digits D,
+                                                     uint32_t *__restrict__ ghist) {
+  __shared__ HistLds L;
+  hist_init(L);
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    hist_add(L, D, recs[(size_t)i * STRIDE] - sub);
+  __syncthreads();
+  hist_flush(L, D, ghist);
+}
 
 // --- Y axis, last pass: the CSR arrays the sweeps read -----------------------
 struct DstCsr {
@@ -362,8 +414,18 @@ __global__ void __launch_bounds__(256) k_nw_order_hist(OrderHistArgs a) {
 // + chunk of the row's X bucket] (strand s) and cnts[2 nch + owner chunk]
 // (xStart/10 / 10W).  Runs of equal ids are added per wave into an LDS window
 // of chunks, flushed with one global atomic per non-zero bin.
+// The processing order the X axis is built from: G halo records (the sharded
+// driver's lead-in from earlier slices, rk_shard_nw.h) ahead of the own
+// records; G = 0 on one device.
+struct RecView {
+  const uint4 *h;
+  uint32_t G;
+  const uint4 *o;
+  __device__ __forceinline__ uint4 operator[](uint32_t k) const { return k < G ? h[k] : o[k - G]; }
+};
+
 constexpr int XN_T = 256, XN_ITEMS = 16, XN_WIN = 1024;
-__global__ void __launch_bounds__(XN_T) k_nw_xcount(const uint4 *__restrict__ R, uint32_t m,
+__global__ void __launch_bounds__(XN_T) k_nw_xcount(const RecView R, uint32_t m,
                                                     uint32_t lgW, uint32_t nch, uint32_t kdiv,
                                                     uint32_t *__restrict__ cnts) {
   __shared__ uint32_t win[3 * XN_WIN];
@@ -406,7 +468,7 @@ __global__ void __launch_bounds__(XN_T) k_nw_xcount(const uint4 *__restrict__ R,
 
 constexpr int XC_WAVES = 4, XC_SLOTS = 8;  // rows per batch: XC_SLOTS x 64
 struct XChunkArgs {
-  const uint4 *R;        // processing order
+  RecView R;             // processing order
   uint32_t m;            // kept rows
   uint32_t W, lgW, nch;  // chunk width in buckets (power of two), chunks
   uint32_t halo;         // ceil(H / 10) in xStart/10 units
@@ -881,11 +943,13 @@ void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint6
   kt_end(st, KID_NW_HIST, 25.0 * n);  // the SoA read once
 }
 
-// the processing order: passes over records, the first one from the file SoA
-void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
-                   const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
-                   hipStream_t st) {
-  const uint32_t n = (uint32_t)in.n;
+// the processing order: passes over records, the first one from `first`
+// (the file SoA, or records received by the sharded driver); the Y records
+// carry processing index base + position
+template <class Src1>
+static void nw_order_passes(const Src1 &first, double in_bytes, uint32_t n, uint32_t nby,
+                            uint32_t base, const NwDigits &a, const uint32_t *ghist,
+                            uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec, hipStream_t st) {
   const Digits D = to_digits(a);
   const size_t sw = nw_status_words(n);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
@@ -899,14 +963,14 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     const bool last = p == D.passes - 1;
-    const DstProc dp{out, reinterpret_cast<uint3 *>(yrec), nby};
+    const DstProc dp{out, reinterpret_cast<uint3 *>(yrec), nby, base};
     if (p == 0) {
-      SrcFile sf{in.x_start, in.y_start, in.length, in.strand, vsize};
       if (last)
-        launch_pass(sf, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 25.0 * n + 28.0 * n, nxt);
+        launch_pass(first, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, in_bytes * n + 28.0 * n,
+                    nxt);
       else
-        launch_pass(sf, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st,
-                    25.0 * n + 16.0 * n, nxt);
+        launch_pass(first, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st,
+                    in_bytes * n + 16.0 * n, nxt);
     } else if (last) {
       launch_pass(SrcRec{src}, dp, n, D.shift[p], D.db[p], gh, stp, ctr, st, 44.0 * n, nxt);
     } else {
@@ -915,8 +979,30 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
     }
   }
 }
+void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
+                   const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
+                   hipStream_t st) {
+  nw_order_passes(SrcFile{in.x_start, in.y_start, in.length, in.strand, vsize}, 25.0,
+                  (uint32_t)in.n, nby, 0u, a, ghist, status, Ra, Rb, yrec, st);
+}
+void nw_order_sort_recs(const uint4 *in, uint32_t m, uint32_t nby, uint32_t base,
+                        const NwDigits &a, const uint32_t *ghist, uint32_t *status, uint4 *Ra,
+                        uint4 *Rb, uint4 *yrec, hipStream_t st) {
+  nw_order_passes(SrcRec{in}, 16.0, m, nby, base, a, ghist, status, Ra, Rb, yrec, st);
+}
 
-// a sort of m 16-B records by .x, the last pass writing through `final`
+void nw_rec_hist(const void *recs, int rec_bytes, uint32_t n, uint32_t sub, const NwDigits &d,
+                 uint32_t *ghist, hipStream_t st) {
+  if (!n) return;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(recs);
+  kt_begin(st);
+  if (rec_bytes == 16)
+    k_nw_rec_hist<4><<<grid_for(n, 256, 2048), 256, 0, st>>>(w, n, sub, to_digits(d), ghist);
+  else
+    k_nw_rec_hist<3><<<grid_for(n, 256, 2048), 256, 0, st>>>(w, n, sub, to_digits(d), ghist);
+  kt_end(st, KID_NW_HIST, (double)rec_bytes * n);  // the records' lines are read whole
+}
+
 
 // The Y axis sort in two parts: every pass but the last (on the second stream,
 // beside the X axis), then the last one, which writes the CSR arrays and --
@@ -924,35 +1010,46 @@ void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const N
 // reads yrec (p = 0) or the previous pass' output; intermediates alternate
 // tmp, yrec (yrec is free once the first pass read it).
 void nw_y_sort_head(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
-                    const uint32_t *yhist, uint32_t *status, hipStream_t st) {
+                    const uint32_t *yhist, uint32_t *status, hipStream_t st, bool arrival_ids,
+                    const uint4 *src0) {
   const Digits D = to_digits(y);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
   const PassStatus ps = pass_status(status, m, D, 12);  // the tail pass' half is cleared here
   // 12-B records (DstProc); the buffers are uint4 arrays, large enough
-  const uint3 *src = reinterpret_cast<const uint3 *>(yrec);
+  const uint3 *src = reinterpret_cast<const uint3 *>(src0 ? src0 : yrec);
   for (int p = 0; p + 1 < D.passes; ++p) {
     ps.prepare(p, m, D, st);
     uint3 *out = reinterpret_cast<uint3 *>(p % 2 == 0 ? tmp : const_cast<uint4 *>(yrec));
-    launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], ghist_of(yhist, p),
-                ps.use(p), status + sw - 64 + p, st, 24.0 * m, ps.next(p, D.passes));
+    if (p == 0 && arrival_ids)
+      launch_pass(SrcIdx12{src}, DstRec12{out}, m, D.shift[p], D.db[p], ghist_of(yhist, p),
+                  ps.use(p), status + sw - 64 + p, st, 24.0 * m, ps.next(p, D.passes));
+    else
+      launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], ghist_of(yhist, p),
+                  ps.use(p), status + sw - 64 + p, st, 24.0 * m, ps.next(p, D.passes));
     src = out;
   }
 }
 void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDigits &y,
                     const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
-                    uint64_t max_y, const uint32_t *xbits, hipStream_t st) {
+                    uint64_t max_y, const uint32_t *xbits, hipStream_t st, bool arrival_ids,
+                    const uint4 *src0) {
   const Digits D = to_digits(y);
   const size_t sw = nw_status_words(m);
   const int p = D.passes - 1;
-  const uint3 *src = reinterpret_cast<const uint3 *>(p == 0 ? yrec : (p - 1) % 2 == 0 ? tmp : yrec);
+  const uint3 *src = reinterpret_cast<const uint3 *>(
+      p == 0 ? (src0 ? src0 : yrec) : (p - 1) % 2 == 0 ? tmp : yrec);
   const PassStatus ps = pass_status(status, m, D, 12);
   ps.prepare(p, m, D, st);  // a no-op after the head's clear-ahead
   if (p == 0) (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);
-  launch_pass(SrcRec12{src},
-              DstCsr{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, xbits, cy.state}, m,
-              D.shift[p], D.db[p], ghist_of(yhist, p), ps.use(p), status + sw - 64 + p, st,
-              12.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0));
+  const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, xbits, cy.state};
+  const double bytes = 12.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0);
+  if (p == 0 && arrival_ids)
+    launch_pass(SrcIdx12{src}, dc, m, D.shift[p], D.db[p], ghist_of(yhist, p), ps.use(p),
+                status + sw - 64 + p, st, bytes);
+  else
+    launch_pass(SrcRec12{src}, dc, m, D.shift[p], D.db[p], ghist_of(yhist, p), ps.use(p),
+                status + sw - 64 + p, st, bytes);
 }
 
 // The member sort by gid: 12-B records {gid, row, key} when every sort key
@@ -1003,6 +1100,22 @@ void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t
                                                       ehist, status, fin, st);
 }
 
+// the member sort of the sharded driver: received {gid, row, key ...} records
+// (12 B when every sort key fits 32 bits, else 16 B), gids made local (- g0)
+void nw_member_sort_recv(const void *recs, bool narrow_keys, uint32_t m, uint32_t g0,
+                         const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint4 *t0,
+                         uint4 *t1, uint32_t *sgid, uint64_t *key, uint32_t *tag, uint32_t *mrow,
+                         hipStream_t st) {
+  const DstMembers fin{sgid, tag, mrow, key};
+  if (narrow_keys)
+    nw_member_passes<uint3, SrcSub12, SrcRec12, DstRec12>(
+        SrcSub12{reinterpret_cast<const uint3 *>(recs), g0}, reinterpret_cast<uint3 *>(t0),
+        reinterpret_cast<uint3 *>(t1), m, e, ehist, status, fin, st);
+  else
+    nw_member_passes<uint4, SrcSub16, SrcRec, DstRec>(
+        SrcSub16{reinterpret_cast<const uint4 *>(recs), g0}, t0, t1, m, e, ehist, status, fin, st);
+}
+
 uint32_t nw_chunk_width(uint32_t m, uint32_t nbx) {
   // about 256-512 rows per chunk (one batch of the chunk kernel), 64..1024 buckets
   const double per_bucket = (double)m / (double)(nbx ? nbx : 1);
@@ -1013,26 +1126,27 @@ uint32_t nw_chunk_width(uint32_t m, uint32_t nbx) {
 
 uint32_t nw_chunks(uint32_t nbx, uint32_t W) { return (nbx + W - 1) / W; }
 
-void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st) {
+void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st,
+                const uint4 *halo, uint32_t G) {
   (void)hipMemsetAsync(cc.cnts, 0, ((size_t)3 * cc.nch + 1) * 4, st);
   if (!m) return;
   kt_begin(st);
-  k_nw_xcount<<<(m + XN_T * XN_ITEMS - 1) / (XN_T * XN_ITEMS), XN_T, 0, st>>>(R, m, cc.lgW, cc.nch,
-                                                                             10 * cc.W, cc.cnts);
+  k_nw_xcount<<<(m + XN_T * XN_ITEMS - 1) / (XN_T * XN_ITEMS), XN_T, 0, st>>>(
+      RecView{halo, G, R}, m, cc.lgW, cc.nch, 10 * cc.W, cc.cnts);
   kt_end(st, KID_NW_XCOUNT, 16.0 * m);
 }
 
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
                  const uint32_t *xoff, Csr cx, uint32_t *xpos, uint4 *erec, uint32_t *ctrl,
-                 uint32_t W, hipStream_t st) {
+                 uint32_t W, hipStream_t st, const uint4 *halo, uint32_t G) {
   if (!m) return;
   uint32_t lgW = 0;
   while ((1u << lgW) < W) ++lgW;
   const uint32_t nch = nw_chunks(nbx, W);
   // the member records take the erec buffer (16 B per row) as two arrays
   uint2 *erk = reinterpret_cast<uint2 *>(erec);
-  XChunkArgs a{R,   m,    W,   lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx, xpos,
-               erk, reinterpret_cast<uint32_t *>(erk + m), ctrl};
+  XChunkArgs a{RecView{halo, G, R}, m, W, lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx,
+               xpos, erk, reinterpret_cast<uint32_t *>(erk + m), ctrl};
   kt_begin(st);
   k_nw_xchunk<<<(nch + XC_WAVES - 1) / XC_WAVES, 64 * XC_WAVES,
                 XC_WAVES * 2 * W * sizeof(uint32_t), st>>>(a);

@@ -585,6 +585,8 @@ enum Slot : int {
   SL_YXH, SL_YMASK, SL_YCODE, SL_COUNT
 };
 
+constexpr int kPoolSlots = 160;  // slots of both drivers (rk_shard_nw.h adds its own)
+
 struct PartPlan {
   uint32_t n = 0, nblk = 1;
   uint32_t *off = nullptr;
@@ -639,7 +641,7 @@ struct Shard {
   template <class T>
   T *take(int slot, size_t count) {
     rk_pool &pl = ctx->pool;
-    if (pl.ptr.size() < (size_t)SL_COUNT) pl.ptr.resize(SL_COUNT, nullptr), pl.cap.resize(SL_COUNT, 0);
+    if (pl.ptr.size() < (size_t)kPoolSlots) pl.ptr.resize(kPoolSlots, nullptr), pl.cap.resize(kPoolSlots, 0);
     const size_t need = align_up(count * sizeof(T) + 16);
     if (need > pl.cap[slot]) {
       if (pl.ptr[slot]) (void)hipFree(pl.ptr[slot]);
@@ -950,6 +952,201 @@ uint32_t resolve(Shard &S, const AxisIn &a, const AxisSlots &sl, const rk_params
   return sweep_axis(S, a, c, p);
 }
 
+// The Y halo check of both drivers: owners send the states of their entries in
+// a neighbour's relevant halo (YStateOp); a rank whose local decisions
+// disagree re-solves its Y problem with that halo fixed -- solve_y(ymap, c):
+// the selected entries, arrival order -- until every rank agrees.
+template <class SolveY>
+void verify_y_halo(Shard &S, RelOp relop, const uint8_t *ycode, uint8_t *ystate, uint8_t *yused,
+                   const Bounds &yb, uint32_t ny, SolveY &&solve_y) {
+  rk_ctx *ctx = S.ctx;
+  rk_shard_stats &ss = ctx->shard_stats;
+  const uint32_t P = S.P, me = S.me;
+  const uint64_t ylo = yb.b[me], yhi = yb.b[me + 1];
+  PartPlan pp;
+  S.plan(relop, ny, pp);
+  const uint32_t nrel = (uint32_t)pp.total;
+  uint32_t *relidx = S.take<uint32_t>(SL_RELIDX, nrel + 1);
+  relop.out = relidx;
+  S.emit(relop, pp);
+  if (nrel) {
+    k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, nullptr, ystate, yused);
+    S.launched("k_set_used");
+  }
+  YStateOp yso{};
+  yso.code = ycode;
+  yso.ystate = ystate;
+  for (uint32_t q = 0; q < P; ++q) {  // whose relevant halo holds my first / last bucket
+    if (q == me) continue;
+    if (yb.b[q + 1] == ylo) yso.first_mask |= 1u << q;
+    if (yb.b[q] == yhi) yso.last_mask |= 1u << q;
+  }
+  for (;;) {
+    ++ss.y_rounds;
+    if (ss.y_rounds > 64) {
+      ctx->err = "Y halo verification did not converge";
+      throw RK_E_INTERNAL;
+    }
+    S.plan(yso, ny, pp);
+    yso.out = S.take<uint8_t>(SL_SEND, pp.total + 1);
+    S.emit(yso, pp);
+    uint32_t n2 = 0;
+    uint8_t *rys = S.exchange<uint8_t>(yso.out, pp, SL_RYS, &n2);
+    if (n2 != nrel) {
+      ctx->err = "Y halo state count mismatch";
+      throw RK_E_INTERNAL;
+    }
+    S.zero(S.ctrl + 2, 4);
+    if (nrel) {
+      k_cmp_y<<<grid_for(nrel, 256, 1024), 256, 0, S.st>>>(relidx, nrel, yused, rys,
+                                                            S.ctrl + 2);
+      S.launched("k_cmp_y");
+    }
+    const uint32_t mism = S.read1(S.ctrl + 2);
+    if (S.sum_any(mism) == 0) break;
+    if (mism) {
+      ++ss.y_reruns;
+      k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, rys, nullptr, yused);
+      S.launched("k_set_used");
+      SelYOp sel{ycode, yused, nullptr};
+      Shard S1 = S;
+      S1.P = 1;
+      S1.me = 0;
+      PartPlan sp;
+      S1.plan(sel, ny, sp);
+      sel.out = S.take<uint32_t>(SL_YMAP, sp.total + 1);
+      S1.emit(sel, sp);
+      solve_y(sel.out, (uint32_t)sp.total);
+    }
+  }
+}
+
+// Roots and gids of both drivers: parents (own X winners in xg, the Y winners
+// of own X misses received in prr) -> slice-local parent chains compressed by
+// pointer jumping, cross-slice links by request/response rounds, gid = global
+// rank of the root among new groups.  Returns the gid of every own entry
+// (processing order); *Gtot = the number of groups.
+const uint32_t *resolve_roots(Shard &S, const uint32_t *xg, const ParRec *prr, uint32_t npar,
+                              uint32_t m, uint32_t poff, const Bounds &slices, uint64_t *Gtot_out) {
+  rk_ctx *ctx = S.ctx;
+  rk_shard_stats &ss = ctx->shard_stats;
+  const uint32_t P = S.P, me = S.me;
+  PartPlan pp;
+  uint32_t *parg = S.take<uint32_t>(SL_PARG, m + 1);
+  uint32_t *lpar = S.take<uint32_t>(SL_LPAR, m + 1);
+  uint32_t *ext = S.take<uint32_t>(SL_EXT, m + 1);
+  uint32_t *isroot = S.take<uint32_t>(SL_ISROOT, m + 2);
+  uint32_t *lrank = S.take<uint32_t>(SL_LRANK, m + 2);
+  uint32_t *junk = S.take<uint32_t>(SL_JUNK, m + 1);
+  uint32_t *lab = S.take<uint32_t>(SL_LAB, m + 1);
+  uint32_t *cur = S.take<uint32_t>(SL_CUR, m + 1);
+  if (m) {
+    kt_begin(S.st);
+    k_par_init<<<grid_for(m, 256), 256, 0, S.st>>>(xg, m, parg);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
+    if (npar) {
+      kt_begin(S.st);
+      k_par_scatter<<<grid_for(npar, 256), 256, 0, S.st>>>(prr, npar, poff, m, parg, S.ctrl);
+      kt_end(S.st, KID_SHARD_AUX, 0.0);
+    }
+    kt_begin(S.st);
+    k_local_par<<<grid_for(m, 256), 256, 0, S.st>>>(parg, m, poff, lpar, ext, isroot, S.ctrl);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
+    S.launched("parents");
+    Proc jp{};
+    jp.par = lpar;
+    for (uint32_t rounds = 0;; ++rounds) {
+      if (rounds > 64) {
+        ctx->err = "pointer jumping did not converge";
+        throw RK_E_INTERNAL;
+      }
+      S.zero(S.ctrl + 3, 4);
+      jump_round(jp, m, S.ctrl + 3, rounds == 0 ? junk : nullptr, S.ctrl, S.st);
+      S.launched("jump_round");
+      if (!S.read1(S.ctrl + 3)) break;
+    }
+    exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), S.st);
+  }
+  S.agree_errors();
+  const uint32_t nroots = m ? S.read1(lrank + m) : 0;
+  std::vector<uint64_t> rall = S.gather1<uint64_t>(nroots);
+  uint64_t goff = 0, Gtot = 0;
+  for (uint32_t q = 0; q < P; ++q) Gtot += rall[q], goff += q < me ? rall[q] : 0;
+  if (m) {
+    kt_begin(S.st);
+    k_init_labels<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, ext, lrank, (uint32_t)goff, m, lab,
+                                                        cur);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
+    S.launched("k_init_labels");
+  }
+  for (;;) {  // cross-slice links: request/response rounds (the owner answers
+              // with its current knowledge, so chains halve every round)
+    ReqOp rq{lpar, lab, cur, slices, nullptr, nullptr};
+    S.plan(rq, m, pp);
+    if (S.sum_any(pp.total) == 0) break;
+    if (++ss.root_rounds > 64) {
+      ctx->err = "cross-slice root resolution did not converge";
+      throw RK_E_INTERNAL;
+    }
+    rq.req = S.take<uint32_t>(SL_REQ, pp.total + 1);
+    rq.src = S.take<uint32_t>(SL_SRC, pp.total + 1);
+    S.emit(rq, pp);
+    uint32_t nq = 0;
+    uint64_t from[MAXP];
+    const uint32_t *rqs = S.exchange<uint32_t>(rq.req, pp, SL_RQ, &nq, from);
+    // the response all-to-all needs its own agreement point: both buffers are
+    // sized by skewed counts and the launch can fail on one rank alone
+    uint2 *resp = nullptr, *back = nullptr;
+    int rrc = RK_OK;
+    try {
+      resp = S.take<uint2>(SL_RESP, nq + 1);
+      back = S.take<uint2>(SL_BACK, pp.total + 1);
+      if (fault_here(ctx, "k_respond")) throw (int)RK_E_NOMEM;
+      if (nq) {
+        k_respond<<<grid_for(nq, 256), 256, 0, S.st>>>(rqs, nq, poff, m, lpar, lab, cur, resp,
+                                                        S.ctrl);
+        S.launched("k_respond");
+      }
+    } catch (int code) {
+      rrc = code;
+    }
+    S.agree(rrc);
+    uint64_t sb[MAXP], rb[MAXP];
+    for (uint32_t q = 0; q < P; ++q) sb[q] = from[q] * sizeof(uint2), rb[q] = pp.cnt[q] * sizeof(uint2);
+    S.run_a2a(resp, sb, back, rb);
+    k_apply<<<grid_for((uint32_t)pp.total, 256), 256, 0, S.st>>>(back, rq.src, (uint32_t)pp.total,
+                                                                  lab, cur);
+    S.launched("k_apply");
+  }
+  uint32_t *gid_own = junk;  // the jump's scratch is free again
+  if (m) {
+    kt_begin(S.st);
+    k_final_gid<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, lab, m, gid_own, S.ctrl);
+    kt_end(S.st, KID_SHARD_AUX, 0.0);
+    S.launched("k_final_gid");
+  }
+  S.agree_errors();
+  *Gtot_out = Gtot;
+  return gid_own;
+}
+
+// the call's statistics and kernel timings (both drivers)
+void finish_stats(Shard &S, uint32_t nl, const rk_shard_result *out,
+                  std::chrono::steady_clock::time_point t0) {
+  rk_ctx *ctx = S.ctx;
+  rk_shard_stats &ss = ctx->shard_stats;
+  if (ctx->profiling) collect_kernel_timing(ctx);
+  ss.bytes_sent = S.bytes_sent;
+  ss.ms_total = ms_since(t0);
+  ctx->stats = rk_stats{};
+  ctx->stats.n_in = nl;
+  ctx->stats.n_proc = ss.n_slice;
+  ctx->stats.n_groups = out->n_groups;
+  ctx->stats.device_ms = ss.ms_total;
+}
+
+#include "rk_shard_nw.h"
+
 int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm,
                           int32_t lead_in, rk_shard_result *out, int pre) {
   rk_ctx *ctx = S.ctx;
@@ -1000,6 +1197,20 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   const uint32_t nl = (uint32_t)in->n;
   ss.n_in = nl;
   ss.n_total = N;
+  // the record pipeline's internals when every row of every rank packs into a
+  // 16-B record (rk_shard_nw.h); RK_SHARD_GENERIC=1 forces this driver
+  static const bool generic_only = [] {
+    const char *e = std::getenv("RK_SHARD_GENERIC");
+    return e && e[0] == '1';
+  }();
+  if (!generic_only) {
+    const int r = classify_sharded_nw(S, in, p, P, me, N, row_base, lead_in, out, t0);
+    if (r != RK_SHARD_FALLBACK) {
+      finish_stats(S, nl, out, t0);
+      return r;
+    }
+    S.zero(S.ctrl, 256 * 4);
+  }
 
   // ---- 1: processing keys, slice bounds from the global xStart/10 histogram
   Frags f{in->x_start, in->y_start, in->length, in->strand, nl};
@@ -1314,63 +1525,9 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   };
   // relevant halo entries grouped by owner (the order owners send their states in)
   const uint64_t ylo = yb.b[me], yhi = yb.b[me + 1];
-  RelOp relop{ycode, ylo ? owner_of_host(yb, ylo - 1) : 0u,
-              yhi < nby ? owner_of_host(yb, yhi) : 0u, nullptr};
-  S.plan(relop, ny, pp);
-  const uint32_t nrel = (uint32_t)pp.total;
-  uint32_t *relidx = S.take<uint32_t>(SL_RELIDX, nrel + 1);
-  relop.out = relidx;
-  S.emit(relop, pp);
-  if (nrel) {
-    k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, nullptr, ystate, yused);
-    S.launched("k_set_used");
-  }
-  YStateOp yso{};
-  yso.code = ycode;
-  yso.ystate = ystate;
-  for (uint32_t q = 0; q < P; ++q) {  // whose relevant halo holds my first / last bucket
-    if (q == me) continue;
-    if (yb.b[q + 1] == ylo) yso.first_mask |= 1u << q;
-    if (yb.b[q] == yhi) yso.last_mask |= 1u << q;
-  }
-  for (;;) {
-    ++ss.y_rounds;
-    if (ss.y_rounds > 64) {
-      ctx->err = "Y halo verification did not converge";
-      throw RK_E_INTERNAL;
-    }
-    S.plan(yso, ny, pp);
-    yso.out = S.take<uint8_t>(SL_SEND, pp.total + 1);
-    S.emit(yso, pp);
-    uint32_t n2 = 0;
-    uint8_t *rys = S.exchange<uint8_t>(yso.out, pp, SL_RYS, &n2);
-    if (n2 != nrel) {
-      ctx->err = "Y halo state count mismatch";
-      throw RK_E_INTERNAL;
-    }
-    S.zero(S.ctrl + 2, 4);
-    if (nrel) {
-      k_cmp_y<<<grid_for(nrel, 256, 1024), 256, 0, S.st>>>(relidx, nrel, yused, rys,
-                                                            S.ctrl + 2);
-      S.launched("k_cmp_y");
-    }
-    const uint32_t mism = S.read1(S.ctrl + 2);
-    if (S.sum_any(mism) == 0) break;
-    if (mism) {
-      ++ss.y_reruns;
-      k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, rys, nullptr, yused);
-      S.launched("k_set_used");
-      SelYOp sel{ycode, yused, nullptr};
-      Shard S1 = S;
-      S1.P = 1;
-      S1.me = 0;
-      PartPlan sp;
-      S1.plan(sel, ny, sp);
-      sel.out = S.take<uint32_t>(SL_YMAP, sp.total + 1);
-      S1.emit(sel, sp);
-      solve_y(sel.out, (uint32_t)sp.total);
-    }
-  }
+  const RelOp relop{ycode, ylo ? owner_of_host(yb, ylo - 1) : 0u,
+                    yhi < nby ? owner_of_host(yb, yhi) : 0u, nullptr};
+  verify_y_halo(S, relop, ycode, ystate, yused, yb, ny, solve_y);
   ss.ms_y += ms_since(ty2);
 
 
@@ -1382,100 +1539,8 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   S.emit(pop, pp);
   uint32_t npar = 0;
   const ParRec *prr = S.exchange<ParRec>(pop.out, pp, SL_PR, &npar);
-  uint32_t *parg = S.take<uint32_t>(SL_PARG, m + 1);
-  uint32_t *lpar = S.take<uint32_t>(SL_LPAR, m + 1);
-  uint32_t *ext = S.take<uint32_t>(SL_EXT, m + 1);
-  uint32_t *isroot = S.take<uint32_t>(SL_ISROOT, m + 2);
-  uint32_t *lrank = S.take<uint32_t>(SL_LRANK, m + 2);
-  uint32_t *junk = S.take<uint32_t>(SL_JUNK, m + 1);
-  uint32_t *lab = S.take<uint32_t>(SL_LAB, m + 1);
-  uint32_t *cur = S.take<uint32_t>(SL_CUR, m + 1);
-  if (m) {
-    kt_begin(S.st);
-    k_par_init<<<grid_for(m, 256), 256, 0, S.st>>>(xg, m, parg);
-    kt_end(S.st, KID_SHARD_AUX, 0.0);
-    if (npar) {
-      kt_begin(S.st);
-      k_par_scatter<<<grid_for(npar, 256), 256, 0, S.st>>>(prr, npar, poff, m, parg, S.ctrl);
-      kt_end(S.st, KID_SHARD_AUX, 0.0);
-    }
-    kt_begin(S.st);
-    k_local_par<<<grid_for(m, 256), 256, 0, S.st>>>(parg, m, poff, lpar, ext, isroot, S.ctrl);
-    kt_end(S.st, KID_SHARD_AUX, 0.0);
-    S.launched("parents");
-    Proc jp{};
-    jp.par = lpar;
-    for (uint32_t rounds = 0;; ++rounds) {
-      if (rounds > 64) {
-        ctx->err = "pointer jumping did not converge";
-        throw RK_E_INTERNAL;
-      }
-      S.zero(S.ctrl + 3, 4);
-      jump_round(jp, m, S.ctrl + 3, rounds == 0 ? junk : nullptr, S.ctrl, S.st);
-      S.launched("jump_round");
-      if (!S.read1(S.ctrl + 3)) break;
-    }
-    exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), S.st);
-  }
-  S.agree_errors();
-  const uint32_t nroots = m ? S.read1(lrank + m) : 0;
-  std::vector<uint64_t> rall = S.gather1<uint64_t>(nroots);
-  uint64_t goff = 0, Gtot = 0;
-  for (uint32_t q = 0; q < P; ++q) Gtot += rall[q], goff += q < me ? rall[q] : 0;
-  if (m) {
-    kt_begin(S.st);
-    k_init_labels<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, ext, lrank, (uint32_t)goff, m, lab,
-                                                        cur);
-    kt_end(S.st, KID_SHARD_AUX, 0.0);
-    S.launched("k_init_labels");
-  }
-  for (;;) {  // cross-slice links: request/response rounds (the owner answers
-              // with its current knowledge, so chains halve every round)
-    ReqOp rq{lpar, lab, cur, slices, nullptr, nullptr};
-    S.plan(rq, m, pp);
-    if (S.sum_any(pp.total) == 0) break;
-    if (++ss.root_rounds > 64) {
-      ctx->err = "cross-slice root resolution did not converge";
-      throw RK_E_INTERNAL;
-    }
-    rq.req = S.take<uint32_t>(SL_REQ, pp.total + 1);
-    rq.src = S.take<uint32_t>(SL_SRC, pp.total + 1);
-    S.emit(rq, pp);
-    uint32_t nq = 0;
-    uint64_t from[MAXP];
-    const uint32_t *rqs = S.exchange<uint32_t>(rq.req, pp, SL_RQ, &nq, from);
-    // the response all-to-all needs its own agreement point: both buffers are
-    // sized by skewed counts and the launch can fail on one rank alone
-    uint2 *resp = nullptr, *back = nullptr;
-    int rrc = RK_OK;
-    try {
-      resp = S.take<uint2>(SL_RESP, nq + 1);
-      back = S.take<uint2>(SL_BACK, pp.total + 1);
-      if (fault_here(ctx, "k_respond")) throw (int)RK_E_NOMEM;
-      if (nq) {
-        k_respond<<<grid_for(nq, 256), 256, 0, S.st>>>(rqs, nq, poff, m, lpar, lab, cur, resp,
-                                                        S.ctrl);
-        S.launched("k_respond");
-      }
-    } catch (int code) {
-      rrc = code;
-    }
-    S.agree(rrc);
-    uint64_t sb[MAXP], rb[MAXP];
-    for (uint32_t q = 0; q < P; ++q) sb[q] = from[q] * sizeof(uint2), rb[q] = pp.cnt[q] * sizeof(uint2);
-    S.run_a2a(resp, sb, back, rb);
-    k_apply<<<grid_for((uint32_t)pp.total, 256), 256, 0, S.st>>>(back, rq.src, (uint32_t)pp.total,
-                                                                  lab, cur);
-    S.launched("k_apply");
-  }
-  uint32_t *gid_own = junk;  // the jump's scratch is free again
-  if (m) {
-    kt_begin(S.st);
-    k_final_gid<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, lab, m, gid_own, S.ctrl);
-    kt_end(S.st, KID_SHARD_AUX, 0.0);
-    S.launched("k_final_gid");
-  }
-  S.agree_errors();
+  uint64_t Gtot = 0;
+  const uint32_t *gid_own = resolve_roots(S, xg, prr, npar, m, poff, slices, &Gtot);
   ss.ms_roots = ms_since(tr);
 
   // ---- 6: members -> gid-range owners; exact in-group order; emit
@@ -1535,14 +1600,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   out->out_offset = ooff;
   out->n_out_total = otot;
   out->n_groups = Gtot;
-  if (ctx->profiling) collect_kernel_timing(ctx);
-  ss.bytes_sent = S.bytes_sent;
-  ss.ms_total = ms_since(t0);
-  ctx->stats = rk_stats{};
-  ctx->stats.n_in = nl;
-  ctx->stats.n_proc = m;
-  ctx->stats.n_groups = Gtot;
-  ctx->stats.device_ms = ss.ms_total;
+  finish_stats(S, nl, out, t0);
   (void)M;
   return RK_OK;
 }
