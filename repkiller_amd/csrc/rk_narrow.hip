@@ -998,8 +998,10 @@ void nw_rec_hist(const void *recs, int rec_bytes, uint32_t n, uint32_t sub, cons
   kt_begin(st);
   if (rec_bytes == 16)
     k_nw_rec_hist<4><<<grid_for(n, 256, 2048), 256, 0, st>>>(w, n, sub, to_digits(d), ghist);
-  else
+  else if (rec_bytes == 12)
     k_nw_rec_hist<3><<<grid_for(n, 256, 2048), 256, 0, st>>>(w, n, sub, to_digits(d), ghist);
+  else  // a plain key array
+    k_nw_rec_hist<1><<<grid_for(n, 256, 2048), 256, 0, st>>>(w, n, sub, to_digits(d), ghist);
   kt_end(st, KID_NW_HIST, (double)rec_bytes * n);  // the records' lines are read whole
 }
 

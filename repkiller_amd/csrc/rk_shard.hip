@@ -104,48 +104,82 @@ struct ParRec {
 // are stable: rank-d records keep element order.
 // mcache: masks of an earlier plan over the same elements (mread), or where
 // this plan stores them (the scatter then reads them back)
+// A block handles PART_TILE consecutive elements in PART_ROUNDS rounds of 256
+// (round r: elements tile + 256 r + thread); per round and wave, only the
+// destinations present in the wave (the OR of its masks) are balloted.
+constexpr uint32_t PART_ROUNDS = 16, PART_TILE = 256 * PART_ROUNDS;
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off);
+  return v;
+}
 template <class Op>
 __global__ void __launch_bounds__(256) k_part_count(Op op, uint32_t n, uint32_t P, uint32_t nblk,
                                                     uint32_t *cnt, uint32_t *mcache, bool mread) {
-  __shared__ uint32_t wc[4][MAXP];
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  uint32_t mask = 0u;
-  if (i < n) {
-    mask = mread ? mcache[i] : op.mask(i);
-    if (mcache && !mread) mcache[i] = mask;
-  }
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (uint32_t d = 0; d < P; ++d) {
-    const uint64_t b = __ballot((mask >> d) & 1u);
-    if (lane == 0) wc[w][d] = (uint32_t)__popcll(b);
+  __shared__ uint32_t bc[MAXP];
+  if (threadIdx.x < MAXP) bc[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t t0 = blockIdx.x * PART_TILE + threadIdx.x;
+  for (uint32_t r = 0; r < PART_ROUNDS; ++r) {
+    const uint32_t i = t0 + 256 * r;
+    uint32_t mask = 0u;
+    if (i < n) {
+      mask = mread ? mcache[i] : op.mask(i);
+      if (mcache && !mread) mcache[i] = mask;
+    }
+    for (uint32_t any = wave_or(mask); any; any &= any - 1) {
+      const uint32_t d = __builtin_ctz(any);
+      const uint64_t b = __ballot((mask >> d) & 1u);
+      if (lane == 0) atomicAdd(&bc[d], (uint32_t)__popcll(b));
+    }
   }
   __syncthreads();
-  if (threadIdx.x < P) {
-    const uint32_t d = threadIdx.x;
-    cnt[(size_t)d * nblk + blockIdx.x] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
-  }
+  if (threadIdx.x < P) cnt[(size_t)threadIdx.x * nblk + blockIdx.x] = bc[threadIdx.x];
 }
 
 template <class Op>
 __global__ void __launch_bounds__(256) k_part_scatter(Op op, uint32_t n, uint32_t P,
                                                       uint32_t nblk, const uint32_t *off,
                                                       const uint32_t *mcache) {
-  __shared__ uint32_t wc[4][MAXP];
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t mask = i < n ? (mcache ? mcache[i] : op.mask(i)) : 0u;
+  // wc[r][w][d]: round r, wave w's count of destination d, then its first position
+  __shared__ uint32_t wc[PART_ROUNDS][4][MAXP];
+  for (uint32_t j = threadIdx.x; j < PART_ROUNDS * 4 * MAXP; j += 256) (&wc[0][0][0])[j] = 0;
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
-  for (uint32_t d = 0; d < P; ++d) {
-    const uint64_t b = __ballot((mask >> d) & 1u);
-    if (lane == 0) wc[w][d] = (uint32_t)__popcll(b);
+  const uint32_t t0 = blockIdx.x * PART_TILE + threadIdx.x;
+  uint32_t mask[PART_ROUNDS];
+#pragma unroll
+  for (uint32_t r = 0; r < PART_ROUNDS; ++r) {
+    const uint32_t i = t0 + 256 * r;
+    mask[r] = i < n ? (mcache ? mcache[i] : op.mask(i)) : 0u;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < PART_ROUNDS; ++r)
+    for (uint32_t any = wave_or(mask[r]); any; any &= any - 1) {
+      const uint32_t d = __builtin_ctz(any);
+      const uint64_t b = __ballot((mask[r] >> d) & 1u);
+      if (lane == 0) wc[r][w][d] = (uint32_t)__popcll(b);
+    }
+  __syncthreads();
+  if (threadIdx.x < P) {  // destination d: its positions in (round, wave) order
+    const uint32_t d = threadIdx.x;
+    uint32_t acc = off[(size_t)d * nblk + blockIdx.x];
+    for (uint32_t r = 0; r < PART_ROUNDS; ++r)
+      for (uint32_t v = 0; v < 4; ++v) {
+        const uint32_t c = wc[r][v][d];
+        wc[r][v][d] = acc;
+        acc += c;
+      }
   }
   __syncthreads();
-  for (uint32_t d = 0; d < P; ++d) {
-    const uint64_t b = __ballot((mask >> d) & 1u);
-    if ((mask >> d) & 1u) {
-      uint32_t pos = off[(size_t)d * nblk + blockIdx.x] + (uint32_t)__popcll(b & lt);
-      for (uint32_t v = 0; v < w; ++v) pos += wc[v][d];
-      op.emit(i, d, pos);
+#pragma unroll
+  for (uint32_t r = 0; r < PART_ROUNDS; ++r) {
+    const uint32_t i = t0 + 256 * r;
+    for (uint32_t any = wave_or(mask[r]); any; any &= any - 1) {
+      const uint32_t d = __builtin_ctz(any);
+      const uint64_t b = __ballot((mask[r] >> d) & 1u);
+      if ((mask[r] >> d) & 1u) op.emit(i, d, wc[r][w][d] + (uint32_t)__popcll(b & lt));
     }
   }
 }
@@ -488,10 +522,6 @@ __global__ void k_set_used(const uint32_t *relidx, uint32_t nrel, const uint8_t 
   }
 }
 
-__global__ void k_par_init(const uint32_t *xg, uint32_t m, uint32_t *par) {
-  GRID_STRIDE(k, m) par[k] = xg[k];
-}
-
 __global__ void k_par_scatter(const ParRec *pr, uint32_t np, uint32_t poff, uint32_t m,
                               uint32_t *par, uint32_t *err) {
   GRID_STRIDE(i, np) {
@@ -506,6 +536,7 @@ __global__ void k_par_scatter(const ParRec *pr, uint32_t np, uint32_t poff, uint
 // cross-slice link; roots are the new groups
 __global__ void k_local_par(const uint32_t *par, uint32_t m, uint32_t poff, uint32_t *lpar,
                             uint32_t *ext, uint32_t *isroot, uint32_t *err) {
+  bool link = false;
   GRID_STRIDE(k, m) {
     uint32_t pg = par[k];
     if (pg == NONE || pg > poff + k) {  // parents are always earlier (or self)
@@ -515,9 +546,11 @@ __global__ void k_local_par(const uint32_t *par, uint32_t m, uint32_t poff, uint
     const bool local = pg >= poff;
     lpar[k] = local ? pg - poff : k;
     ext[k] = local ? NONE : pg;
+    link |= !local;
     isroot[k] = pg == poff + k ? 1u : 0u;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) isroot[m] = 0;
+  if (__ballot(link) && (threadIdx.x & 63) == 0) atomicOr(&err[23], 1u);  // a cross-slice link
 }
 
 __global__ void k_init_labels(const uint32_t *lpar, const uint32_t *ext, const uint32_t *lrank,
@@ -561,6 +594,12 @@ __global__ void k_final_gid(const uint32_t *lpar, const uint32_t *lab, uint32_t 
     if (g == NONE) atomicOr(err, ERRB_INTERNAL);
     gid[k] = g;
   }
+}
+
+// no rank has a cross-slice link: every root is local, gid = goff + its rank
+__global__ void k_final_gid_local(const uint32_t *lpar, const uint32_t *lrank, uint32_t goff,
+                                  uint32_t m, uint32_t *gid) {
+  GRID_STRIDE(k, m) gid[k] = goff + lrank[lpar[k]];
 }
 
 __global__ void k_mem_keys(const ulonglong2 *mem, uint32_t n, uint32_t g0, uint32_t *lg) {
@@ -744,7 +783,7 @@ struct Shard {
   template <class Op>
   void plan(const Op &op, uint32_t n, PartPlan &pp) {
     pp.n = n;
-    pp.nblk = n ? (n + 255) / 256 : 1;
+    pp.nblk = n ? (n + PART_TILE - 1) / PART_TILE : 1;
     const size_t len = (size_t)P * pp.nblk + 1;
     uint32_t *cnt = take<uint32_t>(SL_PCNT, len);
     pp.off = take<uint32_t>(SL_POFF, len);
@@ -759,6 +798,13 @@ struct Shard {
     std::vector<uint32_t> t = d2h(ctrl + 128, P + 1);
     for (uint32_t q = 0; q < P; ++q) pp.cnt[q] = t[q + 1] - t[q];
     pp.total = t[P];
+  }
+  // a plan that sends nothing (the op cannot select any element)
+  void zero_plan(uint32_t n, PartPlan &pp) {
+    pp.n = n;
+    pp.nblk = 1;
+    for (uint32_t q = 0; q < MAXP; ++q) pp.cnt[q] = 0;
+    pp.total = 0;
   }
   template <class Op>
   void emit(const Op &op, const PartPlan &pp) {
@@ -964,11 +1010,14 @@ void verify_y_halo(Shard &S, RelOp relop, const uint8_t *ycode, uint8_t *ystate,
   const uint32_t P = S.P, me = S.me;
   const uint64_t ylo = yb.b[me], yhi = yb.b[me + 1];
   PartPlan pp;
-  S.plan(relop, ny, pp);
+  // no neighbour range on either side (one rank): no relevant halo entries
+  const bool lonely = ylo == 0 && yhi == yb.b[P];
+  if (lonely) S.zero_plan(ny, pp);
+  else S.plan(relop, ny, pp);
   const uint32_t nrel = (uint32_t)pp.total;
   uint32_t *relidx = S.take<uint32_t>(SL_RELIDX, nrel + 1);
   relop.out = relidx;
-  S.emit(relop, pp);
+  if (!lonely) S.emit(relop, pp);
   if (nrel) {
     k_set_used<<<grid_for(nrel, 256), 256, 0, S.st>>>(relidx, nrel, nullptr, ystate, yused);
     S.launched("k_set_used");
@@ -987,9 +1036,11 @@ void verify_y_halo(Shard &S, RelOp relop, const uint8_t *ycode, uint8_t *ystate,
       ctx->err = "Y halo verification did not converge";
       throw RK_E_INTERNAL;
     }
-    S.plan(yso, ny, pp);
+    const bool none = !yso.first_mask && !yso.last_mask;  // no neighbour reads my states
+    if (none) S.zero_plan(ny, pp);
+    else S.plan(yso, ny, pp);
     yso.out = S.take<uint8_t>(SL_SEND, pp.total + 1);
-    S.emit(yso, pp);
+    if (!none) S.emit(yso, pp);
     uint32_t n2 = 0;
     uint8_t *rys = S.exchange<uint8_t>(yso.out, pp, SL_RYS, &n2);
     if (n2 != nrel) {
@@ -1026,13 +1077,13 @@ void verify_y_halo(Shard &S, RelOp relop, const uint8_t *ycode, uint8_t *ystate,
 // pointer jumping, cross-slice links by request/response rounds, gid = global
 // rank of the root among new groups.  Returns the gid of every own entry
 // (processing order); *Gtot = the number of groups.
-const uint32_t *resolve_roots(Shard &S, const uint32_t *xg, const ParRec *prr, uint32_t npar,
+const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_t npar,
                               uint32_t m, uint32_t poff, const Bounds &slices, uint64_t *Gtot_out) {
   rk_ctx *ctx = S.ctx;
   rk_shard_stats &ss = ctx->shard_stats;
   const uint32_t P = S.P, me = S.me;
   PartPlan pp;
-  uint32_t *parg = S.take<uint32_t>(SL_PARG, m + 1);
+  uint32_t *parg = xg;  // X winners; the X misses' Y winners are scattered in
   uint32_t *lpar = S.take<uint32_t>(SL_LPAR, m + 1);
   uint32_t *ext = S.take<uint32_t>(SL_EXT, m + 1);
   uint32_t *isroot = S.take<uint32_t>(SL_ISROOT, m + 2);
@@ -1041,9 +1092,6 @@ const uint32_t *resolve_roots(Shard &S, const uint32_t *xg, const ParRec *prr, u
   uint32_t *lab = S.take<uint32_t>(SL_LAB, m + 1);
   uint32_t *cur = S.take<uint32_t>(SL_CUR, m + 1);
   if (m) {
-    kt_begin(S.st);
-    k_par_init<<<grid_for(m, 256), 256, 0, S.st>>>(xg, m, parg);
-    kt_end(S.st, KID_SHARD_AUX, 0.0);
     if (npar) {
       kt_begin(S.st);
       k_par_scatter<<<grid_for(npar, 256), 256, 0, S.st>>>(prr, npar, poff, m, parg, S.ctrl);
@@ -1069,9 +1117,27 @@ const uint32_t *resolve_roots(Shard &S, const uint32_t *xg, const ParRec *prr, u
   }
   S.agree_errors();
   const uint32_t nroots = m ? S.read1(lrank + m) : 0;
-  std::vector<uint64_t> rall = S.gather1<uint64_t>(nroots);
+  // root count (low 32 bits) and whether this rank has a cross-slice link
+  std::vector<uint64_t> rall =
+      S.gather1<uint64_t>(nroots | (uint64_t)(m ? S.read1(S.ctrl + 23) : 0u) << 32);
   uint64_t goff = 0, Gtot = 0;
-  for (uint32_t q = 0; q < P; ++q) Gtot += rall[q], goff += q < me ? rall[q] : 0;
+  bool links = false;
+  for (uint32_t q = 0; q < P; ++q) {
+    const uint64_t r = rall[q] & 0xFFFFFFFFull;
+    Gtot += r, goff += q < me ? r : 0;
+    links |= (rall[q] >> 32) != 0;
+  }
+  if (!links) {  // every chain ends in its own slice: no label rounds
+    if (m) {
+      kt_begin(S.st);
+      k_final_gid_local<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, lrank, (uint32_t)goff, m, junk);
+      kt_end(S.st, KID_SHARD_AUX, 12.0 * m);
+      S.launched("k_final_gid_local");
+    }
+    S.agree_errors();
+    *Gtot_out = Gtot;
+    return junk;
+  }
   if (m) {
     kt_begin(S.st);
     k_init_labels<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, ext, lrank, (uint32_t)goff, m, lab,

@@ -33,6 +33,14 @@ constexpr int RK_SHARD_FALLBACK = 1 << 20;  // not a status: run the generic dri
 // largest bucket index get_associated_group touches for centre c
 // (SequenceOcupationList.cpp:47-89; the same bound as rk_narrow.hip's)
 __device__ __forceinline__ uint64_t probe_max_bucket_sh(uint64_t c, uint64_t max_index) {
+  if (c < (1ull << 32) - 2 && max_index != 0 && max_index < (1ull << 32)) {
+    // the same in 32 bits (no wrap of c + 2 or max_index - 1 here)
+    const uint32_t c32 = (uint32_t)c, m32 = (uint32_t)max_index;
+    uint32_t b = c32 / 100u;
+    if (c32 < m32 && (c32 + 1) / 100u > b) b = (c32 + 1) / 100u;
+    if (c32 < m32 - 1 && (c32 + 2) / 100u > b) b = (c32 + 2) / 100u;
+    return b;
+  }
   uint64_t b = c / 100;
   if (c < max_index && (c + 1) / 100 > b) b = (c + 1) / 100;
   if (c < max_index - 1 && (c + 2) / 100 > b) b = (c + 2) / 100;
@@ -56,8 +64,11 @@ struct ShRowsArgs {
   Frags f;
   uint64_t vsize, max_x, max_y;
   uint32_t shift;
-  uint32_t *hist, *ctrl;
+  uint32_t *hist, *ctrl;  // hist null: one rank owns everything, no bounds to find
 };
+__device__ __forceinline__ uint64_t div10_sh(uint64_t v) {  // 32-bit when it fits
+  return v < (1ull << 32) ? (uint64_t)((uint32_t)v / 10u) : v / 10;
+}
 __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
   __shared__ uint32_t h[NBINS];
   __shared__ uint32_t red[2];
@@ -69,7 +80,7 @@ __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
   bool ub = false, ubc = false, wide = false;
   GRID_STRIDE(i, a.f.n) {
     const uint64_t xs = a.f.x[i], ys = a.f.y[i], L0 = a.f.len[i];
-    const uint64_t pk = xs / 10;
+    const uint64_t pk = div10_sh(xs);
     ub |= pk >= a.vsize;
     if (pk >= drop) continue;  // the never-iterated last bucket (or out of bounds)
     wide |= L0 >= (1ull << 24) || ys >= (1ull << 35);
@@ -78,7 +89,7 @@ __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
     const uint64_t hl = len / 2;
     ubc |= probe_max_bucket_sh(xs + hl, a.max_x) > a.max_x ||
            probe_max_bucket_sh(ys + hl, a.max_y) > a.max_y;
-    atomicAdd(&h[(uint32_t)pk >> a.shift], 1u);
+    if (a.hist) atomicAdd(&h[(uint32_t)pk >> a.shift], 1u);
   }
   for (int off = 32; off > 0; off >>= 1) {
     const uint32_t o = __shfl_xor(maxlen, off);
@@ -90,8 +101,9 @@ __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
     atomicOr(&red[1], (bub ? 1u : 0u) | (bubc ? 2u : 0u) | (bwide ? 4u : 0u));
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < NBINS; b += 256)
-    if (h[b]) atomicAdd(&a.hist[b], h[b]);
+  if (a.hist)
+    for (uint32_t b = threadIdx.x; b < NBINS; b += 256)
+      if (h[b]) atomicAdd(&a.hist[b], h[b]);
   if (threadIdx.x == 0) {
     if (red[0]) atomicMax(&a.ctrl[21], red[0]);
     if (red[1] & 1u) atomicOr(&a.ctrl[0], ERRB_UB_BUCKET);
@@ -107,7 +119,7 @@ struct RowOp16 {  // kept rows -> slice owners, as processing-order records
   uint32_t drop, row_base;
   uint4 *out;
   __device__ uint32_t key(uint32_t i) const {
-    const uint64_t pk = f.x[i] / 10;
+    const uint64_t pk = div10_sh(f.x[i]);
     return pk < drop ? (uint32_t)pk : drop;
   }
   __device__ uint32_t mask(uint32_t i) const {
@@ -117,9 +129,10 @@ struct RowOp16 {  // kept rows -> slice owners, as processing-order records
   __device__ void emit(uint32_t i, uint32_t, uint32_t pos) const {
     const uint64_t xs = f.x[i], ys = f.y[i], L = f.len[i];
     const uint32_t s = f.strand[i] != 'f' ? 1u : 0u;
-    out[pos] = make_uint4(key(i), row_base + i, (uint32_t)ys,
+    const uint64_t pk = div10_sh(xs);
+    out[pos] = make_uint4((uint32_t)pk, row_base + i, (uint32_t)ys,
                           (uint32_t)(L & 0xFFFFFFu) | s << 24 | (uint32_t)((ys >> 32) & 7u) << 25 |
-                              (uint32_t)(xs % 10) << 28);
+                              (uint32_t)(xs - pk * 10) << 28);
   }
 };
 
@@ -183,15 +196,18 @@ struct YOp12 {  // own Y records -> Y-range owners (+ their halos), processing o
   }
 };
 
-struct ParOp12 {  // Y decisions of own X misses -> slice owners
+struct ParOp12 {  // Y decisions of own X misses -> slice owners (other ranks)
   const uint3 *yr;
   const uint8_t *code;
   Bounds slices;
   const uint32_t *ywin;
+  uint32_t me;
   ParRec *out;
   __device__ uint32_t mask(uint32_t r) const {
     const uint8_t c = code[r];
-    return !(c & 3) && !(c & YC_XHIT) ? 1u << owner_of(slices, yr[r].y) : 0u;
+    if ((c & 3) || (c & YC_XHIT)) return 0u;
+    const uint32_t q = owner_of(slices, yr[r].y);
+    return q == me ? 0u : 1u << q;  // this rank's own slice: written in place
   }
   __device__ void emit(uint32_t r, uint32_t, uint32_t pos) const {
     out[pos] = ParRec{yr[r].y, ywin[r]};
@@ -288,17 +304,26 @@ __global__ void k_sh_ysel(const uint3 *yr, const uint8_t *code, const uint32_t *
   }
 }
 
+// (the Y winner of an X miss of this rank's own slice -- processing index in
+// [poff, poff + m) -- goes straight into its parent word xpar)
 __global__ void k_sh_y_results(const uint3 *yr, const uint8_t *code, const uint32_t *ymap,
-                               uint32_t c, const uint32_t *par, uint8_t *ystate, uint32_t *ywin) {
+                               uint32_t c, const uint32_t *par, uint8_t *ystate, uint32_t *ywin,
+                               uint32_t poff, uint32_t m, uint32_t *xpar) {
   GRID_STRIDE(k, c) {
     const uint32_t r = ymap ? ymap[k] : k;
-    if (code[r] & YC_XHIT) {
+    const uint8_t cr = code[r];
+    if (cr & YC_XHIT) {
       ystate[r] = 1;
       ywin[r] = NONE;
     } else {
       const uint32_t p = par[k];
       ystate[r] = p == k ? 1 : 0;
-      ywin[r] = yr[ymap ? ymap[p] : p].y;
+      const uint32_t w = yr[ymap ? ymap[p] : p].y;
+      ywin[r] = w;
+      if (!(cr & 3)) {
+        const uint32_t own = yr[r].y - poff;
+        if (own < m) xpar[own] = w;
+      }
     }
   }
 }
@@ -351,7 +376,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   if (nl) {
     kt_begin(st);
     k_sh_rows<<<grid_for(nl, 256, 512), 256, 0, st>>>(
-        ShRowsArgs{f, vsize, max_x, max_y, shift, hist, S.ctrl});
+        ShRowsArgs{f, vsize, max_x, max_y, shift, P > 1 ? hist : nullptr, S.ctrl});
     kt_end(st, KID_SH_ROWKEYS, 25.0 * nl);
     S.launched("k_sh_rows");
   }
@@ -362,7 +387,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     nopack |= v & 1u, maxlen = (v >> 1) > maxlen ? (v >> 1) : maxlen;
   if (nopack) return RK_SHARD_FALLBACK;
   std::vector<uint64_t> gh(NBINS, 0);
-  {
+  if (P > 1) {
     std::vector<uint32_t> mine = S.d2h(hist, NBINS), all((size_t)P * NBINS);
     S.allgather(mine.data(), all.data(), NBINS * 4);
     for (uint32_t q = 0; q < P; ++q)
@@ -414,7 +439,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   yop.nby = nby;
   yop.P = P;
   yop.shift = bin_shift(nby);
-  const Bounds yb = split_bounds(global_hist(S, yop, m), yop.shift, nby, P);
+  const Bounds yb = split_bounds(P > 1 ? global_hist(S, yop, m) : std::vector<uint64_t>(NBINS, 0),
+                                 yop.shift, nby, P);
   for (uint32_t q = 0; q < MAXP; ++q) {
     yop.lo[q] = q < P ? (int64_t)yb.b[q] - 1 - (int64_t)H : 0;
     yop.hi[q] = q < P ? (int64_t)yb.b[q + 1] + 1 + (int64_t)H : 0;
@@ -422,10 +448,14 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   PartPlan ypp;
   ypp.mcache = S.take<uint32_t>(SL_YMASK, m + 1);  // the X-hit bytes follow the same masks
   S.plan(yop, m, ypp);
-  yop.out = S.take<uint3>(SN_SY, ypp.total + 1);
-  S.emit(yop, ypp);
+  // every own record stays here, once: the send layout is the records themselves
+  const bool y_self = ypp.total == m && ypp.cnt[me] == m;
+  if (!y_self) {
+    yop.out = S.take<uint3>(SN_SY, ypp.total + 1);
+    S.emit(yop, ypp);
+  }
   uint32_t ny = 0;
-  const uint3 *yr = exchange_nw<uint3>(S, yop.out, ypp, SN_YR, &ny);
+  const uint3 *yr = exchange_nw<uint3>(S, y_self ? yop.yrec : yop.out, ypp, SN_YR, &ny);
   ss.y_entries = ny;
   const uint64_t ylo = yb.b[me], yhi = yb.b[me + 1];
   uint8_t *ycode = S.take<uint8_t>(SL_YCODE, ny + 1);
@@ -634,7 +664,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   auto y_results = [&](const uint32_t *ymap, uint32_t c) {
     if (!c) return;
     kt_begin(st);
-    k_sh_y_results<<<grid_for(c, 256), 256, 0, st>>>(yr, ycode, ymap, c, par_l, ystate, ywin);
+    k_sh_y_results<<<grid_for(c, 256), 256, 0, st>>>(yr, ycode, ymap, c, par_l, ystate, ywin,
+                                                      poff, m, xg);
     kt_end(st, KID_SH_YRES, 0.0);
     S.launched("k_sh_y_results");
   };
@@ -660,10 +691,11 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
 
   // ---- 8: parents back to the slice owners; roots; gids
   const auto tr = std::chrono::steady_clock::now();
-  ParOp12 pop{yr, ycode, slices, ywin, nullptr};
-  S.plan(pop, ny, pp);
+  ParOp12 pop{yr, ycode, slices, ywin, me, nullptr};
+  if (P == 1) S.zero_plan(ny, pp);  // every parent is local (written by k_sh_y_results)
+  else S.plan(pop, ny, pp);
   pop.out = S.take<ParRec>(SL_SEND, pp.total + 1);
-  S.emit(pop, pp);
+  if (P > 1) S.emit(pop, pp);
   uint32_t npar = 0;
   const ParRec *prr = S.exchange<ParRec>(pop.out, pp, SL_PR, &npar);
   uint64_t Gtot = 0;
@@ -679,16 +711,28 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   MemOpNw mop{gid_own, erk + Gfin, reinterpret_cast<const uint32_t *>(erk + mx) + Gfin,
               {}, bin_shift(Gtot), narrow, nullptr};
   (void)hfin;
-  const Bounds gb = split_bounds(global_hist(S, mop, m), mop.shift, Gtot, P);
+  const Bounds gb = split_bounds(P > 1 ? global_hist(S, mop, m) : std::vector<uint64_t>(NBINS, 0),
+                                 mop.shift, Gtot, P);
   mop.B = gb;
   S.plan(mop, m, pp);
   const size_t esz = narrow ? 12 : 16;
-  mop.out = S.take<uint8_t>(SN_SMEM, (pp.total + 1) * esz);
-  S.emit(mop, pp);
+  // one rank: every member stays here and the X chunk's member arrays are
+  // exactly the own rows (no halo): the member sort reads them in place, as on
+  // one device
+  const bool m_self = P == 1 && pp.total == m && Gfin == 0;
+  if (!m_self) {
+    mop.out = S.take<uint8_t>(SN_SMEM, (pp.total + 1) * esz);
+    S.emit(mop, pp);
+  }
   uint32_t mr = 0;
-  const void *mem = narrow
-      ? (const void *)exchange_nw<uint3>(S, (const uint3 *)mop.out, pp, SL_MEM, &mr)
-      : (const void *)exchange_nw<uint4>(S, (const uint4 *)mop.out, pp, SL_MEM, &mr);
+  const void *mem = nullptr;
+  if (m_self) {
+    S.agree(RK_OK);  // the exchange's agreement point
+    mr = m;
+  } else {
+    mem = narrow ? (const void *)exchange_nw<uint3>(S, (const uint3 *)mop.out, pp, SL_MEM, &mr)
+                 : (const void *)exchange_nw<uint4>(S, (const uint4 *)mop.out, pp, SL_MEM, &mr);
+  }
   const uint32_t g0 = (uint32_t)gb.b[me], Gl = (uint32_t)(gb.b[me + 1] - gb.b[me]);
   uint32_t *ogid = S.take<uint32_t>(SL_OGID, mr + 1);
   uint8_t *orep = S.take<uint8_t>(SL_OREP, mr + 1);
@@ -705,9 +749,15 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     uint32_t *mstat = S.take<uint32_t>(SN_STAT, nw_status_words(mr + 1));
     void *gsort = S.take<uint8_t>(SL_GSORT, groupsort_scratch_bytes(mr));
     S.zero(ehist, 4096 * 4);
-    nw_rec_hist(mem, (int)esz, mr, g0, ed, ehist, st);
-    nw_member_sort_recv(mem, narrow, mr, g0, ed, ehist, mstat, t0, t1, sgid, reckey, tag, mrow,
-                        st);
+    if (m_self) {
+      nw_rec_hist(gid_own, 4, mr, g0, ed, ehist, st);
+      nw_member_sort(reinterpret_cast<const uint4 *>(erk), gid_own, t0, t1, mr, ed, ehist, mstat,
+                     sgid, reckey, tag, mrow, narrow, st);
+    } else {
+      nw_rec_hist(mem, (int)esz, mr, g0, ed, ehist, st);
+      nw_member_sort_recv(mem, narrow, mr, g0, ed, ehist, mstat, t0, t1, sgid, reckey, tag, mrow,
+                          st);
+    }
     group_offsets(sgid, mr, Gl, goffs, st);
     // the group-sort tiers on both streams, as in the single-device path
     sort_groups_exact(sgid, goffs, Gl, mr, reckey, tag, otag, gsort,
