@@ -162,6 +162,7 @@ struct SrcMem16 {
 // sorted slots of the tile (kWave = false: not at all)
 #define RK_NO_WAVE                   \
   static constexpr bool kWave = false; \
+  static constexpr bool kPre = false;  \
   template <class R_>                  \
   __device__ __forceinline__ void wave(const R_ &, bool) const {}
 struct DstRec {
@@ -281,14 +282,21 @@ __global__ void __launch_bounds__(256) k_nw_rec_hist(const uint32_t *__restrict_
 }
 
 // --- Y axis, last pass: the CSR arrays the sweeps read -----------------------
+// The X-hit lookup is a dependent load per record; with kPre the write-out
+// issues it one slot round ahead (pre), and store() takes the loaded word.
 struct DstCsr {
-  RK_NO_WAVE
+  static constexpr bool kPre = true;
   uint32_t *key, *ent;
   uint2 *pk;
   uint8_t *nbd;
   uint32_t nb;
   uint64_t max_index;
-  __device__ __forceinline__ void store(uint32_t pos, const uint3 &r) const {
+  const uint32_t *xbits;  // null: the states are filled later (k_nw_fill_y)
+  uint8_t *state;
+  __device__ __forceinline__ uint32_t pre(const uint3 &r) const {
+    return xbits ? xbits[r.y >> 5] : 0u;
+  }
+  __device__ __forceinline__ void store(uint32_t pos, const uint3 &r, uint32_t xw) const {
     key[pos] = r.x;
     ent[pos] = r.y;
     const uint32_t b = r.x >= nb ? r.x - nb : r.x;
@@ -297,10 +305,8 @@ struct DstCsr {
     nbd[pos] = nbd_code_nw(c, max_index);
     // with the X results (bitmask by processing index): the Y states -- X hits
     // sit in the Y lists (commonFunctions.cpp:59), X misses query them
-    if (xbits) state[pos] = (xbits[r.y >> 5] >> (r.y & 31)) & 1u ? ST_ACTIVE : ST_UNKNOWN;
+    if (xbits) state[pos] = (xw >> (r.y & 31)) & 1u ? ST_ACTIVE : ST_UNKNOWN;
   }
-  const uint32_t *xbits;  // null: the states are filled later (k_nw_fill_y)
-  uint8_t *state;
 };
 
 // --- group members, last pass: gid order (stable: processing order inside) -

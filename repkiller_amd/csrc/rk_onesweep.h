@@ -263,15 +263,33 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
         __syncthreads();
       }
       const uint32_t h1 = cnt - h0 < (uint32_t)LSLOTS ? cnt : h0 + LSLOTS;
-      for (uint32_t j0 = h0; j0 < h1; j0 += T) {  // wave-uniform trip count (Dst::wave)
-        const uint32_t j = j0 + threadIdx.x;
-        const bool live = j < h1;
-        const R r = live ? srec[j - h0] : R{};
-        if (live) {
-          const uint32_t d = (src.key(r) >> shift) & (RADIX - 1);
-          dst.store(gpos[d] + (j - lbase[d]), r);
+      if constexpr (Dst::kPre) {
+        // the Dst's dependent per-record load issued one slot round ahead
+        uint32_t j = h0 + threadIdx.x;
+        R r = j < h1 ? srec[j - h0] : R{};
+        uint32_t pv = j < h1 ? dst.pre(r) : 0u;
+        for (uint32_t j0 = h0; j0 < h1; j0 += T, j += T) {
+          const uint32_t jn = j + T;
+          const R rn = jn < h1 ? srec[jn - h0] : R{};
+          const uint32_t pn = jn < h1 ? dst.pre(rn) : 0u;
+          if (j < h1) {
+            const uint32_t d = (src.key(r) >> shift) & (RADIX - 1);
+            dst.store(gpos[d] + (j - lbase[d]), r, pv);
+          }
+          r = rn;
+          pv = pn;
         }
-        if (Dst::kWave) dst.wave(r, live);
+      } else {
+        for (uint32_t j0 = h0; j0 < h1; j0 += T) {  // wave-uniform trip count (Dst::wave)
+          const uint32_t j = j0 + threadIdx.x;
+          const bool live = j < h1;
+          const R r = live ? srec[j - h0] : R{};
+          if (live) {
+            const uint32_t d = (src.key(r) >> shift) & (RADIX - 1);
+            dst.store(gpos[d] + (j - lbase[d]), r);
+          }
+          if (Dst::kWave) dst.wave(r, live);
+        }
       }
     }
     if (trace && threadIdx.x == 0) {  // RK_NW_TRACE: phase timestamps of this tile
