@@ -490,17 +490,23 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   rk::nw_x_count(w.Ra, m, cc, st);
   rk::exclusive_scan_u32(w.xcnt, w.xoff, (size_t)3 * cc.nch + 1, ss, st);
   HIPCHK(ctx, hipGetLastError());
-  // the Y axis sorts on the second stream while the X axis is built and resolved
-  // (RK_Y_SERIAL=1: on the main stream, before it)
-  static const bool y_serial = [] {
-    const char *e = getenv("RK_Y_SERIAL");
+  // The Y axis is sorted once X is resolved (default): its first pass reads
+  // each record's X-hit bit in processing order and the last writes the Y
+  // states from it -- no per-record lookup, and no record pass shares the
+  // device with the X sweeps.  RK_Y_OVERLAP=1: the earlier schedule, every Y
+  // pass but the last on the second stream beside the X axis, the last one
+  // looking up the X-hit bits (cfg3 11.0 ms against 11.2 with those passes
+  // serial before X).
+  static const bool y_overlap = [] {
+    const char *e = getenv("RK_Y_OVERLAP");
     return e && e[0] == '1';
   }();
-  const hipStream_t sty = y_serial ? st : st2;
-  HIPCHK(ctx, hipEventRecord(ctx->fork, st));
-  HIPCHK(ctx, hipStreamWaitEvent(sty, ctx->fork, 0));
-  rk::nw_y_sort_head(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, sty);
-  HIPCHK(ctx, hipEventRecord(ctx->join, sty));
+  if (y_overlap) {
+    HIPCHK(ctx, hipEventRecord(ctx->fork, st));
+    HIPCHK(ctx, hipStreamWaitEvent(st2, ctx->fork, 0));
+    rk::nw_y_sort_head(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, st2);
+    HIPCHK(ctx, hipEventRecord(ctx->join, st2));
+  }
   mark(ctx, RK_PH_GATHER);
   rk::nw_x_chunks(w.Ra, m, pl.nbx, pl.max_x, maxlen, w.xoff, w.cx, w.xpos, w.erec, w.ctrl, cc.W,
                   st);
@@ -523,11 +529,14 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     ctx->stats.x_sweeps = sweeps;
     if (prof) mark(ctx, RK_PH_SWEEP_Y);
     rk::nw_x_bits(w.xpos, w.cx.state, m, w.xbits, st);
-    if (q == 0) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
-    if (q == 0)  // the Y sort's last pass writes the CSR and the Y states
+    if (q == 0 && y_overlap) {  // the Y sort's last pass writes the CSR and the Y states
+      HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
       rk::nw_y_sort_tail(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y,
                          w.xbits, st);
-    else  // later ratio pairs: the same CSR, new X results
+    } else if (q == 0) {
+      rk::nw_y_sort_after_x(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y,
+                            w.xbits, st);
+    } else  // later ratio pairs: the same CSR, new X results
       rk::nw_fill_y(w.cy.ent, w.xbits, w.cy.state, m, st);
     rk::Axis ay{w.cy.key, w.cy.ent, nullptr, nullptr, w.cy.state, nullptr, w.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,

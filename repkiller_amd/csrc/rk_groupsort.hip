@@ -149,6 +149,189 @@ __device__ void heap_sort_segment(const V &v, uint32_t f, uint32_t l) {
     for (uint32_t x = f; x < l; ++x) v.B[x] = 2;
 }
 
+// ---------------------------------------------------------------------------
+// __partial_sort(first, last, last) of a LARGE segment (its depth budget spent:
+// a median-of-three killer, never ordinary data), one 256-thread block:
+//  * __make_heap calls __adjust_heap for the parents (len-2)/2 down to 0; a
+//    call touches only its own subtree and every deeper level comes first, so
+//    the calls of one level run in parallel, level after level;
+//  * __sort_heap by wavefront 0, the heap's top HLV levels kept in LDS.  A
+//    pop's __adjust_heap descent (the larger child -- the right one unless
+//    right < left --, down while the hole has two children, then a lone left
+//    child) is found up to HR levels at a time: lanes load the 2^(HR+1) - 2
+//    nodes below the hole (two per lane), each right child compares with its
+//    left sibling (one xor shuffle), one ballot holds every direction and the
+//    path follows in scalar steps.  __push_heap of the displaced value then
+//    needs no loads: the path's keys descend, so the value rises past exactly
+//    the path keys below it (a ballot count), and only the path positions
+//    above its slot are written.
+constexpr uint32_t HEAP_BLOCK_MIN = 2048;  // smaller exhausted segments: one thread
+constexpr int HLV = 13;                    // heap levels in LDS
+constexpr uint32_t HTOP = (1u << HLV) - 1;
+constexpr int HR = 6;                      // levels per descent round (126 nodes)
+constexpr uint32_t HR_LAST = (1u << HR) - 2, HR_NODES = (2u << HR) - 2;  // 62, 126
+static_assert(HR_NODES <= 128, "two logical nodes per lane");
+constexpr int HRMAX = 6;                   // rounds per pop (heaps below 2^36 nodes)
+
+struct HeapMem {  // node x: LDS below HTOP, else the segment in global memory
+  uint64_t *K;
+  uint32_t *T;
+  uint64_t *lk;
+  uint32_t *lt;
+  __device__ __forceinline__ uint64_t key(uint32_t x) const { return x < HTOP ? lk[x] : K[x]; }
+  __device__ __forceinline__ uint32_t tag(uint32_t x) const { return x < HTOP ? lt[x] : T[x]; }
+  __device__ __forceinline__ void put(uint32_t x, uint64_t k, uint32_t t) const {
+    if (x < HTOP) lk[x] = k, lt[x] = t;
+    else K[x] = k, T[x] = t;
+  }
+};
+
+// __sort_heap of [0, n) by one wavefront (lane = 0..63)
+__device__ void wave_sort_heap(const HeapMem &h, uint32_t n, uint32_t lane) {
+  for (uint32_t last = n - 1; last > 0; --last) {
+    // __pop_heap: the root moves to `last`, the value there is re-inserted
+    const uint64_t vk = h.key(last);
+    const uint32_t vt = h.tag(last);
+    const uint64_t rk = h.key(0);
+    const uint32_t rt = h.tag(0);
+    if (lane == 0) h.put(last, rk, rt);
+    const uint32_t len = last;
+    const uint32_t two_lim = (len - 1) / 2;  // hole x has two children iff x < two_lim
+    // descent rounds: per round, the path's nodes among the loaded ones
+    uint64_t pm0[HRMAX], pm1[HRMAX];  // path masks: logical node c in round r (c < 64 / >= 64)
+    uint64_t k0[HRMAX], k1[HRMAX];    // keys of this lane's two logical nodes
+    uint32_t t0[HRMAX], t1[HRMAX];
+    uint32_t x0[HRMAX], x1[HRMAX];    // their heap positions
+    uint32_t hole = 0;
+    int rounds = 0;
+    bool more = true;
+#pragma unroll
+    for (int r = 0; r < HRMAX; ++r) {
+      pm0[r] = pm1[r] = 0;
+      k0[r] = k1[r] = 0;
+      t0[r] = t1[r] = 0;
+      x0[r] = x1[r] = 0;
+      if (!more) continue;
+      ++rounds;
+      // logical node c (0..125): depth d = log2(c + 2) below the hole, offset
+      // o = c + 2 - 2^d: heap position (hole + 1) 2^d - 1 + o
+      uint64_t kk[2];
+      uint32_t tt[2], xx[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t c = lane + 64 * s;
+        const int d = 31 - __clz((int)(c + 2));
+        const uint64_t pos = ((uint64_t)hole + 1) * (1ull << d) - 1 + (c + 2 - (1u << d));
+        const bool in = c < HR_NODES && pos < len;
+        xx[s] = in ? (uint32_t)pos : 0u;
+        kk[s] = in ? h.key((uint32_t)pos) : 0ull;
+        tt[s] = in ? h.tag((uint32_t)pos) : 0u;
+      }
+      // right children (odd c) against their left siblings: ties go right
+      uint64_t dir[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t lo = (uint32_t)kk[s], hi = (uint32_t)(kk[s] >> 32);
+        const uint64_t sib = (uint64_t)(uint32_t)__shfl_xor((int)hi, 1) << 32 |
+                             (uint32_t)__shfl_xor((int)lo, 1);
+        dir[s] = __ballot((lane & 1) && !(kk[s] < sib));
+      }
+      // the walk (scalar): internal node J (0 = the hole, else logical node
+      // J - 1) has children c = 2J, 2J + 1
+      uint32_t J = 0, x = hole;
+      more = false;
+      for (;;) {
+        if (x >= two_lim) {  // no second child: a lone left child ends the descent
+          if ((len & 1) == 0 && x == (len - 2) / 2) {
+            const uint32_t c = 2 * J;
+            if (c < 64) pm0[r] |= 1ull << c;
+            else pm1[r] |= 1ull << (c - 64);
+          }
+          break;
+        }
+        const uint32_t cr = 2 * J + 1;
+        const bool right = ((cr < 64 ? dir[0] >> cr : dir[1] >> (cr - 64)) & 1ull) != 0;
+        const uint32_t c = right ? cr : cr - 1;
+        if (c < 64) pm0[r] |= 1ull << c;
+        else pm1[r] |= 1ull << (c - 64);
+        x = 2 * x + (right ? 2 : 1);
+        if (c >= HR_LAST) {  // the round's last level: the next round starts below x
+          hole = x;
+          more = true;
+          break;
+        }
+        J = c + 1;
+      }
+      k0[r] = kk[0], k1[r] = kk[1];
+      t0[r] = tt[0], t1[r] = tt[1];
+      x0[r] = xx[0], x1[r] = xx[1];
+    }
+    // __push_heap: the value rises past the path keys below it (a suffix)
+    uint32_t D = 0, below = 0;
+#pragma unroll
+    for (int r = 0; r < HRMAX; ++r) {
+      if (r >= rounds) break;
+      D += __popcll(pm0[r]) + __popcll(pm1[r]);
+      below += __popcll(__ballot(((pm0[r] >> lane) & 1) && k0[r] < vk)) +
+               __popcll(__ballot(((pm1[r] >> lane) & 1) && k1[r] < vk));
+    }
+    const uint32_t j = D - below;  // the value's slot is path position j (0: the root)
+    // path position p (1-based) of every path node: its key moves to its
+    // parent when p <= j, and the value lands at position j
+    uint32_t before = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < HRMAX; ++r) {
+      if (r >= rounds) break;
+      const bool on0 = (pm0[r] >> lane) & 1, on1 = (pm1[r] >> lane) & 1;
+      const uint32_t p0 = before + __popcll(pm0[r] & lt) + 1;
+      const uint32_t p1 = before + __popcll(pm0[r]) + __popcll(pm1[r] & lt) + 1;
+      if (on0 && p0 <= j) {
+        h.put((x0[r] - 1) / 2, k0[r], t0[r]);
+        if (p0 == j) h.put(x0[r], vk, vt);
+      }
+      if (on1 && p1 <= j) {
+        h.put((x1[r] - 1) / 2, k1[r], t1[r]);
+        if (p1 == j) h.put(x1[r], vk, vt);
+      }
+      before += __popcll(pm0[r]) + __popcll(pm1[r]);
+    }
+    if (j == 0 && lane == 0) h.put(0, vk, vt);
+    // the next pop reads what this one wrote (LDS and this CU's global lines)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  }
+}
+
+// The whole __partial_sort of segment [0, n) of K/T (global memory) by one
+// 256-thread block; its final tags go to out[0..n).
+__device__ void block_heap_sort(uint64_t *K, uint32_t *T, uint32_t n, uint32_t *out, uint64_t *lk,
+                                uint32_t *lt) {
+  const uint32_t tid = threadIdx.x;
+  if (n < 2) {
+    for (uint32_t x = tid; x < n; x += blockDim.x) out[x] = T[x];
+    __syncthreads();
+    return;
+  }
+  {
+    const uint32_t last_parent = (n - 2) / 2;
+    for (int lv = 31 - __clz((int)(last_parent + 1)); lv >= 0; --lv) {
+      const uint32_t a = (1u << lv) - 1;
+      const uint32_t e = min((1u << (lv + 1)) - 2, last_parent);
+      for (uint32_t x = a + tid; x <= e; x += blockDim.x)
+        adjust_heap(GView{K, T, nullptr, nullptr, nullptr}, 0, x, n, K[x], T[x]);
+      __syncthreads();
+    }
+    for (uint32_t x = tid; x < n && x < HTOP; x += blockDim.x) lk[x] = K[x], lt[x] = T[x];
+    __syncthreads();
+    if (tid < 64) wave_sort_heap(HeapMem{K, T, lk, lt}, n, tid);
+    __syncthreads();
+  }
+  for (uint32_t x = tid; x < n; x += blockDim.x) out[x] = x < HTOP ? lt[x] : T[x];
+  __syncthreads();
+}
+
 // cross-lane moves: pull from lane `src` (ds_bpermute) / push to lane `dst`
 // (ds_permute; the destinations must form a permutation)
 __device__ __forceinline__ uint32_t pull(int src, uint32_t v) {
@@ -682,11 +865,20 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
   return cut;
 }
 
+// Depth-exhausted segments of at least HEAP_BLOCK_MIN members found by phase
+// A, heap-sorted afterwards by k_heap_segments (one block each, its LDS holding
+// the heap's top levels)
+struct HeapSeg {
+  uint32_t b, f, n, pad;
+};
+constexpr uint32_t HEAPQ_CAP = 512;
+
 __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tier,
                                                            const uint32_t *goff, uint64_t *key,
                                                            uint32_t *tag, uint32_t *otag,
                                                            uint32_t *pl, uint32_t *pr,
-                                                           uint8_t *bnd) {
+                                                           uint8_t *bnd, uint32_t *heapq_n,
+                                                           HeapSeg *heapq) {
   __shared__ Frame stack[SPLIT_STACK];
   __shared__ uint32_t s_w[16];
   const uint32_t tid = threadIdx.x;
@@ -714,6 +906,17 @@ __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tie
           break;
         }
         if (d == 0) {  // __partial_sort fallback on a large segment
+          if (l - f >= HEAP_BLOCK_MIN) {  // queued for k_heap_segments
+            if (tid == 0) {
+              const uint32_t i = atomicAdd(heapq_n, 1u);
+              s_w[10] = i < HEAPQ_CAP;
+              if (i < HEAPQ_CAP) heapq[i] = HeapSeg{b, f, l - f, 0u};
+            }
+            __syncthreads();
+            const bool queued = s_w[10] != 0;
+            __syncthreads();
+            if (queued) break;
+          }
           if (tid == 0) heap_sort_segment(GView{K, T, nullptr, nullptr, nullptr}, f, l);
           __syncthreads();
           for (uint32_t x = f + tid; x < l; x += 256) otag[b + x] = T[x];
@@ -728,6 +931,19 @@ __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tie
       }
     }
     __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_heap_segments(const uint32_t *heapq_n,
+                                                       const HeapSeg *heapq, uint64_t *key,
+                                                       uint32_t *tag, uint32_t *otag) {
+  __shared__ uint64_t lk[HTOP];
+  __shared__ uint32_t lt[HTOP];
+  const uint32_t cnt = min(*heapq_n, HEAPQ_CAP);
+  for (uint32_t s = blockIdx.x; s < cnt; s += gridDim.x) {
+    const HeapSeg g = heapq[s];
+    const size_t o = (size_t)g.b + g.f;
+    block_heap_sort(key + o, tag + o, g.n, otag + o, lk, lt);
   }
 }
 
@@ -921,7 +1137,8 @@ size_t groupsort_scratch_bytes(uint32_t n) {
   // pl, pr (stopper lists; segment heads); tier lists; bounds; block counts
   // (+ scan), block members
   return (size_t)n * 4 * 2 + ((size_t)n + 1) * 4 + (size_t)n + 128 +
-         (nblk * NTIER + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + 256;
+         (nblk * NTIER + 1) * 4 * 2 + nblk * NTIER * 4 + 256 + 256 +
+         (HEAPQ_CAP + 1) * sizeof(HeapSeg) + 64;
 }
 
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
@@ -944,6 +1161,9 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
       (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
   uint32_t *boff = bc + (size_t)NL * nblk + 1;
   uint32_t *bm = boff + (size_t)NL * nblk + 1;
+  HeapSeg *heapq = reinterpret_cast<HeapSeg *>(
+      (reinterpret_cast<uintptr_t>(bm + (size_t)NL * nblk) + 63) & ~(uintptr_t)63);
+  uint32_t *heapq_n = reinterpret_cast<uint32_t *>(heapq + HEAPQ_CAP);
   const bool timing = g_ktimer != nullptr;
   if (timing) {
     g_ktimer->tier_nblk = nblk;
@@ -1052,10 +1272,13 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   // phase A marks the final segments' starts in bnd (cleared first); both
   // kernels return at once when no group is that large
   k_clear_if_tier<<<1024, 256, 0, st>>>(tl, NTIER - 1, bnd, m);
+  (void)hipMemsetAsync(heapq_n, 0, 4, st);
   kt_begin(st);
-  k_sort_groups_split<<<2048, 256, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd);
+  k_sort_groups_split<<<2048, 256, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
+                                            heapq_n, heapq);
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
+  k_heap_segments<<<64, 256, 0, st>>>(heapq_n, heapq, key, tag, otag);
   kt_begin(st);
   if (narrow_keys)
     k_sort_segments<uint32_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 4), st>>>(

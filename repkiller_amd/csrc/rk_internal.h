@@ -263,6 +263,11 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
                     const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
                     uint64_t max_y, const uint32_t *xbits, hipStream_t st,
                     bool arrival_ids = false, const uint4 *src0 = nullptr);
+// the whole Y sort once the X axis is resolved: the X-hit bits (by processing
+// index) ride in the records from the first pass; the last writes CSR + states
+void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
+                       const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
+                       uint64_t max_y, const uint32_t *xbits, hipStream_t st);
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
                  const uint32_t *xoff, Csr cx, uint32_t *xpos, uint4 *erec, uint32_t *ctrl,
                  uint32_t W, hipStream_t st, const uint4 *halo = nullptr, uint32_t G = 0);

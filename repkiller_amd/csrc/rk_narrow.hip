@@ -296,17 +296,33 @@ struct DstCsr {
   __device__ __forceinline__ uint32_t pre(const uint3 &r) const {
     return xbits ? xbits[r.y >> 5] : 0u;
   }
+  bool hit_bit;  // the X-hit bit travels in bit 31 of the record (SrcYX12): no lookup
   __device__ __forceinline__ void store(uint32_t pos, const uint3 &r, uint32_t xw) const {
     key[pos] = r.x;
     ent[pos] = r.y;
     const uint32_t b = r.x >= nb ? r.x - nb : r.x;
-    const uint64_t c = (uint64_t)b * 100 + (r.z >> 24);  // centre = bucket * 100 + remainder
+    const uint64_t c = (uint64_t)b * 100 + ((r.z >> 24) & 0x7Fu);  // bucket * 100 + remainder
     pk[pos] = make_uint2((uint32_t)c, r.z & 0xFFFFFFu);
     nbd[pos] = nbd_code_nw(c, max_index);
-    // with the X results (bitmask by processing index): the Y states -- X hits
-    // sit in the Y lists (commonFunctions.cpp:59), X misses query them
-    if (xbits) state[pos] = (xw >> (r.y & 31)) & 1u ? ST_ACTIVE : ST_UNKNOWN;
+    // with the X results: the Y states -- X hits sit in the Y lists
+    // (commonFunctions.cpp:59), X misses query them
+    if (hit_bit) state[pos] = (r.z >> 31) ? ST_ACTIVE : ST_UNKNOWN;
+    else if (xbits) state[pos] = (xw >> (r.y & 31)) & 1u ? ST_ACTIVE : ST_UNKNOWN;
   }
+};
+// the Y records in processing order with their fragment's X-hit bit (bitmask
+// by processing index, read sequentially) in bit 31 of the third word
+struct SrcYX12 {
+  using rec_t = uint3;
+  const uint3 *in;
+  const uint32_t *xbits;
+  __device__ __forceinline__ uint3 load(uint32_t i) const {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
+    const uint32_t y = __builtin_nontemporal_load(p + 1);
+    const uint32_t hit = (xbits[y >> 5] >> (y & 31)) & 1u;
+    return make_uint3(__builtin_nontemporal_load(p), y, __builtin_nontemporal_load(p + 2) | hit << 31);
+  }
+  __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
 };
 
 // --- group members, last pass: gid order (stable: processing order inside) -
@@ -1050,7 +1066,7 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
   const PassStatus ps = pass_status(status, m, D, 12);
   ps.prepare(p, m, D, st);  // a no-op after the head's clear-ahead
   if (p == 0) (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);
-  const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, xbits, cy.state};
+  const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, xbits, cy.state, false};
   const double bytes = 12.0 * m + 17.0 * m + (xbits ? 5.0 * m : 0.0);
   if (p == 0 && arrival_ids)
     launch_pass(SrcIdx12{src}, dc, m, D.shift[p], D.db[p], ghist_of(yhist, p), ps.use(p),
@@ -1058,6 +1074,40 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
   else
     launch_pass(SrcRec12{src}, dc, m, D.shift[p], D.db[p], ghist_of(yhist, p), ps.use(p),
                 status + sw - 64 + p, st, bytes);
+}
+
+// The Y axis sort after the X axis is resolved (one device): the first pass
+// reads the Y records in processing order together with their X-hit bits
+// (sequential bitmask words) and carries the bit in the records, so the last
+// pass writes the Y states from it instead of looking it up per record
+void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
+                       const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
+                       uint64_t max_y, const uint32_t *xbits, hipStream_t st) {
+  const Digits D = to_digits(y);
+  const size_t sw = nw_status_words(m);
+  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  const PassStatus ps = pass_status(status, m, D, 12);
+  const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, nullptr, cy.state, true};
+  const uint3 *src = reinterpret_cast<const uint3 *>(yrec);
+  for (int p = 0; p < D.passes; ++p) {
+    ps.prepare(p, m, D, st);
+    const bool last = p == D.passes - 1;
+    uint3 *out = reinterpret_cast<uint3 *>(p % 2 == 0 ? tmp : const_cast<uint4 *>(yrec));
+    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes), *ctr = status + sw - 64 + p;
+    const uint32_t *gh = ghist_of(yhist, p);
+    const double bytes = (p == 0 ? 12.0 + 0.125 : 12.0) * m + (last ? 18.0 : 12.0) * m;
+    if (p == 0 && last)
+      launch_pass(SrcYX12{src, xbits}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else if (p == 0)
+      launch_pass(SrcYX12{src, xbits}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
+                  bytes, nxt);
+    else if (last)
+      launch_pass(SrcRec12{src}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else
+      launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes,
+                  nxt);
+    src = out;
+  }
 }
 
 // The member sort by gid: 12-B records {gid, row, key} when every sort key

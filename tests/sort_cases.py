@@ -65,6 +65,20 @@ def mcilroy_killer(n: int) -> np.ndarray:
     return np.array(val, np.uint64)
 
 
+def killer_with_keys(n: int, span: int, seed: int, base: int = 0) -> np.ndarray:
+    """A median-of-3 killer whose never-compared ("gas") items get keys of
+    their own: uniform in [gas + 1, gas + span], all above the solid ones, so
+    every comparison the introsort made before its depth limit keeps its
+    outcome (same partitions, same heapsort segment) while the heapsort then
+    orders varied keys (span 1: all equal; 3: heavy ties; 2^40: distinct).
+    `base` is added to every key (base >= 2^32: 64-bit keys)."""
+    k = mcilroy_killer(n).astype(np.uint64)
+    gas = k == n
+    rng = np.random.default_rng(seed)
+    k[gas] = np.uint64(n + 1) + rng.integers(0, span, int(gas.sum())).astype(np.uint64)
+    return k + np.uint64(base)
+
+
 def heap_fallbacks(keys: np.ndarray) -> int:
     k = [int(v) for v in keys]
     return _introsort_trace(len(k), lambda x, y: k[x] < k[y])

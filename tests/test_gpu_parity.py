@@ -313,6 +313,26 @@ def test_std_sort_large_segments_vs_restatement(gpu_ctx):
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
 
 
+def test_std_sort_block_heapsort_vs_restatement(gpu_ctx):
+    """The depth-limit heapsort of large segments (one block per segment, the
+    heap's top levels in LDS, the pops' descents 6 levels per round): killers
+    whose heapsort segment is just above the block threshold, straddles the
+    LDS-resident levels or spans 17 levels, over all-equal, heavily tied and
+    distinct keys, 32- and 64-bit."""
+    from sort_cases import heap_fallbacks, killer_with_keys
+    segs = [killer_with_keys(2300, 1, 1), killer_with_keys(2300, 3, 2),
+            killer_with_keys(8400, 3, 3), killer_with_keys(8400, 1 << 40, 4),
+            killer_with_keys(20000, 5, 5, base=1 << 40), killer_with_keys(70000, 1 << 20, 6)]
+    for s in segs:
+        assert heap_fallbacks(s) > 0
+    keys = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
+    perm = gpu_ctx.std_sort_segments(keys, off)
+    for a, b, s in zip(off[:-1], off[1:], segs):
+        want = ro.std_sort(s) + a
+        assert np.array_equal(perm[a:b], want), (int(a), s.size)
+
+
 def test_pipeline_choice(gpu_ctx, generic_ctx):
     """The record pipeline runs on the BASELINE-shaped sets; inputs it cannot
     represent (a length >= 2^24) take the generic one with the same result."""
