@@ -297,10 +297,10 @@ __device__ void wave_sort_heap(const HeapMem &h, uint32_t n, uint32_t lane) {
       before += __popcll(pm0[r]) + __popcll(pm1[r]);
     }
     if (j == 0 && lane == 0) h.put(0, vk, vt);
-    // the next pop reads what this one wrote (LDS and this CU's global lines)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    // the next pop reads what this one wrote: one wavefront's LDS and global
+    // accesses are performed in order, so a wavefront-scope fence (no wait
+    // for the stores' completion) keeps the compiler from reordering them
+    wave_sync();
   }
 }
 

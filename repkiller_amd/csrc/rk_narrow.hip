@@ -310,17 +310,22 @@ struct DstCsr {
     else if (xbits) state[pos] = (xw >> (r.y & 31)) & 1u ? ST_ACTIVE : ST_UNKNOWN;
   }
 };
-// the Y records in processing order with their fragment's X-hit bit (bitmask
-// by processing index, read sequentially) in bit 31 of the third word
+// the Y records in processing order with their fragment's X-hit bit in bit
+// 31 of the third word.  Record i is fragment i (DstProc, one device), and a
+// wave loads 64 consecutive records from a multiple of 64 (k_onesweep's
+// layout: the tile and every wave's slice are multiples of 64 records), so
+// the wave's 64 bits are one uniform 8-B load
 struct SrcYX12 {
   using rec_t = uint3;
   const uint3 *in;
-  const uint32_t *xbits;
+  const uint64_t *xbits64;
   __device__ __forceinline__ uint3 load(uint32_t i) const {
     const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
-    const uint32_t y = __builtin_nontemporal_load(p + 1);
-    const uint32_t hit = (xbits[y >> 5] >> (y & 31)) & 1u;
-    return make_uint3(__builtin_nontemporal_load(p), y, __builtin_nontemporal_load(p + 2) | hit << 31);
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane(i) & ~63u;
+    const uint64_t w = xbits64[i0 >> 6];
+    const uint32_t hit = (uint32_t)(w >> (i - i0)) & 1u;
+    return make_uint3(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
+                      __builtin_nontemporal_load(p + 2) | hit << 31);
   }
   __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
 };
@@ -730,6 +735,8 @@ constexpr int OS_T = 256;
 #ifndef RK_NW_ITEMS12
 #define RK_NW_ITEMS12 14
 #endif
+// SrcYX12: a wave's slice of a tile starts at a multiple of 64 records
+static_assert(512 * RK_NW_ITEMS12 % 64 == 0 && 512 * 12 % 64 == 0, "waves load from multiples of 64");
 int nw_shape();
 // records per tile of a pass with DB-bit digits over rec_bytes-B records (the
 // shape of launch_pass_db)
@@ -1097,9 +1104,9 @@ void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits
     const uint32_t *gh = ghist_of(yhist, p);
     const double bytes = (p == 0 ? 12.0 + 0.125 : 12.0) * m + (last ? 18.0 : 12.0) * m;
     if (p == 0 && last)
-      launch_pass(SrcYX12{src, xbits}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+      launch_pass(SrcYX12{src, reinterpret_cast<const uint64_t *>(xbits)}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
     else if (p == 0)
-      launch_pass(SrcYX12{src, xbits}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
+      launch_pass(SrcYX12{src, reinterpret_cast<const uint64_t *>(xbits)}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
                   bytes, nxt);
     else if (last)
       launch_pass(SrcRec12{src}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
