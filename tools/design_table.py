@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Regenerate DESIGN.md's kernel table from profiles/r2_bench.json (HIP-event
-timing inside bench.py's timed steps, cfg3, two streams), profiles/traffic.json
+"""Regenerate DESIGN.md's kernel table from profiles/r3_bench.json (HIP-event
+timing inside bench.py's timed steps, cfg3), profiles/traffic.json
 (PMC HBM bytes, cfg3) and profiles/r2_bench_cfg5.json (the same timing at cfg5,
 one GPU) when present."""
 import json
@@ -8,17 +8,17 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
-BENCH, CFG5 = "r2_bench.json", "r2_bench_cfg5.json"
+BENCH, CFG5 = "r3_bench.json", "r2_bench_cfg5.json"
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
-    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (4 processing-order passes, 8 + 7 + 7 + 7-bit digits at cfg3), 12-B records 7168 per tile (3 Y passes with 9-bit digits, 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last order pass: 57)"),
+    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (4 processing-order passes, 8 + 7 + 7 + 7-bit digits at cfg3), 12-B records 7168 per tile (3 Y passes, 9 + 9 + 8 bits, after X: the first carries the X-hit bits, the last writes CSR + states; 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last order pass: 57; last Y pass: 30)"),
     ("k_nw_xcount", "entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
     ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "50"),
     ("k_sweep_fast", "occupancy decisions, first sweep: a wavefront per 64-position window, ballot rounds, 32-bit candidate tests", "26"),
     ("k_sweep_fast_more", "later sweeps: one wavefront per 64 windows handles the still-pending ones", "-"),
     ("k_sweep_long32", "runs of more than 64 entries, 64 entries at a time against LDS lists", "-"),
-    ("k_nw_x_bits", "X hits as a bitmask by processing index (ballots over the X states at each fragment's X position)", "5"),
-    ("k_nw_fill_y", "Y states from the bitmask (X hits sit in the Y lists)", "5"),
+    ("k_nw_x_bits", "X hits as a bitmask by processing index (ballots over the X states at each fragment's X position), read in order by the first Y pass", "5"),
+    ("k_nw_fill_y", "Y states from the bitmask for later ratio pairs (X hits sit in the Y lists)", "5"),
     ("k_jump", "chase parent chains to the root", "16"),
     ("k_nw_assign", "gid from the root's rank into each member record; member-sort histograms", "12"),
     ("k_group_offsets", "group bounds", "4"),
@@ -27,6 +27,7 @@ JOBS = [
     ("k_sort_groups_lds", "65..2048 members in LDS: partitions down to the leaves, then the final insertion pass with ballot-found leaf bounds (257..2048: second stream, first)", "16 per member"),
     ("k_sort_groups_split", "groups above 2048: block-wide partitions down to 512-member segments", "16 per member"),
     ("k_sort_segments", "those segments, one LDS wavefront each", "16 per member"),
+    ("k_heap_segments", "depth-exhausted segments of >= 2048 members (median-of-3 killers only): make_heap level-parallel, sort_heap by one wavefront, top 13 heap levels in LDS", "-"),
     ("k_emit", "gid, flag, output order", "29"),
 ]
 
