@@ -432,7 +432,7 @@ bool record_pipeline_enabled() {
 }
 
 int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, uint32_t npairs,
-                    rk_result *outs, const Plan &pl, bool *fallback) {
+                    rk_result *outs, const Plan &pl, bool *fallback, const uint3 *wire) {
   *fallback = false;
   const uint32_t n = (uint32_t)pl.n;
   NWork w{};
@@ -456,7 +456,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   HIPCHK(ctx, hipMemsetAsync(w.ahist, 0, 3 * 4096 * sizeof(uint32_t), st));
   mark(ctx, RK_PH_PREP);
   rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, ad, yd, w.ahist, w.yhist, w.ctrl,
-                    st);
+                    st, wire);
   HIPCHK(ctx, hipGetLastError());
   if ((rc = readback(ctx, w.ctrl, 9))) return rc;
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
@@ -486,7 +486,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   cc.nch = rk::nw_chunks(pl.nbx, cc.W);
   cc.cnts = w.xcnt;
   mark(ctx, RK_PH_ORDER);
-  rk::nw_order_sort(*in, pl.vsize, pl.nby, ad, w.ahist, w.astatus, w.Ra, w.Rb, w.yrec, st);
+  rk::nw_order_sort(*in, pl.vsize, pl.nby, ad, w.ahist, w.astatus, w.Ra, w.Rb, w.yrec, st, wire);
   rk::nw_x_count(w.Ra, m, cc, st);
   rk::exclusive_scan_u32(w.xcnt, w.xoff, (size_t)3 * cc.nch + 1, ss, st);
   HIPCHK(ctx, hipGetLastError());
@@ -612,8 +612,16 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
 // every (len_ratio, pos_ratio) pair runs the sweeps, groups and in-group order
 // (repkiller.cpp:60-72 runs each pair through the whole path).  Phase
 // profiling covers the shared part and the first pair.
+// The record pipeline takes this input (and the generic one is not forced).
+bool record_eligible(const rk_ctx *ctx, uint64_t n) {
+  return ctx->pipeline == RK_PIPELINE_AUTO && record_pipeline_enabled() && n > 0 &&
+         n < (1ull << 30);
+}
+
+// wire: the rows as 12-B wire records in HBM (rk_classify's compact upload,
+// rk_io.hip); only in->n is read then, and the input must be record-eligible
 int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, uint32_t npairs,
-                    rk_result *outs) {
+                    rk_result *outs, const uint3 *wire = nullptr) {
   if (!ctx || !in || !prms || !outs || npairs == 0) return RK_E_ARG;
   if (in->n >= 0xFFFFFFFFull) return RK_E_TOO_MANY;
   for (uint32_t q = 0; q < npairs; ++q) {
@@ -628,7 +636,12 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     }
     if (in->n && (!outs[q].gid || !outs[q].repval || !outs[q].out_order)) return RK_E_ARG;
   }
-  if (in->n && (!in->x_start || !in->y_start || !in->length || !in->strand)) return RK_E_ARG;
+  if (in->n && !wire && (!in->x_start || !in->y_start || !in->length || !in->strand))
+    return RK_E_ARG;
+  if (wire && !record_eligible(ctx, in->n)) {
+    ctx->err = "wire rows need the record pipeline";
+    return RK_E_INTERNAL;
+  }
   HIPCHK(ctx, hipSetDevice(ctx->device));
   std::memset(&ctx->stats, 0, sizeof ctx->stats);
   hipStream_t st = ctx->stream;
@@ -648,11 +661,14 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   pl.nbx = (uint32_t)(pl.max_x + 1);
   pl.nby = (uint32_t)(pl.max_y + 1);
   int rc;
-  if (ctx->pipeline == RK_PIPELINE_AUTO && record_pipeline_enabled() && pl.n > 0 &&
-      pl.n < (1ull << 30)) {
+  if (record_eligible(ctx, pl.n)) {
     bool fallback = false;
-    rc = classify_narrow(ctx, in, prms, npairs, outs, pl, &fallback);
+    rc = classify_narrow(ctx, in, prms, npairs, outs, pl, &fallback, wire);
     if (rc || !fallback) return rc;
+    if (wire) {  // wire rows always pack (checked on the host)
+      ctx->err = "wire rows did not pack";
+      return RK_E_INTERNAL;
+    }
     // the generic pipeline needs its own ~200 B per row: give the HBM back
     (void)hipStreamSynchronize(ctx->stream2);
     (void)hipFree(ctx->ws_nw);
@@ -1008,6 +1024,54 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
   return rc;
 }
 
+// rk_classify through the compact wire format; RK_WIRE_UNPACKABLE when some
+// row does not fit a wire record (nothing was classified: the caller uploads
+// the SoA columns instead)
+constexpr int RK_WIRE_UNPACKABLE = 1 << 20;
+static int classify_wire(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p, uint32_t npairs,
+                         rk_result *out) {
+  const size_t n = in->n;
+  const size_t need = align_up(n * 12 + 16) +
+                      (size_t)npairs * (align_up(n + 16) + align_up(n * 4 + 16) * 2);
+  if (need > ctx->io_cap) {
+    if (ctx->io) (void)hipFree(ctx->io);
+    ctx->io = nullptr;
+    ctx->io_cap = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->io, need));
+    ctx->io_cap = need;
+  }
+  Carve c{(char *)ctx->io};
+  uint3 *rows = c.take<uint3>(n);
+  std::vector<rk_result> dres(npairs);
+  for (uint32_t q = 0; q < npairs; ++q) {
+    uint8_t *drep = c.take<uint8_t>(n);
+    uint32_t *dgid = c.take<uint32_t>(n), *dord = c.take<uint32_t>(n);
+    dres[q] = rk_result{dord, dgid, drep, 0, 0};
+  }
+  const double t0 = rk::wall_ms();
+  int rc = rk::io_h2d_rows(ctx, *in, rows);
+  if (rc) return rc == 1 ? RK_WIRE_UNPACKABLE : rc;
+  const double t1 = rk::wall_ms();
+  const rk_frags_soa din{nullptr, nullptr, nullptr, nullptr, n};
+  rc = classify_device(ctx, &din, p, npairs, dres.data(), rows);
+  if (rc) return rc;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const double t2 = rk::wall_ms();
+  std::vector<rk::IoPiece> down;
+  for (uint32_t q = 0; q < npairs; ++q) {
+    out[q].n_out = dres[q].n_out;
+    out[q].n_groups = dres[q].n_groups;
+    down.push_back({out[q].out_order, dres[q].out_order, dres[q].n_out * 4});
+    down.push_back({out[q].repval, dres[q].repval, dres[q].n_out});
+  }
+  if ((rc = rk::io_d2h(ctx, down))) return rc;
+  for (uint32_t q = 0; q < npairs; ++q)
+    rk::gids_from_flags(ctx, out[q].repval, out[q].n_out, out[q].gid);
+  ctx->stats.h2d_ms = t1 - t0;
+  ctx->stats.d2h_ms = rk::wall_ms() - t2;
+  return RK_OK;
+}
+
 extern "C" int rk_classify_pairs(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p,
                                  uint32_t npairs, rk_result *out) {
   if (!ctx || !in || !p || !out || npairs == 0) return RK_E_ARG;
@@ -1018,6 +1082,18 @@ extern "C" int rk_classify_pairs(rk_ctx *ctx, const rk_frags_soa *in, const rk_p
   for (uint32_t q = 0; q < npairs; ++q)
     if (n && (!out[q].gid || !out[q].repval || !out[q].out_order)) return RK_E_ARG;
   HIPCHK(ctx, hipSetDevice(ctx->device));
+  // The compact wire format (RK_WIRE=0: off): rows go up as 12-B records
+  // packed by the host threads (25 B per row as SoA columns), and results come
+  // down as order + flag (5 B per row instead of 9): a new group starts at
+  // every row whose flag is not 2, so the gids are a host prefix count.
+  static const bool wire_on = [] {
+    const char *e = getenv("RK_WIRE");
+    return !e || e[0] != '0';
+  }();
+  if (wire_on && record_eligible(ctx, n)) {
+    const int rc = classify_wire(ctx, in, p, npairs, out);
+    if (rc != RK_WIRE_UNPACKABLE) return rc;
+  }
   // device staging: x, y, len (u64), strand (u8) in; per pair gid, order (u32), rep (u8) out
   size_t need = align_up(n * 8 + 16) * 3 + align_up(n + 16) +
                 (size_t)npairs * (align_up(n + 16) + align_up(n * 4 + 16) * 2);

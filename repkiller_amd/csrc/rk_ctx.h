@@ -95,6 +95,14 @@ struct IoPiece {
 };
 int io_h2d(rk_ctx *ctx, const std::vector<IoPiece> &pieces);
 int io_d2h(rk_ctx *ctx, const std::vector<IoPiece> &pieces);
+// the rows of a host SoA as 12-B wire records {xStart lo, yStart lo, length
+// (24) | reverse (1) | yStart >> 32 (3) | xStart >> 32 (4)} at `dev`, packed by
+// the host threads into the staging ring; 1 when some row does not fit
+// (length >= 2^24, yStart >= 2^35 or xStart >= 2^36)
+int io_h2d_rows(rk_ctx *ctx, const rk_frags_soa &in, void *dev);
+// gid[k] = (rows j <= k with flag[j] != 2) - 1: a new group starts at every
+// row whose repeat flag is not 2 (host threads)
+void gids_from_flags(rk_ctx *ctx, const uint8_t *flag, size_t n, uint32_t *gid);
 void io_destroy(rk_ctx *ctx);
 bool host_pinned(const void *p);
 double wall_ms();

@@ -243,12 +243,14 @@ struct NwChunkCounts {
   uint32_t W, lgW, nch;
   uint32_t *cnts;
 };
+// wire: the rows as rk_classify's 12-B wire records (rk_io.hip) instead of
+// the SoA columns of `in` (only in.n is read then)
 void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
                    uint32_t nby, const NwDigits &a, const NwDigits &y, uint32_t *ghist,
-                   uint32_t *yhist, uint32_t *ctrl, hipStream_t st);
+                   uint32_t *yhist, uint32_t *ctrl, hipStream_t st, const uint3 *wire = nullptr);
 void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
                    const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
-                   hipStream_t st);
+                   hipStream_t st, const uint3 *wire = nullptr);
 // (halo, G): the sharded driver's G lead-in records ahead of R (R holds m - G)
 void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st,
                 const uint4 *halo = nullptr, uint32_t G = 0);

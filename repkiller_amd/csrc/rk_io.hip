@@ -13,6 +13,7 @@
 // host copy of chunk k out of its slot).  HIP's own pageable path stages
 // through one thread; the parallel host copy is what lifts it to PCIe rate.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -231,6 +232,71 @@ int io_d2h(rk_ctx *ctx, const std::vector<IoPiece> &pieces) {
   }
   HIPCHK(ctx, hipStreamSynchronize(e.io));
   return RK_OK;
+}
+
+int io_h2d_rows(rk_ctx *ctx, const rk_frags_soa &in, void *dev) {
+  int rc = io_ready(ctx);
+  if (rc) return rc;
+  IoEngine &e = *ctx->ioe;
+  const size_t n = in.n, per = SLOT / 12;
+  bool busy[NSLOT] = {};
+  int k = 0;
+  std::atomic<bool> bad{false};
+  for (size_t a = 0; a < n; a += per) {
+    const size_t cnt = std::min(per, n - a);
+    if (busy[k]) HIPCHK(ctx, hipEventSynchronize(e.ev[k]));
+    uint32_t *slot = reinterpret_cast<uint32_t *>(e.slot[k]);
+    const size_t share = (cnt + e.pool->size() - 1) / e.pool->size();
+    const std::function<void(int)> job = [&](int t) {
+      const size_t lo = (size_t)t * share, hi = std::min(cnt, lo + share);
+      bool ok = true;
+      for (size_t i = lo; i < hi; ++i) {
+        const uint64_t x = in.x_start[a + i], y = in.y_start[a + i], L = in.length[a + i];
+        ok &= L < (1ull << 24) && y < (1ull << 35) && x < (1ull << 36);
+        const uint32_t s = in.strand[a + i] != 'f' ? 1u : 0u;
+        uint32_t *r = slot + 3 * i;
+        r[0] = (uint32_t)x;
+        r[1] = (uint32_t)y;
+        r[2] = (uint32_t)(L & 0xFFFFFFu) | s << 24 | (uint32_t)((y >> 32) & 7u) << 25 |
+               (uint32_t)((x >> 32) & 15u) << 28;
+      }
+      if (!ok) bad = true;
+    };
+    e.pool->run(job);
+    if (bad) {
+      HIPCHK(ctx, hipStreamSynchronize(e.io));
+      return 1;
+    }
+    HIPCHK(ctx, hipMemcpyAsync((char *)dev + a * 12, slot, cnt * 12, hipMemcpyHostToDevice, e.io));
+    HIPCHK(ctx, hipEventRecord(e.ev[k], e.io));
+    busy[k] = true;
+    k = (k + 1) % NSLOT;
+  }
+  HIPCHK(ctx, hipStreamSynchronize(e.io));
+  return RK_OK;
+}
+
+void gids_from_flags(rk_ctx *ctx, const uint8_t *flag, size_t n, uint32_t *gid) {
+  if (!n) return;
+  HostPool *pool = ctx->ioe->pool;  // io_d2h built the engine
+  const int T = pool->size();
+  const size_t share = (n + T - 1) / T;
+  std::vector<uint32_t> cnt(T + 1, 0);
+  pool->run([&](int t) {
+    const size_t lo = std::min(n, (size_t)t * share), hi = std::min(n, lo + share);
+    uint32_t c = 0;
+    for (size_t i = lo; i < hi; ++i) c += flag[i] != 2;
+    cnt[t + 1] = c;
+  });
+  for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+  pool->run([&](int t) {
+    const size_t lo = std::min(n, (size_t)t * share), hi = std::min(n, lo + share);
+    uint32_t g = cnt[t];
+    for (size_t i = lo; i < hi; ++i) {
+      g += flag[i] != 2;
+      gid[i] = g - 1;
+    }
+  });
 }
 
 double wall_ms() {

@@ -192,22 +192,49 @@ __device__ __forceinline__ void wave_run_add(uint32_t v, uint32_t *arr) {
   }
 }
 
-// --- processing order, pass 1: the file-order SoA becomes records ----------
-struct SrcFile {
-  using rec_t = uint4;
+// --- processing order, pass 1: the file-order rows become records ---------
+// A row source gives row i's (xStart, yStart, length, strand != 'f'): the
+// caller's SoA in HBM, or the 12-B wire rows rk_classify uploads (packed on
+// the host: {xStart lo 32, yStart lo 32, length (24) | reverse (1) | yStart
+// >> 32 (3) | xStart >> 32 (4)}, rk_io.hip)
+struct RowSoA {
   const uint64_t *x, *y, *len;
   const uint8_t *strand;
+  __device__ __forceinline__ void row(uint32_t i, uint64_t &xs, uint64_t &ys, uint64_t &L,
+                                      uint32_t &s) const {
+    xs = x[i], ys = y[i], L = len[i];
+    s = strand[i] != 'f' ? 1u : 0u;
+  }
+};
+struct RowWire {
+  const uint3 *w;
+  __device__ __forceinline__ void row(uint32_t i, uint64_t &xs, uint64_t &ys, uint64_t &L,
+                                      uint32_t &s) const {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(w + i);
+    const uint32_t a = __builtin_nontemporal_load(p), b = __builtin_nontemporal_load(p + 1),
+                   c = __builtin_nontemporal_load(p + 2);
+    xs = (uint64_t)(c >> 28) << 32 | a;
+    ys = (uint64_t)((c >> 25) & 7u) << 32 | b;
+    L = c & 0xFFFFFFu;
+    s = (c >> 24) & 1u;
+  }
+};
+template <class Rows>
+struct SrcFile {
+  using rec_t = uint4;
+  Rows rows;
   uint64_t vsize;
   __device__ __forceinline__ uint4 load(uint32_t i) const {
-    const uint64_t xs = x[i], ys = y[i], L = len[i];
-    const uint32_t s = strand[i] != 'f' ? 1u : 0u;
+    uint64_t xs, ys, L;
+    uint32_t s;
+    rows.row(i, xs, ys, L, s);
     const uint64_t pk = div_small(xs, 10);
     const uint32_t key = (uint32_t)(pk < vsize - 1 ? pk : vsize - 1);
     // (rows that do not pack were flagged by k_nw_order_hist: the generic
     // pipeline takes over then)
     return make_uint4(key, i, (uint32_t)ys,
                       (uint32_t)(L & 0xFFFFFFu) | s << 24 | (uint32_t)((ys >> 32) & 7u) << 25 |
-                          (uint32_t)(xs % 10) << 28);
+                          (uint32_t)(xs - pk * 10) << 28);
   }
   __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
 };
@@ -358,16 +385,17 @@ struct DstMembers {
 // out-of-bounds checks (xStart/10 >= vsize; probes past an occupancy array)
 // and whether every row packs into a record.  ctrl: [0] error bits, [1] kept
 // rows, [3] some row does not pack, [4] longest kept length, [8] forward kept.
+template <class Rows>
 struct OrderHistArgs {
-  const uint64_t *x, *y, *len;
-  const uint8_t *strand;
+  Rows rows;
   uint32_t n;
   uint64_t vsize, max_x, max_y;
   uint32_t nby;
   Digits D, yd;
   uint32_t *ghist, *yhist, *ctrl;
 };
-__global__ void __launch_bounds__(256) k_nw_order_hist(OrderHistArgs a) {
+template <class Rows>
+__global__ void __launch_bounds__(256) k_nw_order_hist(OrderHistArgs<Rows> a) {
   __shared__ HistLds L, LY;
   __shared__ uint32_t red[4];
   hist_init(L);
@@ -378,8 +406,9 @@ __global__ void __launch_bounds__(256) k_nw_order_hist(OrderHistArgs a) {
   bool ub = false, ubc = false, wide = false;
   const uint64_t drop = a.vsize - 1;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-    const uint64_t xs = a.x[i], ys = a.y[i], L0 = a.len[i];
-    const uint32_t s = a.strand[i] != 'f' ? 1u : 0u;
+    uint64_t xs, ys, L0;
+    uint32_t s;
+    a.rows.row(i, xs, ys, L0, s);
     const uint64_t pk = div_small(xs, 10);
     ub |= pk >= a.vsize;
     wide |= L0 >= (1ull << 24) || ys >= (1ull << 35);
@@ -960,16 +989,27 @@ static PassStatus pass_status(uint32_t *status, uint32_t n, const Digits &D, int
   return PassStatus{status, half, same && 2 * half + 64 <= nw_status_words(n), rec_bytes};
 }
 
+template <class Rows>
+static void order_hist(const Rows &rows, uint32_t n, double row_bytes, uint64_t vsize,
+                       uint64_t max_x, uint64_t max_y, uint32_t nby, const NwDigits &a,
+                       const NwDigits &y, uint32_t *ghist, uint32_t *yhist, uint32_t *ctrl,
+                       hipStream_t st) {
+  if (!n) return;
+  OrderHistArgs<Rows> args{rows, n, vsize, max_x, max_y, nby, to_digits(a), to_digits(y), ghist,
+                           yhist, ctrl};
+  kt_begin(st);
+  k_nw_order_hist<Rows><<<grid_for(n, 256, 2048), 256, 0, st>>>(args);
+  kt_end(st, KID_NW_HIST, row_bytes * n);  // the rows read once
+}
 void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint64_t max_y,
                    uint32_t nby, const NwDigits &a, const NwDigits &y, uint32_t *ghist,
-                   uint32_t *yhist, uint32_t *ctrl, hipStream_t st) {
-  const uint32_t n = (uint32_t)in.n;
-  if (!n) return;
-  OrderHistArgs args{in.x_start, in.y_start, in.length, in.strand, n, vsize, max_x, max_y, nby,
-                     to_digits(a), to_digits(y), ghist, yhist, ctrl};
-  kt_begin(st);
-  k_nw_order_hist<<<grid_for(n, 256, 2048), 256, 0, st>>>(args);
-  kt_end(st, KID_NW_HIST, 25.0 * n);  // the SoA read once
+                   uint32_t *yhist, uint32_t *ctrl, hipStream_t st, const uint3 *wire) {
+  if (wire)
+    order_hist(RowWire{wire}, (uint32_t)in.n, 12.0, vsize, max_x, max_y, nby, a, y, ghist, yhist,
+               ctrl, st);
+  else
+    order_hist(RowSoA{in.x_start, in.y_start, in.length, in.strand}, (uint32_t)in.n, 25.0, vsize,
+               max_x, max_y, nby, a, y, ghist, yhist, ctrl, st);
 }
 
 // the processing order: passes over records, the first one from `first`
@@ -1010,9 +1050,14 @@ static void nw_order_passes(const Src1 &first, double in_bytes, uint32_t n, uint
 }
 void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
                    const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
-                   hipStream_t st) {
-  nw_order_passes(SrcFile{in.x_start, in.y_start, in.length, in.strand, vsize}, 25.0,
-                  (uint32_t)in.n, nby, 0u, a, ghist, status, Ra, Rb, yrec, st);
+                   hipStream_t st, const uint3 *wire) {
+  if (wire)
+    nw_order_passes(SrcFile<RowWire>{RowWire{wire}, vsize}, 12.0, (uint32_t)in.n, nby, 0u, a,
+                    ghist, status, Ra, Rb, yrec, st);
+  else
+    nw_order_passes(
+        SrcFile<RowSoA>{RowSoA{in.x_start, in.y_start, in.length, in.strand}, vsize}, 25.0,
+        (uint32_t)in.n, nby, 0u, a, ghist, status, Ra, Rb, yrec, st);
 }
 void nw_order_sort_recs(const uint4 *in, uint32_t m, uint32_t nby, uint32_t base,
                         const NwDigits &a, const uint32_t *ghist, uint32_t *status, uint4 *Ra,
