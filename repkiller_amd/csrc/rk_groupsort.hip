@@ -703,13 +703,21 @@ __global__ void __launch_bounds__(256) k_sort_groups_reg(TierLists tl, int tier,
 __host__ __device__ constexpr uint32_t lds_stack(uint32_t cap) {
   return 2 * (31 - __builtin_clz(cap)) + 4;
 }
-template <class KT>
-__global__ void __launch_bounds__(64) k_sort_groups_lds(TierLists tl, int tier,
-                                                        const uint32_t *goff, const uint64_t *key,
-                                                        const uint32_t *tag, uint32_t *otag,
-                                                        uint32_t cap, uint32_t reg_max) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  const uint32_t lane = threadIdx.x;
+// WPB independent wavefronts per block, each with its own LDS slab of `slab`
+// bytes (a CU holds a bounded number of blocks, so one-wave blocks of the
+// small caps leave it with few resident wavefronts)
+template <class KT, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_sort_groups_lds(TierLists tl, int tier,
+                                                              const uint32_t *goff,
+                                                              const uint64_t *key,
+                                                              const uint32_t *tag, uint32_t *otag,
+                                                              uint32_t cap, uint32_t reg_max,
+                                                              uint32_t slab) {
+  extern __shared__ __align__(16) uint8_t smem_all[];
+  // the wavefront index in a scalar register: every LDS base stays uniform
+  const uint32_t lane = threadIdx.x & 63,
+                 wv = WPB == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t *smem = smem_all + (size_t)wv * slab;
   const uint32_t nfr = cap / (THRESH + 1) + 2;
   KT *K = reinterpret_cast<KT *>(smem);
   uint32_t *T = reinterpret_cast<uint32_t *>(K + cap);
@@ -722,7 +730,7 @@ __global__ void __launch_bounds__(64) k_sort_groups_lds(TierLists tl, int tier,
   const ViewT<KT, uint16_t> v{K, T, PL, PR, B};
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
-  for (uint32_t w = lo + blockIdx.x; w < hi; w += gridDim.x) {
+  for (uint32_t w = lo + blockIdx.x * WPB + wv; w < hi; w += gridDim.x * WPB) {
     const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     for (uint32_t x = lane; x < n; x += 64) {
@@ -967,19 +975,24 @@ __global__ void __launch_bounds__(256) k_clear_if_tier(TierLists tl, int tier, u
   }
 }
 
-template <class KT>
-__global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, uint32_t m,
-                                                      const uint8_t *bnd, const uint32_t *head,
-                                                      const uint64_t *key, const uint32_t *tag,
-                                                      uint32_t *otag, uint32_t reg_max) {
+template <class KT, int WPB>
+__global__ void __launch_bounds__(64 * WPB) k_sort_segments(TierLists tl, int tier, uint32_t m,
+                                                            const uint8_t *bnd,
+                                                            const uint32_t *head,
+                                                            const uint64_t *key,
+                                                            const uint32_t *tag, uint32_t *otag,
+                                                            uint32_t reg_max, uint32_t slab) {
   {
     uint32_t lo, hi;
     tl.range(tier, lo, hi);
     if (lo == hi) return;
   }
-  extern __shared__ __align__(16) uint8_t smem[];
+  extern __shared__ __align__(16) uint8_t smem_all[];
   constexpr uint32_t cap = SPLIT_T;
-  const uint32_t lane = threadIdx.x;
+  // the wavefront index in a scalar register: every LDS base stays uniform
+  const uint32_t lane = threadIdx.x & 63,
+                 wv = WPB == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t *smem = smem_all + (size_t)wv * slab;
   const uint32_t nfr = cap / (THRESH + 1) + 2;
   KT *K = reinterpret_cast<KT *>(smem);
   uint32_t *T = reinterpret_cast<uint32_t *>(K + cap);
@@ -990,7 +1003,7 @@ __global__ void __launch_bounds__(64) k_sort_segments(TierLists tl, int tier, ui
   uint16_t *PR = PL + cap;
   uint8_t *B = reinterpret_cast<uint8_t *>(PR + cap);
   const ViewT<KT, uint16_t> v{K, T, PL, PR, B};
-  for (uint32_t w0 = blockIdx.x * 64; w0 < m; w0 += gridDim.x * 64) {
+  for (uint32_t w0 = (blockIdx.x * WPB + wv) * 64; w0 < m; w0 += gridDim.x * WPB * 64) {
     uint64_t hb = __ballot(w0 + lane < m && bnd[w0 + lane] == 1);
     while (hb) {
       const uint32_t x = w0 + (uint32_t)__builtin_ctzll(hb);
@@ -1210,16 +1223,33 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     const int b = e ? atoi(e) : 2;
     return b < 0 ? 0 : b > NLDS ? NLDS : b;
   }();
+  // wavefronts per block of the LDS tiers up to 512 members (RK_GS_WPB: 1 or 4;
+  // cfg3 group-sort phase 1.199-1.205 / 1.203-1.205 ms, neutral)
+  static const int wpb = [] {
+    const char *e = getenv("RK_GS_WPB");
+    return e && atoi(e) == 4 ? 4 : 1;
+  }();
   auto launch_lds = [&](int j, hipStream_t sj) {
     const uint32_t cap = caps.c[j];
-    const uint32_t grid = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
+    const uint32_t waves = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
+    const int wp = cap <= 512 ? wpb : 1;
+    const size_t slab = (lds_bytes(cap, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
     kt_begin(sj);
-    if (narrow_keys)
-      k_sort_groups_lds<uint32_t><<<grid, 64, lds_bytes(cap, 4), sj>>>(tl, TIER_LDS0 + j, goff, key,
-                                                                       tag, otag, cap, reg_max);
-    else
-      k_sort_groups_lds<uint64_t><<<grid, 64, lds_bytes(cap, 8), sj>>>(tl, TIER_LDS0 + j, goff, key,
-                                                                       tag, otag, cap, reg_max);
+    if (wp == 4) {
+      if (narrow_keys)
+        k_sort_groups_lds<uint32_t, 4><<<waves / 4, 256, 4 * slab, sj>>>(
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, reg_max, (uint32_t)slab);
+      else
+        k_sort_groups_lds<uint64_t, 4><<<waves / 4, 256, 4 * slab, sj>>>(
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, reg_max, (uint32_t)slab);
+    } else {
+      if (narrow_keys)
+        k_sort_groups_lds<uint32_t, 1><<<waves, 64, slab, sj>>>(tl, TIER_LDS0 + j, goff, key, tag,
+                                                                otag, cap, reg_max, (uint32_t)slab);
+      else
+        k_sort_groups_lds<uint64_t, 1><<<waves, 64, slab, sj>>>(tl, TIER_LDS0 + j, goff, key, tag,
+                                                                otag, cap, reg_max, (uint32_t)slab);
+    }
     kt_end(sj, KID_SORT_LDS, 0.0);
     tier_slot(TIER_LDS0 + j);
   };
@@ -1280,12 +1310,24 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   tier_slot(NTIER - 1);
   k_heap_segments<<<64, 256, 0, st>>>(heapq_n, heapq, key, tag, otag);
   kt_begin(st);
-  if (narrow_keys)
-    k_sort_segments<uint32_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 4), st>>>(
-        tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max);
-  else
-    k_sort_segments<uint64_t><<<8192, 64, seg_lds_bytes(SPLIT_T, 8), st>>>(
-        tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max);
+  {
+    const size_t slab = (seg_lds_bytes(SPLIT_T, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
+    if (wpb == 4) {
+      if (narrow_keys)
+        k_sort_segments<uint32_t, 4><<<2048, 256, 4 * slab, st>>>(
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
+      else
+        k_sort_segments<uint64_t, 4><<<2048, 256, 4 * slab, st>>>(
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
+    } else {
+      if (narrow_keys)
+        k_sort_segments<uint32_t, 1><<<8192, 64, slab, st>>>(tl, NTIER - 1, m, bnd, pl, key, tag,
+                                                             otag, reg_max, (uint32_t)slab);
+      else
+        k_sort_segments<uint64_t, 1><<<8192, 64, slab, st>>>(tl, NTIER - 1, m, bnd, pl, key, tag,
+                                                             otag, reg_max, (uint32_t)slab);
+    }
+  }
   kt_end(st, KID_SORT_SEGS, 0.0);
   tier_slot(NTIER);
   if (side) (void)hipStreamWaitEvent(st, ev_join, 0);
