@@ -92,6 +92,10 @@ struct RcclComm final : rk_comm {
 
   int allgather(const void *send, void *recv, size_t bytes, hipStream_t st) override {
     if (!bytes) return RK_OK;
+    if (size == 1) {  // no peers: the gathered block is our own (no device round trip)
+      std::memcpy(recv, send, bytes);
+      return RK_OK;
+    }
     const size_t need = bytes * (size_t)(size + 1);
     if (need > stage_cap) {
       if (stage) (void)hipFree(stage);

@@ -302,8 +302,22 @@ __global__ void __launch_bounds__(256) k_nw_rec_hist(const uint32_t *__restrict_
   __shared__ HistLds L;
   hist_init(L);
   __syncthreads();
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    hist_add(L, D, recs[(size_t)i * STRIDE] - sub);
+  if (STRIDE == 1) {
+    // 4-B keys (the sharded driver's group ids by processing index) come in
+    // long runs of equal high digits: one LDS atomic per run of a wavefront
+    // instead of one per key on the same counter
+    const uint32_t step = gridDim.x * blockDim.x;
+    for (uint32_t b = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < n; b += step) {
+      const uint32_t i = b + (threadIdx.x & 63);
+      const bool in = i < n;
+      const uint32_t key = in ? recs[i] - sub : 0u;
+      for (int p = 0; p < D.passes; ++p)
+        wave_run_add(in ? (uint32_t)p * 1024u + D.digit(p, key) : NONE, L.h);
+    }
+  } else {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+      hist_add(L, D, recs[(size_t)i * STRIDE] - sub);
+  }
   __syncthreads();
   hist_flush(L, D, ghist);
 }

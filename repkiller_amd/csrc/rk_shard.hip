@@ -48,6 +48,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -187,6 +188,19 @@ __global__ void __launch_bounds__(256) k_part_scatter(Op op, uint32_t n, uint32_
 __global__ void k_totals(const uint32_t *off, uint32_t nblk, uint32_t P, uint32_t *tot) {
   const uint32_t d = threadIdx.x;
   if (d <= P) tot[d] = off[(size_t)d * nblk];
+}
+
+// a plan built from host-known counts: the device's own offsets must agree
+// (else ERRB_INTERNAL, caught at the next agreement point; the send buffers
+// of such plans are sized for every element, so a disagreement cannot write
+// out of bounds)
+struct Expect {
+  uint32_t v[MAXP + 1];
+};
+__global__ void k_expect_totals(const uint32_t *off, uint32_t nblk, uint32_t P, Expect e,
+                                uint32_t *ctrl) {
+  const uint32_t d = threadIdx.x;
+  if (d <= P && off[(size_t)d * nblk] != e.v[d]) atomicOr(&ctrl[0], ERRB_INTERNAL);
 }
 
 template <class Op>
@@ -799,6 +813,52 @@ struct Shard {
     for (uint32_t q = 0; q < P; ++q) pp.cnt[q] = t[q + 1] - t[q];
     pp.total = t[P];
   }
+  // a plan whose per-destination counts are known on the host: the device
+  // offsets are built, without a readback
+  template <class Op>
+  void plan_counts(const Op &op, uint32_t n, PartPlan &pp, const uint64_t *cnt) {
+    PartPlan ref;
+    ref.total = 0;
+    for (uint32_t q = 0; q < MAXP; ++q) {
+      ref.cnt[q] = q < P ? cnt[q] : 0;
+      ref.total += ref.cnt[q];
+    }
+    plan_same(op, n, pp, ref);
+  }
+  // a plan whose host counts are known to equal `ref`'s (the same selection
+  // in the same order): the device offsets are rebuilt, without a readback
+  template <class Op>
+  void plan_same(const Op &op, uint32_t n, PartPlan &pp, const PartPlan &ref) {
+    pp.n = n;
+    pp.nblk = n ? (n + PART_TILE - 1) / PART_TILE : 1;
+    const size_t len = (size_t)P * pp.nblk + 1;
+    uint32_t *cnt = take<uint32_t>(SL_PCNT, len);
+    pp.off = take<uint32_t>(SL_POFF, len);
+    zero(cnt + len - 1, 4);
+    kt_begin(st);
+    k_part_count<<<pp.nblk, 256, 0, st>>>(op, n, P, pp.nblk, cnt, pp.mcache, pp.mread);
+    kt_end(st, KID_PART, 0.0);
+    launched("k_part_count");
+    exclusive_scan_u32(cnt, pp.off, len, scan_scratch(SL_PSCAN, len), st);
+    for (uint32_t q = 0; q < MAXP; ++q) pp.cnt[q] = ref.cnt[q];
+    pp.total = ref.total;
+    Expect e{};
+    for (uint32_t q = 0, acc = 0; q <= P; ++q) {
+      e.v[q] = acc;
+      if (q < P) acc += (uint32_t)ref.cnt[q];
+    }
+    k_expect_totals<<<1, 64, 0, st>>>(pp.off, pp.nblk, P, e, ctrl);
+    launched("k_expect_totals");
+  }
+  // several device words in one round trip
+  std::vector<uint32_t> d2h_words(std::initializer_list<const uint32_t *> src) {
+    std::vector<uint32_t> h(src.size());
+    size_t i = 0;
+    for (const uint32_t *d : src)
+      hip(hipMemcpyAsync(&h[i++], d, 4, hipMemcpyDeviceToHost, st), "d2h");
+    hip(hipStreamSynchronize(st), "d2h sync");
+    return h;
+  }
   // a plan that sends nothing (the op cannot select any element)
   void zero_plan(uint32_t n, PartPlan &pp) {
     pp.n = n;
@@ -862,8 +922,8 @@ struct Shard {
   }
 
   // device error bits agreed by every rank
-  void agree_errors() {
-    uint32_t bits = read1(ctrl);
+  void agree_errors() { agree_error_bits(read1(ctrl)); }
+  void agree_error_bits(uint32_t bits) {
     uint32_t any = 0;
     for (uint32_t b : gather1<uint32_t>(bits)) any |= b;
     check(err_status(ctx, any & ~(uint32_t)ERRB_WIDE_LENGTH));
@@ -1053,7 +1113,7 @@ void verify_y_halo(Shard &S, RelOp relop, const uint8_t *ycode, uint8_t *ystate,
                                                             S.ctrl + 2);
       S.launched("k_cmp_y");
     }
-    const uint32_t mism = S.read1(S.ctrl + 2);
+    const uint32_t mism = nrel ? S.read1(S.ctrl + 2) : 0u;  // no relevant halo: nothing to compare
     if (S.sum_any(mism) == 0) break;
     if (mism) {
       ++ss.y_reruns;
@@ -1115,11 +1175,18 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
     }
     exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), S.st);
   }
-  S.agree_errors();
-  const uint32_t nroots = m ? S.read1(lrank + m) : 0;
+  // the error bits, the root count and the cross-slice link flag: one readback
+  uint32_t nroots = 0, xlink = 0;
+  if (m) {
+    const std::vector<uint32_t> w = S.d2h_words({S.ctrl, lrank + m, S.ctrl + 23});
+    S.agree_error_bits(w[0]);
+    nroots = w[1];
+    xlink = w[2];
+  } else {
+    S.agree_errors();
+  }
   // root count (low 32 bits) and whether this rank has a cross-slice link
-  std::vector<uint64_t> rall =
-      S.gather1<uint64_t>(nroots | (uint64_t)(m ? S.read1(S.ctrl + 23) : 0u) << 32);
+  std::vector<uint64_t> rall = S.gather1<uint64_t>(nroots | (uint64_t)xlink << 32);
   uint64_t goff = 0, Gtot = 0;
   bool links = false;
   for (uint32_t q = 0; q < P; ++q) {
@@ -1134,7 +1201,8 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
       kt_end(S.st, KID_SHARD_AUX, 12.0 * m);
       S.launched("k_final_gid_local");
     }
-    S.agree_errors();
+    // (no agreement point here: k_final_gid_local raises no error bits, and
+    // the driver's last agreement follows)
     *Gtot_out = Gtot;
     return junk;
   }

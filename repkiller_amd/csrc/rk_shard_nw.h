@@ -59,7 +59,8 @@ __device__ __forceinline__ uint32_t nwy_bucket(const uint3 &r, uint32_t nby) {
 }
 
 // ---- source side: processing keys, the checks, the slice histogram --------
-// ctrl: [0] error bits, [20] some kept row does not pack, [21] longest kept length
+// ctrl: [0] error bits, [20] some kept row does not pack, [21] longest kept
+// length, [25] kept rows
 struct ShRowsArgs {
   Frags f;
   uint64_t vsize, max_x, max_y;
@@ -71,18 +72,19 @@ __device__ __forceinline__ uint64_t div10_sh(uint64_t v) {  // 32-bit when it fi
 }
 __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
   __shared__ uint32_t h[NBINS];
-  __shared__ uint32_t red[2];
+  __shared__ uint32_t red[3];
   for (uint32_t b = threadIdx.x; b < NBINS; b += 256) h[b] = 0;
-  if (threadIdx.x < 2) red[threadIdx.x] = 0;
+  if (threadIdx.x < 3) red[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t drop = a.vsize - 1;
-  uint32_t maxlen = 0;
+  uint32_t maxlen = 0, kept = 0;
   bool ub = false, ubc = false, wide = false;
   GRID_STRIDE(i, a.f.n) {
     const uint64_t xs = a.f.x[i], ys = a.f.y[i], L0 = a.f.len[i];
     const uint64_t pk = div10_sh(xs);
     ub |= pk >= a.vsize;
     if (pk >= drop) continue;  // the never-iterated last bucket (or out of bounds)
+    ++kept;
     wide |= L0 >= (1ull << 24) || ys >= (1ull << 35);
     const uint32_t len = (uint32_t)(L0 & 0xFFFFFFu);  // exact whenever the row packs
     maxlen = len > maxlen ? len : maxlen;
@@ -94,17 +96,20 @@ __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
   for (int off = 32; off > 0; off >>= 1) {
     const uint32_t o = __shfl_xor(maxlen, off);
     maxlen = o > maxlen ? o : maxlen;
+    kept += __shfl_xor(kept, off);
   }
   const uint64_t bub = __ballot(ub), bubc = __ballot(ubc), bwide = __ballot(wide);
   if ((threadIdx.x & 63) == 0) {
     atomicMax(&red[0], maxlen);
     atomicOr(&red[1], (bub ? 1u : 0u) | (bubc ? 2u : 0u) | (bwide ? 4u : 0u));
+    atomicAdd(&red[2], kept);
   }
   __syncthreads();
   if (a.hist)
     for (uint32_t b = threadIdx.x; b < NBINS; b += 256)
       if (h[b]) atomicAdd(&a.hist[b], h[b]);
   if (threadIdx.x == 0) {
+    if (red[2]) atomicAdd(&a.ctrl[25], red[2]);
     if (red[0]) atomicMax(&a.ctrl[21], red[0]);
     if (red[1] & 1u) atomicOr(&a.ctrl[0], ERRB_UB_BUCKET);
     if (red[1] & 2u) atomicOr(&a.ctrl[0], ERRB_UB_CENTER);
@@ -373,33 +378,54 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   const uint32_t shift = bin_shift(drop);
   uint32_t *hist = S.take<uint32_t>(SN_HIST, 3 * 4096);  // later the sorts' digit histograms
   S.zero(hist, NBINS * 4);
+  S.zero(S.ctrl + 25, 4);
   if (nl) {
+    // more blocks when there is no slice histogram to flush (one rank)
     kt_begin(st);
-    k_sh_rows<<<grid_for(nl, 256, 512), 256, 0, st>>>(
+    k_sh_rows<<<grid_for(nl, 256, P > 1 ? 1024 : 4096), 256, 0, st>>>(
         ShRowsArgs{f, vsize, max_x, max_y, shift, P > 1 ? hist : nullptr, S.ctrl});
     kt_end(st, KID_SH_ROWKEYS, 25.0 * nl);
     S.launched("k_sh_rows");
   }
-  S.agree_errors();
-  const std::vector<uint32_t> flags = S.d2h(S.ctrl + 20, 2);
+  // the error bits (ctrl[0]), the pack flags (ctrl[20..21]) and the kept
+  // count (ctrl[25]) in one readback
+  const std::vector<uint32_t> flags = S.d2h(S.ctrl, 26);
+  S.agree_error_bits(flags[0]);
   uint32_t nopack = 0, maxlen = 0;
-  for (uint32_t v : S.gather1<uint32_t>(flags[0] | (flags[1] << 1)))
+  for (uint32_t v : S.gather1<uint32_t>(flags[20] | (flags[21] << 1)))
     nopack |= v & 1u, maxlen = (v >> 1) > maxlen ? (v >> 1) : maxlen;
   if (nopack) return RK_SHARD_FALLBACK;
   std::vector<uint64_t> gh(NBINS, 0);
+  std::vector<uint32_t> mine;
   if (P > 1) {
-    std::vector<uint32_t> mine = S.d2h(hist, NBINS), all((size_t)P * NBINS);
+    std::vector<uint32_t> all((size_t)P * NBINS);
+    mine = S.d2h(hist, NBINS);
     S.allgather(mine.data(), all.data(), NBINS * 4);
     for (uint32_t q = 0; q < P; ++q)
       for (uint32_t b = 0; b < NBINS; ++b) gh[b] += all[(size_t)q * NBINS + b];
   }
   const Bounds slice_keys = split_bounds(gh, shift, drop, P);
 
-  // ---- 2: rows -> slice owners as 16-B records (arrival order = file order)
+  // ---- 2: rows -> slice owners as 16-B records (arrival order = file order);
+  // the bounds lie on histogram bins (or at the end), so this rank's count per
+  // owner is a sum of its own bins -- the plan needs no readback
   RowOp16 rop{f, slice_keys, drop, (uint32_t)row_base, nullptr};
   PartPlan pp;
-  S.plan(rop, nl, pp);
-  rop.out = S.take<uint4>(SN_SROWS, pp.total + 1);
+  {
+    uint64_t cnt[MAXP] = {};
+    if (P == 1) {
+      cnt[0] = flags[25];
+    } else {
+      const uint64_t unit = 1ull << shift;
+      for (uint32_t q = 0; q < P; ++q) {
+        const uint64_t b0 = (slice_keys.b[q] + unit - 1) >> shift,
+                       b1 = (slice_keys.b[q + 1] + unit - 1) >> shift;
+        for (uint64_t b = b0; b < b1 && b < NBINS; ++b) cnt[q] += mine[b];
+      }
+    }
+    S.plan_counts(rop, nl, pp, cnt);
+  }
+  rop.out = S.take<uint4>(SN_SROWS, (size_t)nl + 1);  // room for every row (see plan_counts)
   S.emit(rop, pp);
   uint32_t m = 0;
   const uint4 *rin = exchange_nw<uint4>(S, rop.out, pp, SN_RIN, &m);
@@ -487,13 +513,19 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
       nw_y_sort_tail(yB, yA, n, yd, yhist, ystat, cy, nby, max_y, bits, s, true,
                      reinterpret_cast<const uint4 *>(src));
   };
+  // RK_SH_YSERIAL=1: the Y head on the main stream, ahead of X (A/B)
+  static const bool y_serial = [] {
+    const char *e = getenv("RK_SH_YSERIAL");
+    return e && e[0] == '1';
+  }();
+  hipStream_t sy = y_serial ? st : st2;
   S.hip(hipEventRecord(ctx->fork, st), "fork");
   S.hip(hipStreamWaitEvent(st2, ctx->fork, 0), "fork wait");
   if (ny) {
-    k_sh_ycode<<<grid_for(ny, 256), 256, 0, st2>>>(yr, ny, nby, ylo, yhi, ycode);
+    k_sh_ycode<<<grid_for(ny, 256), 256, 0, sy>>>(yr, ny, nby, ylo, yhi, ycode);
     S.launched("k_sh_ycode");
   }
-  y_sort(yr, ny, nullptr, st2, true, false);
+  y_sort(yr, ny, nullptr, sy, true, false);
   S.launched("Y sort head");
   S.hip(hipEventRecord(ctx->join, st2), "join");
   ss.ms_y = ms_since(ty);
@@ -529,7 +561,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   const uint32_t nsuf = m - gop.base;
   const uint64_t bmin_me = slice_keys.b[me] / 10;
   const uint64_t rel_x = bmin_me >= 1 ? bmin_me - 1 : 0;  // relevant: probed by own queries
-  S.plan(gop, nsuf, pp);
+  if (nsuf) S.plan(gop, nsuf, pp);
+  else S.zero_plan(0, pp);  // no row can reach a later slice: nothing to send
   gop.out = S.take<uint4>(SN_SHALO, pp.total + 1);
   S.emit(gop, pp);
   uint32_t G = 0;
@@ -583,7 +616,9 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   };
   S.zero(S.ctrl + 6, 4);
   solve_x(hx, G);
-  for (;;) {  // verify the relevant halo against its owners' decisions
+  // verify the relevant halo against its owners' decisions (one rank: there
+  // are no later slices, so no halo was sent or received)
+  for (; P > 1;) {
     ++ss.x_rounds;
     if (ss.x_rounds > P + 2) {
       ctx->err = "X halo verification did not converge";
@@ -633,7 +668,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     PartPlan xpp;
     xpp.mcache = ypp.mcache;
     xpp.mread = true;
-    S.plan(xop, m, xpp);
+    S.plan_same(xop, m, xpp, ypp);  // the Y records' own selection: counts known
     xop.xout = S.take<uint8_t>(SN_SXH, xpp.total + 1);
     S.emit(xop, xpp);
     uint32_t n2 = 0;
@@ -714,12 +749,12 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   const Bounds gb = split_bounds(P > 1 ? global_hist(S, mop, m) : std::vector<uint64_t>(NBINS, 0),
                                  mop.shift, Gtot, P);
   mop.B = gb;
-  S.plan(mop, m, pp);
   const size_t esz = narrow ? 12 : 16;
   // one rank: every member stays here and the X chunk's member arrays are
   // exactly the own rows (no halo): the member sort reads them in place, as on
-  // one device
-  const bool m_self = P == 1 && pp.total == m && Gfin == 0;
+  // one device (no plan needed)
+  const bool m_self = P == 1 && Gfin == 0;
+  if (!m_self) S.plan(mop, m, pp);
   if (!m_self) {
     mop.out = S.take<uint8_t>(SN_SMEM, (pp.total + 1) * esz);
     S.emit(mop, pp);
