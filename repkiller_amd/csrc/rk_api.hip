@@ -541,6 +541,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::Axis ay{w.cy.key, w.cy.ent, nullptr, nullptr, w.cy.state, nullptr, w.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
+    ay.par_dev = true;
     if ((rc = rk::resolve_axis(ctx, ay, sc, true, &sweeps))) return rc;
     ctx->stats.y_sweeps = sweeps;
 
@@ -754,6 +755,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::Axis ay{w.cy.key, w.cy.ent, w.cy.cen, w.cy.len, w.cy.state, nullptr, w.p.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
+    ay.par_dev = true;
     if ((rc = rk::resolve_axis(ctx, ay, sweep_scratch(w), fast32, &sweeps))) return rc;
     ctx->stats.y_sweeps = sweeps;
 

@@ -120,6 +120,9 @@ struct Axis {          // one axis' occupancy entries in CSR (bucket-run) order
   uint32_t m;          // entries
   uint64_t max_index;  // seq_size / 100 (SequenceOcupationList.cpp:4)
   double len_ratio, pos_ratio;
+  // the first window sweep evaluates the winners' deviations lane-parallel
+  // (the Y axis: ~24 deviations per window against ~2 on the X axis)
+  bool par_dev = false;
 };
 // The axis' bucket runs: the 64-position windows (wpend[w] = window w still
 // owns undecided entries) and the runs longer than 64 entries, which take a

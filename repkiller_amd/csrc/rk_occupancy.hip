@@ -518,11 +518,11 @@ __device__ __forceinline__ void win_ballot(bool c0, bool c1, uint64_t lowt, uint
 // owns undecided entries, and records that in wpend[w].  NSLOT == 1 serves
 // the windows whose last run's tail fits in the lanes before the first run
 // start (most windows): every slot's code runs once instead of twice.
-template <int NSLOT>
+template <int NSLOT, bool PAR>
 __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t *wpend,
                                              uint8_t *lflag, uint8_t *rpend, uint2 *pk,
-                                             uint32_t *ent,
-                                             uint32_t *key, int lane, uint64_t S0, uint64_t S1,
+                                             uint32_t *ent, uint32_t *key, double *dev,
+                                             int lane, uint64_t S0, uint64_t S1,
                                              int t, uint2 pk0, uint32_t ent0, uint8_t st00,
                                              uint8_t nd00, uint2 pk1, uint32_t ent1, uint8_t st01,
                                              uint8_t nd01) {
@@ -687,44 +687,149 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
     // winners: the first strict maximum in scan order among the matching
     // ACTIVE candidates (own run newest first, then the neighbour run); a
     // single candidate needs no deviation
+#ifdef RK_SWEEP_PROF
+    uint32_t ndev = 0;  // deviations computed by this lane
+#endif
+    bool multi[2] = {false, false};
+    uint64_t aov[2] = {0, 0}, anv[2] = {0, 0};
+    uint32_t winv[2] = {NONE, NONE};
+    double bestv[2] = {0.0, 0.0};
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
       if (!own[s]) continue;
       pending |= st[s] == ST_UNKNOWN || st[s] == ST_HIT_PENDING;
-      if (st[s] == st0[s]) continue;
-      const uint32_t p = base + P[s];
-      if (st[s] == ST_HIT) {
-        const uint64_t ao = bits_from(A0, A1, rs[s]) & rown[s];
-        const uint64_t an = rnb[s] ? bits_from(A0, A1, nbs[s]) & rnb[s] : 0;
-        uint32_t win;
-        if (__popcll(ao) + __popcll(an) + (fs[s].any_active ? 1 : 0) == 1) {
-          win = ao ? ent[rs[s] + 63 - __clzll(ao)]
-                   : an ? ent[nbs[s] + 63 - __clzll(an)] : fs[s].win;
-        } else {
-          const Q32 q = make_q32(pk[P[s]].x, pk[P[s]].y, ax.len_ratio, ax.pos_ratio);
-          double best = 0.0;
-          win = NONE;
-          uint64_t b = ao;
-          while (b) {
-            const int v = 63 - __clzll(b);
-            b &= ~(1ull << v);
-            const double d = dev32(q, pk[rs[s] + v], ax.len_ratio, ax.pos_ratio);
-            if (d > best) best = d, win = ent[rs[s] + v];
-          }
-          b = an;
-          while (b) {
-            const int v = 63 - __clzll(b);
-            b &= ~(1ull << v);
-            const double d = dev32(q, pk[nbs[s] + v], ax.len_ratio, ax.pos_ratio);
-            if (d > best) best = d, win = ent[nbs[s] + v];
-          }
-          if (fs[s].any_active && fs[s].best > best) win = fs[s].win;
+      if (st[s] == st0[s] || st[s] != ST_HIT) continue;
+      const uint64_t ao = bits_from(A0, A1, rs[s]) & rown[s];
+      const uint64_t an = rnb[s] ? bits_from(A0, A1, nbs[s]) & rnb[s] : 0;
+      if (__popcll(ao) + __popcll(an) + (fs[s].any_active ? 1 : 0) == 1) {
+        winv[s] = ao ? ent[rs[s] + 63 - __clzll(ao)]
+                     : an ? ent[nbs[s] + 63 - __clzll(an)] : fs[s].win;
+      } else {
+        multi[s] = true;
+        aov[s] = ao;
+        anv[s] = an;
+      }
+    }
+    // deviations of the lanes with several candidates: lane-parallel over all
+    // (query, candidate) pairs of the wavefront when some lane has three or
+    // more (a serial loop would run to the longest list), serial otherwise
+    const uint32_t c0 = multi[0] ? __popcll(aov[0]) + __popcll(anv[0]) : 0u;
+    const uint32_t c1 = NSLOT == 2 && multi[1 % NSLOT] ? __popcll(aov[1 % NSLOT]) + __popcll(anv[1 % NSLOT]) : 0u;
+    const uint32_t ct = c0 + c1;
+#ifdef RK_SWEEP_PROF
+    ndev = ct;
+#endif
+    uint32_t cmax = ct;
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t o = __shfl_xor(cmax, off);
+      cmax = o > cmax ? o : cmax;
+    }
+    if (PAR && cmax >= 3) {
+      uint32_t incl = ct;  // inclusive prefix of the pair counts
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+      }
+      const uint32_t start = incl - ct, T = __shfl(incl, 63);
+      uint32_t *owner_at = key;  // the keys are done with (64 words used)
+      for (uint32_t cb = 0; cb < T; cb += 64) {
+        // owners mark their pairs inside this chunk
+        {
+          const uint32_t j0 = start > cb ? start : cb, j1e = start + ct, j1 = j1e < cb + 64 ? j1e : cb + 64;
+          for (uint32_t j = j0; j < j1; ++j) owner_at[j - cb] = lane;
         }
+        wave_sync_lds();
+        const uint32_t i = cb + lane;
+        const bool live = i < T;
+        const uint32_t o = live ? owner_at[lane] : 0u;
+        // the owner's lists, pulled from its lane (every lane takes part)
+        const uint32_t so = __shfl(start, (int)o), c0o = __shfl(c0, (int)o);
+        const uint32_t k = i - so;
+        const bool second = NSLOT == 2 && k >= c0o;
+        const uint32_t kk = second ? k - c0o : k;
+        uint64_t ao = 0, an = 0;
+        int rso = 0, nbo = 0, Po = 0;
+#pragma unroll
+        for (int s = 0; s < NSLOT; ++s) {
+          const uint64_t a = (uint64_t)(uint32_t)__shfl((int)(uint32_t)aov[s], (int)o) |
+                             (uint64_t)(uint32_t)__shfl((int)(uint32_t)(aov[s] >> 32), (int)o) << 32;
+          const uint64_t n = (uint64_t)(uint32_t)__shfl((int)(uint32_t)anv[s], (int)o) |
+                             (uint64_t)(uint32_t)__shfl((int)(uint32_t)(anv[s] >> 32), (int)o) << 32;
+          const int r = __shfl(rs[s], (int)o), nb = __shfl(nbs[s], (int)o), pp = __shfl(P[s], (int)o);
+          if (s == (second ? 1 : 0)) ao = a, an = n, rso = r, nbo = nb, Po = pp;
+        }
+        // the kk-th candidate in scan order: the (kk)-th highest bit of ao, then of an
+        const uint32_t na = __popcll(ao);
+        const bool in_own = kk < na;
+        uint64_t msk = in_own ? ao : an;
+        uint32_t r = (uint32_t)__popcll(msk) - 1u - (in_own ? kk : kk - na);  // rank from the bottom
+        int bpos = 0;
+#pragma unroll
+        for (int wdt = 32; wdt > 0; wdt >>= 1) {
+          const uint32_t lowc = __popcll(msk & ((1ull << wdt) - 1ull));
+          if (r >= lowc) {
+            r -= lowc;
+            msk >>= wdt;
+            bpos += wdt;
+          }
+        }
+        const int cpos = (in_own ? rso : nbo) + bpos;
+        double d = 0.0;
+        if (live) {
+          const uint2 qp = pk[Po];
+          const Q32 q = make_q32(qp.x, qp.y, ax.len_ratio, ax.pos_ratio);
+          d = dev32(q, pk[cpos], ax.len_ratio, ax.pos_ratio);
+          dev[lane] = d;
+          owner_at[64 + lane] = (uint32_t)cpos;
+        }
+        wave_sync_lds();
+        // every owner takes its pairs of this chunk in scan order
+        {
+          const uint32_t j0 = start > cb ? start : cb, j1e = start + ct, j1 = j1e < cb + 64 ? j1e : cb + 64;
+          for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t x = j - cb, kj = j - start;
+            const double dj = dev[x];
+            if (NSLOT == 2 && kj >= c0) {
+              if (dj > bestv[1 % NSLOT]) bestv[1 % NSLOT] = dj, winv[1 % NSLOT] = ent[owner_at[64 + x]];
+            } else {
+              if (dj > bestv[0]) bestv[0] = dj, winv[0] = ent[owner_at[64 + x]];
+            }
+          }
+        }
+        wave_sync_lds();
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < NSLOT; ++s) {
+        if (!multi[s]) continue;
+        const Q32 q = make_q32(pk[P[s]].x, pk[P[s]].y, ax.len_ratio, ax.pos_ratio);
+        uint64_t b = aov[s];
+        while (b) {
+          const int v = 63 - __clzll(b);
+          b &= ~(1ull << v);
+          const double d = dev32(q, pk[rs[s] + v], ax.len_ratio, ax.pos_ratio);
+          if (d > bestv[s]) bestv[s] = d, winv[s] = ent[rs[s] + v];
+        }
+        b = anv[s];
+        while (b) {
+          const int v = 63 - __clzll(b);
+          b &= ~(1ull << v);
+          const double d = dev32(q, pk[nbs[s] + v], ax.len_ratio, ax.pos_ratio);
+          if (d > bestv[s]) bestv[s] = d, winv[s] = ent[nbs[s] + v];
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NSLOT; ++s) {
+      if (!own[s] || st[s] == st0[s]) continue;
+      if (st[s] == ST_HIT) {
+        uint32_t win = winv[s];
+        if (multi[s] && fs[s].any_active && fs[s].best > bestv[s]) win = fs[s].win;
         record_decision(ax, ent[P[s]], ST_HIT, win);
       } else if (st[s] == ST_ACTIVE) {
         record_decision(ax, ent[P[s]], ST_ACTIVE, NONE);
       }
-      store_state(&ax.state[p], st[s]);
+      store_state(&ax.state[base + P[s]], st[s]);
     }
     const bool wp = __ballot(pending) != 0;
     if (lane == 0) wpend[w] = wp;
@@ -740,6 +845,16 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
     SP_ADD(6, 1);
     SP_ADD(7, o1 != 0);
     SP_ADD(8, NSLOT == 1);
+    {
+      uint32_t mx = ndev, sm = ndev;
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = __shfl_xor(mx, off);
+        mx = o > mx ? o : mx;
+        sm += __shfl_xor(sm, off);
+      }
+      SP_ADD(9, mx);   // the longest deviation list of a lane
+      SP_ADD(10, sm);  // deviations computed
+    }
 #endif
     return wp;
   }
@@ -748,9 +863,11 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
 // One window: the keys and slot-0 records in one memory round trip, the run
 // starts, then the one-slot core when the last run's tail (t entries past
 // position 63) fits in the lanes before the window's first run start f.
+template <bool PAR>
 __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8_t *wpend,
                                                uint8_t *lflag, uint8_t *rpend, uint2 *pk,
-                                               uint32_t *ent, uint32_t *key, int lane) {
+                                               uint32_t *ent, uint32_t *key, double *dev,
+                                               int lane) {
   const uint32_t base = w * 64, m = ax.m;
   uint64_t S0, S1;
   const uint32_t p0 = base + lane;
@@ -788,9 +905,9 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
     if (re > 64 && re - L <= (int)LONG_RUN && base + L < m) t = re - 64;
   }
   if (t <= f && t < 64)
-    return sweep_core32<1>(ax, w, wpend, lflag, rpend, pk, ent, key, lane, S0, S1, t, pk0, ent0,
+    return sweep_core32<1, PAR>(ax, w, wpend, lflag, rpend, pk, ent, key, dev, lane, S0, S1, t, pk0, ent0,
                            st00, nd00, pk1, ent1, st01, nd01);
-  return sweep_core32<2>(ax, w, wpend, lflag, rpend, pk, ent, key, lane, S0, S1, t, pk0, ent0,
+  return sweep_core32<2, PAR>(ax, w, wpend, lflag, rpend, pk, ent, key, dev, lane, S0, S1, t, pk0, ent0,
                          st00, nd00, pk1, ent1, st01, nd01);
 }
 
@@ -799,24 +916,29 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
 #ifndef RK_SWEEP_WPE
 #define RK_SWEEP_WPE 8
 #endif
+template <bool PAR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RK_SWEEP_WPE)))
 k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint8_t *lflag,
              uint8_t *rpend) {
   __shared__ uint2 s_pk[4][128 + OWN_U];  // {centre low 32 bits, length}; read padding
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
+  __shared__ double s_dev[4][PAR ? 64 : 1];  // the lane-parallel winner deviations
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t w = blockIdx.x * 4 + wv;
   bool pending = false;
   if (w < nwin)
-    pending = sweep_window32(ax, w, wpend, lflag, rpend, s_pk[wv], s_ent[wv], s_key[wv], lane);
+    pending = sweep_window32<PAR>(ax, w, wpend, lflag, rpend, s_pk[wv], s_ent[wv], s_key[wv],
+                             s_dev[wv], lane);
   count_pending(counters, pending && lane == 0);
 }
 
 // later sweeps: one wavefront per 64 windows, which reads their flags with
 // one coalesced load and handles the still-pending ones in turn
+template <bool PAR>
 __global__ void __launch_bounds__(256) k_sweep_fast_more(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters) {
   __shared__ uint2 s_pk[4][128 + OWN_U];
   __shared__ uint32_t s_ent[4][128], s_key[4][128];
+  __shared__ double s_dev[4][PAR ? 64 : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t g = blockIdx.x * 4 + wv, w0 = g * 64;
   bool pending = false;
@@ -826,8 +948,8 @@ __global__ void __launch_bounds__(256) k_sweep_fast_more(Axis ax, uint8_t *wpend
       const int b = __builtin_ctzll(todo);
       todo &= todo - 1;
       wave_sync_lds();  // the previous window's LDS reads are done
-      pending |= sweep_window32(ax, w0 + b, wpend, nullptr, nullptr, s_pk[wv], s_ent[wv],
-                                s_key[wv], lane);
+      pending |= sweep_window32<PAR>(ax, w0 + b, wpend, nullptr, nullptr, s_pk[wv], s_ent[wv],
+                                s_key[wv], s_dev[wv], lane);
     }
   }
   count_pending(counters, pending && lane == 0);
@@ -1392,12 +1514,21 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   // the window flags (their real work is what the first one left open)
   if (rl.nwin) {
     kt_begin(st);
-    if (rl.fast32 && first)
-      k_sweep_fast<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters,
-                                                      reinterpret_cast<uint8_t *>(rl.big), rpend);
-    else if (rl.fast32)
-      k_sweep_fast_more<<<((rl.nwin + 63) / 64 + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin,
-                                                                       counters);
+    if (rl.fast32 && first) {
+      if (ax.par_dev)
+        k_sweep_fast<true><<<(rl.nwin + 3) / 4, 256, 0, st>>>(
+            ax, rl.wpend, rl.nwin, counters, reinterpret_cast<uint8_t *>(rl.big), rpend);
+      else
+        k_sweep_fast<false><<<(rl.nwin + 3) / 4, 256, 0, st>>>(
+            ax, rl.wpend, rl.nwin, counters, reinterpret_cast<uint8_t *>(rl.big), rpend);
+    } else if (rl.fast32) {
+      if (ax.par_dev)
+        k_sweep_fast_more<true><<<((rl.nwin + 63) / 64 + 3) / 4, 256, 0, st>>>(ax, rl.wpend,
+                                                                             rl.nwin, counters);
+      else
+        k_sweep_fast_more<false><<<((rl.nwin + 63) / 64 + 3) / 4, 256, 0, st>>>(ax, rl.wpend,
+                                                                              rl.nwin, counters);
+    }
     else
       k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
     kt_end(st, rl.fast32 ? (first ? KID_SWEEP_FAST : KID_SWEEP_MORE) : KID_SWEEP_TILE,
@@ -1408,8 +1539,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
       (void)hipStreamSynchronize(st);
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sweep_prof), sizeof h);
       const double w = h[6] ? (double)h[6] : 1.0;
-      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f one-slot windows %.3f\n",
-              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w);
+      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f one-slot windows %.3f | longest deviation list/win %.2f deviations/win %.2f\n",
+              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w, h[9] / w, h[10] / w);
       (void)hipMemsetAsync(g_sweep_prof_ptr(), 0, sizeof h, st);
     }
 #endif

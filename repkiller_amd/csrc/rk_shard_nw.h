@@ -690,6 +690,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     Axis ay{cy.key, cy.ent, nullptr, nullptr, cy.state, nullptr, par_l, cy.pk, cy.nbd,
             S.take<uint32_t>(SL_RLEN, n), S.take<uint32_t>(SL_RBEG, n), n, max_y, p.len_ratio,
             p.pos_ratio};
+    ay.par_dev = true;
     SweepScratch sc{S.take<uint32_t>(SL_RUNS, runs_scratch_words(n)),
                     S.take<uint8_t>(SL_WPEND, n / 64 + 1), S.take<uint8_t>(SL_RPEND, n),
                     S.ctrl + 64, S.ctrl + 4};
