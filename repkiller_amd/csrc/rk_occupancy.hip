@@ -592,6 +592,9 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
       }
     }
     SP_T(2);
+#ifdef RK_SWEEP_PROF
+    uint32_t nbl = 0, nfor = 0;  // neighbour-run entries in LDS / foreign scans of this lane
+#endif
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
       if (!open[s] || !nd[s]) continue;
@@ -626,8 +629,14 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
       }
       if (nb >= 0) {
         nbs[s] = nb;
+#ifdef RK_SWEEP_PROF
+        nbl += ne - nb;
+#endif
         for (int u = nb; u < ne && ent[u] < i; ++u) rnb[s] |= (uint64_t)m32(q, pk[u]) << (u - nb);
       } else if (foreign) {
+#ifdef RK_SWEEP_PROF
+        ++nfor;
+#endif
         foreign_scan32(ax, g0, dir, k + dir, i, q, fs[s]);
       }
     }
@@ -854,6 +863,16 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
       }
       SP_ADD(9, mx);   // the longest deviation list of a lane
       SP_ADD(10, sm);  // deviations computed
+      uint32_t m2 = nbl, s2 = nbl, f2 = nfor;
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = __shfl_xor(m2, off);
+        m2 = o > m2 ? o : m2;
+        s2 += __shfl_xor(s2, off);
+        f2 += __shfl_xor(f2, off);
+      }
+      SP_ADD(11, m2);  // the longest LDS neighbour run of a lane
+      SP_ADD(12, s2);  // LDS neighbour entries tested
+      SP_ADD(13, f2);  // foreign neighbour scans
     }
 #endif
     return wp;
@@ -1539,8 +1558,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
       (void)hipStreamSynchronize(st);
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sweep_prof), sizeof h);
       const double w = h[6] ? (double)h[6] : 1.0;
-      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f one-slot windows %.3f | longest deviation list/win %.2f deviations/win %.2f\n",
-              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w, h[9] / w, h[10] / w);
+      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f one-slot windows %.3f | longest deviation list/win %.2f deviations/win %.2f | longest LDS neighbour run/win %.2f LDS neighbour entries/win %.2f foreign scans/win %.3f\n",
+              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w, h[9] / w, h[10] / w, h[11] / w, h[12] / w, h[13] / w);
       (void)hipMemsetAsync(g_sweep_prof_ptr(), 0, sizeof h, st);
     }
 #endif
