@@ -434,10 +434,13 @@ __device__ __forceinline__ void diffs32(const Q32 &q, uint2 o, uint32_t &dl, uin
   const int32_t d = (int32_t)(q.c - o.x);
   dc = (uint32_t)(d < 0 ? -d : d);
 }
+// (bitwise, not short-circuit: the `&&` form compiled to a branch around the
+// centre test of every candidate)
 __device__ __forceinline__ bool m32(const Q32 &q, uint2 o) {
   uint32_t dl, dc;
   diffs32(q, o, dl, dc);
-  return q.ok && dl <= q.tl && dc <= q.tc && !(q.eq && dl == q.tl && dc == q.tc);
+  const bool at_both = (dl == q.tl) & (dc == q.tc);
+  return q.ok & (dl <= q.tl) & (dc <= q.tc) & !(q.eq & at_both);
 }
 // deviation (SequenceOcupationList.cpp:20-31) from the same integer operands
 __device__ __forceinline__ double dev32(const Q32 &q, uint2 o, double lr, double pr) {
