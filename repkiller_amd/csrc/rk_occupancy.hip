@@ -205,24 +205,20 @@ __device__ __forceinline__ void set_bit(M128 &m, int u) {
 __device__ __forceinline__ bool any_and(const M128 &a, const M128 &b) {
   return ((a.lo & b.lo) | (a.hi & b.hi)) != 0;
 }
-// highest set bit <= P (-1 if none) / lowest set bit > P (128 if none)
+// highest set bit <= P (-1 if none) / lowest set bit > P (128 if none);
+// P is per lane (0..127): selects, no branches (both halves are cheap)
 __device__ __forceinline__ int hs_le(uint64_t s0, uint64_t s1, int P) {
-  if (P >= 64) {
-    const uint64_t m = s1 & ((2ull << (P - 64)) - 1ull);
-    if (m) return 127 - __clzll(m);
-    P = 63;
-  }
-  const uint64_t m = s0 & ((2ull << P) - 1ull);
-  return m ? 63 - __clzll(m) : -1;
+  const bool up = P >= 64;
+  const int p1 = (P - 64) & 63;
+  const uint64_t m1 = up ? s1 & ((2ull << p1) - 1ull) : 0ull;
+  const uint64_t m0 = s0 & (up ? ~0ull : (2ull << (P & 63)) - 1ull);
+  return m1 ? 127 - (int)__clzll(m1) : m0 ? 63 - (int)__clzll(m0) : -1;
 }
 __device__ __forceinline__ int ls_gt(uint64_t s0, uint64_t s1, int P) {
-  if (P < 64) {
-    const uint64_t m = s0 & ~((2ull << P) - 1ull);
-    if (m) return __builtin_ctzll(m);
-    return s1 ? 64 + __builtin_ctzll(s1) : 128;
-  }
-  const uint64_t m = s1 & ~((2ull << (P - 64)) - 1ull);
-  return m ? 64 + __builtin_ctzll(m) : 128;
+  const bool up = P >= 64;
+  const uint64_t m0 = up ? 0ull : s0 & ~((2ull << (P & 63)) - 1ull);
+  const uint64_t m1 = up ? s1 & ~((2ull << ((P - 64) & 63)) - 1ull) : s1;
+  return m0 ? (int)__builtin_ctzll(m0) : m1 ? 64 + (int)__builtin_ctzll(m1) : 128;
 }
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -397,14 +393,16 @@ __global__ void __launch_bounds__(256) k_sweep_tile(Axis ax, uint8_t *wpend, uin
 }
 
 // 64 bits of a 128-bit window mask starting at bit a (0 <= a < 128)
-// m << a as a 128-bit window mask (0 <= a < 128)
+// m << a as a 128-bit window mask (0 <= a < 128); selects, no branches
 __device__ __forceinline__ M128 shl128(uint64_t m, int a) {
-  if (a >= 64) return M128{0, m << (a - 64)};
-  return M128{m << a, a ? m >> (64 - a) : 0};
+  const int b = a & 63;
+  const uint64_t sh = m << b, carry = b ? m >> (64 - b) : 0ull;
+  return a >= 64 ? M128{0ull, sh} : M128{sh, carry};
 }
 __device__ __forceinline__ uint64_t bits_from(uint64_t lo, uint64_t hi, int a) {
-  if (a >= 64) return hi >> (a - 64);
-  return a ? (lo >> a) | (hi << (64 - a)) : lo;
+  const int b = a & 63;
+  const uint64_t hs = hi >> b, ls = b ? (lo >> b) | (hi << (64 - b)) : lo;
+  return a >= 64 ? hs : ls;
 }
 
 // ---- 32-bit fast path of the window sweep --------------------------------
@@ -736,7 +734,10 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
       const uint32_t o = __shfl_xor(cmax, off);
       cmax = o > cmax ? o : cmax;
     }
-    if (PAR && cmax >= 3) {
+#ifndef RK_DEV_PAR_MIN
+#define RK_DEV_PAR_MIN 3
+#endif
+    if (PAR && cmax >= RK_DEV_PAR_MIN) {
       uint32_t incl = ct;  // inclusive prefix of the pair counts
       for (int off = 1; off < 64; off <<= 1) {
         const uint32_t o = __shfl_up(incl, off);
