@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 3 mid refresh on HEAD: the driver's bench command (with the CPU leg), rocprof summary, PMC traffic passes,
+# cfg5 on one GPU, the ratio-pair batch, the heap killers.
+export TMPDIR=/tmp
+O=gpurun_out/r3ac
+mkdir -p $O
+timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o p -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $O/prof.log 2>&1 || exit 2
+bash tools/pmc_run.sh $O/pmc --no-cpu --steps 3 --warmup 1 || exit 3
+timeout -k 10 600 python3 bench.py --gpus 1 --config cfg5 --steps 3 --warmup 1 --no-cpu > $O/bench_cfg5.json 2> $O/bench_cfg5.err || exit 4
+timeout -k 10 600 python3 tools/pairs_bench.py > $O/pairs.json 2> $O/pairs.err || exit 5

@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """Regenerate DESIGN.md's kernel table from profiles/r3_bench.json (HIP-event
 timing inside bench.py's timed steps, cfg3), profiles/traffic.json
-(PMC HBM bytes, cfg3) and profiles/r2_bench_cfg5.json (the same timing at cfg5,
+(PMC HBM bytes, cfg3) and profiles/r3_bench_cfg5.json (the same timing at cfg5,
 one GPU) when present."""
 import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
-BENCH, CFG5 = "r3_bench.json", "r2_bench_cfg5.json"
+BENCH, CFG5 = "r3_bench.json", "r3_bench_cfg5.json"
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
     ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (4 processing-order passes, 8 + 7 + 7 + 7-bit digits at cfg3), 12-B records 7168 per tile (3 Y passes, 9 + 9 + 8 bits, after X: the first carries the X-hit bits, the last writes CSR + states; 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last order pass: 57; last Y pass: 30)"),
