@@ -939,8 +939,12 @@ __device__ __forceinline__ bool sweep_window32(const Axis &ax, uint32_t w, uint8
 #ifndef RK_SWEEP_WPE
 #define RK_SWEEP_WPE 8
 #endif
+#ifndef RK_SWEEP_WPE_PAR
+#define RK_SWEEP_WPE_PAR 7  // 71 VGPRs, no spills (neutral against 8 waves with 44 B of scratch)
+#endif
 template <bool PAR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RK_SWEEP_WPE)))
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(PAR ? RK_SWEEP_WPE_PAR : RK_SWEEP_WPE)))
 k_sweep_fast(Axis ax, uint8_t *wpend, uint32_t nwin, uint32_t *counters, uint8_t *lflag,
              uint8_t *rpend) {
   __shared__ uint2 s_pk[4][128 + OWN_U];  // {centre low 32 bits, length}; read padding
