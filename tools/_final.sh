@@ -6,6 +6,5 @@ O=gpurun_out/final
 mkdir -p $O
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 2
-tools/_refresh.sh > $O/refresh.log 2>&1 || exit 3
+bash tools/_refresh.sh $O/refresh > $O/refresh.log 2>&1 || exit 3
 timeout -k 10 600 python -u tools/cfg5_check.py --out $O/cfg5_check.json > $O/cfg5_check.log 2>&1 || exit 4
-timeout -k 10 400 python bench.py --config cfg5 --no-cpu --steps 3 --warmup 1 > $O/bench_cfg5.json 2> $O/bench_cfg5.err || exit 5
