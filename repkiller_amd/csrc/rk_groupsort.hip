@@ -477,9 +477,40 @@ __device__ void reg_batch(const V &v, bool in, int bl, uint32_t bm, int len, int
 // wavefront-parallel __unguarded_partition_pivot on [f, l); returns the cut
 template <bool GLOBAL, class V>
 __device__ uint32_t wave_partition(const V &v, uint32_t f, uint32_t l, uint32_t lane) {
-  if (lane == 0) median_to_first(v, f, l);
+  // __move_median_to_first by lane 0 with every read issued up front (the
+  // three candidates and the first slot, then the median's tag); the pivot
+  // (the median's key) reaches the other lanes by a lane read, not from memory
+  typename V::key_t p = 0;
+  if (lane == 0) {
+    const uint32_t a = f + 1, b = f + (l - f) / 2, c = l - 1;
+    const typename V::key_t ka = v.K[a], kb = v.K[b], kc = v.K[c], kf = v.K[f];
+    const uint32_t tf = v.T[f];
+    uint32_t m;
+    typename V::key_t km;
+    if (ka < kb) {
+      if (kb < kc) m = b, km = kb;
+      else if (ka < kc) m = c, km = kc;
+      else m = a, km = ka;
+    } else {
+      if (ka < kc) m = a, km = ka;
+      else if (kb < kc) m = c, km = kc;
+      else m = b, km = kb;
+    }
+    const uint32_t tm = v.T[m];
+    v.K[m] = kf;
+    v.T[m] = tf;
+    v.K[f] = km;
+    v.T[f] = tm;
+    p = km;
+  }
+  if (sizeof(p) == 8) {
+    const uint64_t p64 = (uint64_t)p;
+    p = (typename V::key_t)((uint64_t)(uint32_t)__shfl((int)(uint32_t)p64, 0) |
+                            (uint64_t)(uint32_t)__shfl((int)(uint32_t)(p64 >> 32), 0) << 32);
+  } else {
+    p = (typename V::key_t)(uint32_t)__shfl((int)(uint32_t)p, 0);
+  }
   sync_mem<GLOBAL>();
-  const typename V::key_t p = v.K[f];
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t nL = 0, nR = 0;
   for (uint32_t c = f; c < l; c += 64) {
