@@ -95,6 +95,10 @@ typedef struct {
                                does not pack into a record */
   double h2d_ms, d2h_ms;    /* rk_classify*: host wall time of the input upload and of the
                                result download (0 for the device entry points) */
+  uint32_t wire;            /* rk_classify*: 1 when the rows crossed PCIe as 12-B wire
+                               records (order + flag back, gids rebuilt on the host), 0
+                               when as the SoA */
+  uint32_t reserved;
 } rk_stats;
 
 int rk_create(rk_ctx **ctx, int device);

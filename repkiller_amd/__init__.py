@@ -88,7 +88,8 @@ class Stats(ctypes.Structure):
                 ("x_hits", ctypes.c_uint64), ("y_hits", ctypes.c_uint64),
                 ("device_ms", ctypes.c_double), ("pipeline", ctypes.c_uint32),
                 ("record_fallback", ctypes.c_uint32), ("h2d_ms", ctypes.c_double),
-                ("d2h_ms", ctypes.c_double)]
+                ("d2h_ms", ctypes.c_double), ("wire", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -1071,6 +1071,7 @@ static int classify_wire(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p
     rk::gids_from_flags(ctx, out[q].repval, out[q].n_out, out[q].gid);
   ctx->stats.h2d_ms = t1 - t0;
   ctx->stats.d2h_ms = rk::wall_ms() - t2;
+  ctx->stats.wire = 1;
   return RK_OK;
 }
 

@@ -347,6 +347,23 @@ def test_pipeline_choice(gpu_ctx, generic_ctx):
     assert gpu_ctx.stats()["pipeline"] == 2
 
 
+def test_wire_format_and_fallback(gpu_ctx):
+    """rk_classify's compact wire format (12-B rows up, output order + repeat
+    flag down, gids rebuilt on the host from the flags: a new group wherever
+    the flag is not 2, commonFunctions.cpp:101-115) on a set the record
+    pipeline takes, and the SoA upload for rows outside the wire bounds (a
+    length >= 2^24 here): both bit-exact with the oracle."""
+    f = rk.synth(30_000, 3_000_000, seed=71)
+    gpu_vs_oracle(gpu_ctx, f, 3_000_000, 3_000_000)
+    st = gpu_ctx.stats()
+    assert st["wire"] == 1 and st["pipeline"] == 1
+    g = rk.synth(30_000, 60_000_000, seed=72)
+    g.length[123] = np.uint64(1 << 24)  # beyond the wire's 24 length bits
+    gpu_vs_oracle(gpu_ctx, g, 60_000_000, 60_000_000)
+    st = gpu_ctx.stats()
+    assert st["wire"] == 0 and st["pipeline"] == 2
+
+
 def test_dense_x_chunks(gpu_ctx):
     """Dense X chunks (record pipeline): a chunk's rows are streamed in
     batches of 512 and its bins have no capacity limit, so even a single
