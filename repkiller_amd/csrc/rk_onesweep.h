@@ -36,9 +36,10 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 // 4 / 8 / 12 / 16 / 24: 6.09-6.22 / 6.11-6.25 / 6.15-6.29 / 6.18-6.31 /
 // 6.38-6.42 ms (RK_LIB builds, interleaved; the spread is the box's); with
 // the late-Y schedule, k_onesweep per step at 8 / 16: 4.157-4.173 /
-// 4.229-4.232 ms (three interleaved runs each, profiles/r3_lb_batch.json).
+// 4.229-4.232 ms (three interleaved runs each, profiles/r3_lb_batch.json);
+// later, 4 / 6 / 8 / 12: 4.138-4.141 / 4.138 / 4.151-4.155 / 4.191-4.193 ms.
 #ifndef RK_LB_BATCH
-#define RK_LB_BATCH 8
+#define RK_LB_BATCH 6
 #endif
 // RK_LB_SLEEP: s_sleep units between polls of unpublished tiles (0 / 1 / 4:
 // 12.09-12.10 / 12.12-12.14 / 12.10-12.18 ms, neutral)
