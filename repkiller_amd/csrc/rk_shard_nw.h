@@ -473,7 +473,12 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   }
   PartPlan ypp;
   ypp.mcache = S.take<uint32_t>(SL_YMASK, m + 1);  // the X-hit bytes follow the same masks
-  S.plan(yop, m, ypp);
+  if (P == 1) {  // one Y range, halos included: every record stays, count known
+    const uint64_t cnt1[1] = {m};
+    S.plan_counts(yop, m, ypp, cnt1);
+  } else {
+    S.plan(yop, m, ypp);
+  }
   // every own record stays here, once: the send layout is the records themselves
   const bool y_self = ypp.total == m && ypp.cnt[me] == m;
   if (!y_self) {
