@@ -798,7 +798,10 @@ __global__ void __launch_bounds__(64 * WPB) k_sort_groups_lds(TierLists tl, int 
 // segment's remaining depth budget, writing the segment's final order.
 // Together the two phases are the libstdc++ recursion exactly: sibling
 // segments are independent, and every segment keeps its own depth budget.
-constexpr uint32_t SPLIT_T = 512;
+#ifndef RK_SPLIT_T
+#define RK_SPLIT_T 512
+#endif
+constexpr uint32_t SPLIT_T = RK_SPLIT_T;
 constexpr int SPLIT_STACK = 72;  // one frame per level: 2 * log2(2^32) + slack
 
 __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint32_t *PR,
