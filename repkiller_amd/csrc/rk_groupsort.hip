@@ -304,6 +304,100 @@ __device__ void wave_sort_heap(const HeapMem &h, uint32_t n, uint32_t lane) {
   }
 }
 
+// __sort_heap of [0, n) when every key is equal -- the heap segment of a
+// median-of-three killer is exactly that: the adversary leaves the members it
+// never separated for the fallback.  No comparison is then true, so every
+// pop's descent is the right spine 0, 2, 6, .., 2^(j+1) - 2 while the hole has
+// two children (then the lone left child, `len` - 1, under the even-length
+// rule) and the displaced value stays where the descent ends: the descent's
+// slots shift up by one, the root leaves to `last`.  Spine slot j lives in
+// lane j; the descent's slots 0..m form a ring from lane `head` (re-linearised
+// by one shuffle when m shrinks, ~lg n times), so a pop is two lane reads and
+// two lane selects.  Every other position is read once, in descending order,
+// from two prefetched 64-position chunks.  Tags only: the keys are all equal.
+__device__ void wave_sort_heap_equal(uint32_t *T, uint32_t n, uint32_t lane) {
+  auto sp = [](uint32_t j) { return (2ull << j) - 2; };
+  uint32_t s = lane < 32 && sp(lane) < n ? T[sp(lane)] : 0u;
+  uint32_t L = n - 1, m = 0;
+  while (sp(m) < (L - 1) / 2) ++m;
+  uint32_t head = 0, pv = 0;
+  bool pend = false;  // the previous pop left its value at position L
+  // chunk [B - 63, B] holds L: the chunk's positions are in one register
+  // (position B - lane), the next two chunks' in two more, and the pops'
+  // outputs gather in ob (position B - lane), stored once per chunk -- a store
+  // per pop would make every lane read wait for it.  The three registers take
+  // turns (the loop below is unrolled by three), so a chunk's load lands in
+  // its own register a whole chunk of pops before it is read
+  int64_t B = L;
+  auto ld = [&](int64_t q) { return T[q >= 0 ? q : 0]; };  // below 0: never read
+  uint32_t ca = ld(B - lane), cb = ld(B - 64 - lane), cc = ld(B - 128 - lane), ob = 0;
+  // the spine arrives before the loop: left pending, every lane read of it in
+  // the loop would wait for all memory accesses in flight (the chunks' too)
+  __builtin_amdgcn_s_waitcnt(0);
+  auto chunk = [&](const uint32_t c0, const uint32_t c1) {  // pops L = B .. B - 63
+    auto at = [&](int64_t q) {
+      const int i = (int)(B - q);
+      return (uint32_t)(i < 64 ? __builtin_amdgcn_readlane((int)c0, i)
+                               : __builtin_amdgcn_readlane((int)c1, i - 64));
+    };
+    // A chunk with no event -- no shrink of the descent, no even-length rule,
+    // no spine slot among its positions, no value left by the previous pop --
+    // is a FIFO of delay m + 1: pop i outputs ring slot i (i <= m), else the
+    // value pop i - m - 1 re-inserted (chunk lane i - m - 1), and leaves the
+    // chunk's last m + 1 values as the ring.  Events come only near L = 2^k - 2
+    // (a few chunks per heap level); the other chunks take three shuffles.
+    const int64_t lo = B - 63;
+    const int64_t shrink_at = m > 0 ? (int64_t)(2 * sp(m - 1) + 2) : -1;
+    const int64_t special_at = (int64_t)(2 * sp(m) + 2);
+    const int kb = 31 - __clz((int)(B + 2));
+    const bool spine_in = ((1ll << kb) - 2) >= lo;
+    if (lo >= 1 && !pend && shrink_at < lo && !(special_at >= lo && special_at <= B) && !spine_in) {
+      const uint32_t mp1 = m + 1, hl = head + lane;
+      const uint32_t from_s = (uint32_t)__shfl((int)s, (int)(hl < mp1 ? hl : hl - mp1));
+      const uint32_t from_c = (uint32_t)__shfl((int)c0, (int)(lane - mp1) & 63);
+      const uint32_t ring = (uint32_t)__shfl((int)c0, (int)(64 - mp1 + lane) & 63);
+      ob = lane < mp1 ? from_s : from_c;
+      s = lane < mp1 ? ring : s;
+      head = 0;
+      L -= 64;
+    }
+    for (; L > 0 && B - L < 64; --L) {
+      while (m > 0 && sp(m - 1) >= (L - 1) / 2) {
+        s = (uint32_t)__shfl((int)s, lane <= m ? (int)((head + lane) % (m + 1)) : (int)lane);
+        head = 0;
+        --m;
+      }
+      uint32_t v;
+      if (pend) v = pv;
+      else if (((L + 2) & (L + 1)) == 0)  // a spine slot below the descent
+        v = (uint32_t)__builtin_amdgcn_readlane((int)s, 30 - __clz((int)(L + 2)));
+      else v = at(L);
+      const uint32_t root = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)head);
+      ob = lane == (uint32_t)(B - L) ? root : ob;
+      const bool special = (L & 1) == 0 && sp(m) == (L - 2) / 2;
+      const uint32_t bottom = special ? at(L - 1) : v;
+      s = lane == head ? bottom : s;
+      head = head == m ? 0 : head + 1;
+      pend = special;
+      pv = v;
+    }
+    if ((int64_t)lane < B - L) T[B - lane] = ob;  // positions B .. L + 1
+    B -= 64;
+  };
+  for (;;) {
+    chunk(ca, cb);
+    if (L == 0) break;
+    ca = ld(B - 128 - lane);
+    chunk(cb, cc);
+    if (L == 0) break;
+    cb = ld(B - 128 - lane);
+    chunk(cc, ca);
+    if (L == 0) break;
+    cc = ld(B - 128 - lane);
+  }
+  if (lane == 0) T[0] = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)head);
+}
+
 // The whole __partial_sort of segment [0, n) of K/T (global memory) by one
 // 256-thread block; its final tags go to out[0..n).
 __device__ void block_heap_sort(uint64_t *K, uint32_t *T, uint32_t n, uint32_t *out, uint64_t *lk,
@@ -314,6 +408,9 @@ __device__ void block_heap_sort(uint64_t *K, uint32_t *T, uint32_t n, uint32_t *
     __syncthreads();
     return;
   }
+  int neq = 0;
+  for (uint32_t x = tid; x < n; x += blockDim.x) neq |= K[x] != K[0];
+  const bool equal = __syncthreads_or(neq) == 0;
   {
     const uint32_t last_parent = (n - 2) / 2;
     for (int lv = 31 - __clz((int)(last_parent + 1)); lv >= 0; --lv) {
@@ -322,6 +419,13 @@ __device__ void block_heap_sort(uint64_t *K, uint32_t *T, uint32_t n, uint32_t *
       for (uint32_t x = a + tid; x <= e; x += blockDim.x)
         adjust_heap(GView{K, T, nullptr, nullptr, nullptr}, 0, x, n, K[x], T[x]);
       __syncthreads();
+    }
+    if (equal) {
+      if (tid < 64) wave_sort_heap_equal(T, n, tid);
+      __syncthreads();
+      for (uint32_t x = tid; x < n; x += blockDim.x) out[x] = T[x];
+      __syncthreads();
+      return;
     }
     for (uint32_t x = tid; x < n && x < HTOP; x += blockDim.x) lk[x] = K[x], lt[x] = T[x];
     __syncthreads();

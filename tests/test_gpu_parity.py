@@ -318,11 +318,15 @@ def test_std_sort_block_heapsort_vs_restatement(gpu_ctx):
     heap's top levels in LDS, the pops' descents 6 levels per round): killers
     whose heapsort segment is just above the block threshold, straddles the
     LDS-resident levels or spans 17 levels, over all-equal, heavily tied and
-    distinct keys, 32- and 64-bit."""
+    distinct keys, 32- and 64-bit (all-equal segments take the spine-ring
+    path, `wave_sort_heap_equal`)."""
     from sort_cases import heap_fallbacks, killer_with_keys
     segs = [killer_with_keys(2300, 1, 1), killer_with_keys(2300, 3, 2),
             killer_with_keys(8400, 3, 3), killer_with_keys(8400, 1 << 40, 4),
-            killer_with_keys(20000, 5, 5, base=1 << 40), killer_with_keys(70000, 1 << 20, 6)]
+            killer_with_keys(20000, 5, 5, base=1 << 40), killer_with_keys(70000, 1 << 20, 6),
+            # all-equal heap segments (the lane-ring path) of odd and even length
+            killer_with_keys(2301, 1, 7), killer_with_keys(33000, 1, 8),
+            killer_with_keys(33001, 1, 9, base=1 << 40), killer_with_keys(65601, 1, 10)]
     for s in segs:
         assert heap_fallbacks(s) > 0
     keys = np.concatenate(segs)

@@ -27,7 +27,7 @@ JOBS = [
     ("k_sort_groups_lds", "65..2048 members in LDS: partitions down to the leaves, then the final insertion pass with ballot-found leaf bounds (257..2048: second stream, first)", "16 per member"),
     ("k_sort_groups_split", "groups above 2048: block-wide partitions down to 512-member segments", "16 per member"),
     ("k_sort_segments", "those segments, one LDS wavefront each", "16 per member"),
-    ("k_heap_segments", "depth-exhausted segments of >= 2048 members (median-of-3 killers only): make_heap level-parallel, sort_heap by one wavefront, top 13 heap levels in LDS", "-"),
+    ("k_heap_segments", "depth-exhausted segments of >= 2048 members (median-of-3 killers only): make_heap level-parallel; sort_heap by one wavefront: all-equal keys (the killer) as a spine FIFO, else top 13 heap levels in LDS", "-"),
     ("k_emit", "gid, flag, output order", "29"),
 ]
 
