@@ -20,8 +20,10 @@ max time over ranks is reported.
 
 Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the kernel with the
 most device time per step (algorithmic bytes per launch / HIP-event launch time
-measured inside the timed steps; PMC HBM traffic from profiles/traffic.json),
-`kernels` (the same per kernel),
+measured inside the timed steps -- only that kernel's launches carry events
+there, so the timers cost the step little; PMC HBM traffic from
+profiles/traffic.json), `kernels` (every kernel, from PROFILED_STEPS further
+steps with every launch timed, after the timed region),
 `cpu_baseline` (the reference built from its sources, oracle/_ref/ref_driver, on
 a bounded sample, 1 core), `phases_ms` (per-step device time per phase).
 """
@@ -222,12 +224,22 @@ def roofline_of(kt: dict, steps: int, config: str):
     return kernels, roofline
 
 
+# the record pipeline's dominant kernel (DESIGN.md kernel table): the one
+# kernel whose launches carry HIP events inside the timed steps
+ROOFLINE_KERNEL = "k_onesweep"
+PROFILED_STEPS = 3  # steps after the timed region with every launch timed
+
+
 def timed(step, args, world, ctx):
-    """W untimed steps, then K timed steps (launch-level profiling on) between
-    barriers + device syncs."""
+    """W untimed steps, then K timed steps between barriers + device syncs
+    (phase events and the roofline kernel's launch events on; RK_BENCH_NOPROF=1
+    turns them off, RK_BENCH_ALLPROF=1 times every launch there instead)."""
     for _ in range(args.warmup):
         step()
-    ctx.set_profiling(not os.environ.get("RK_BENCH_NOPROF"))  # A/B of the timers' own cost
+    if os.environ.get("RK_BENCH_NOPROF"):
+        ctx.set_profiling(False)
+    else:
+        ctx.set_profiling(True, None if os.environ.get("RK_BENCH_ALLPROF") else ROOFLINE_KERNEL)
     ctx.reset_phases()
     torch.cuda.synchronize()
     barrier(world)
@@ -240,6 +252,30 @@ def timed(step, args, world, ctx):
     dt = time.perf_counter() - t0
     ctx.set_profiling(False)
     return out, dt
+
+
+def kernel_tables(step, args, ctx, config: str):
+    """`roofline` from the timed steps' launch events (read before this is
+    called: ctx.kernel_timing() right after timed()) and the `kernels` table
+    from PROFILED_STEPS more steps with every launch timed."""
+    kt_timed = ctx.kernel_timing()
+    _, roofline = roofline_of(kt_timed, args.steps, config)
+    ctx.set_profiling(True)
+    ctx.reset_phases()
+    for _ in range(PROFILED_STEPS):
+        step()
+    torch.cuda.synchronize()
+    ctx.set_profiling(False)
+    kernels, roof_all = roofline_of(ctx.kernel_timing(), PROFILED_STEPS, config)
+    if roof_all and (not roofline or roofline["kernel"] != roof_all["kernel"]):
+        # another kernel dominates (e.g. the generic pipeline ran): its figures
+        # come from the profiled steps
+        roof_all["timed_in"] = f"{PROFILED_STEPS} profiled steps after the timed region"
+        roofline = roof_all
+    elif roofline:
+        roofline["timed_in"] = ("the timed steps (every launch timed)" if os.environ.get("RK_BENCH_ALLPROF")
+                                else "the timed steps (this kernel's launches only)")
+    return kernels, roofline
 
 
 def upload(f, dev):
@@ -270,8 +306,7 @@ def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
     frags_total, dt_max = aggregate(world, n, dt)
     st = rk.shard_stats(ctx)
     sent = allsum(world, float(st["bytes_sent"]))
-    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps,
-                                    f"{args.config}-sharded-x{world}")
+    kernels, roofline = kernel_tables(step, args, ctx, f"{args.config}-sharded-x{world}")
     comm.close()
     value = frags_total * args.steps / dt_max
     n_all = int(frags_total)
@@ -348,7 +383,7 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
     frags_total, dt_max = aggregate(world, n, dt)
     phases = ctx.phases()
     st = ctx.stats()
-    kernels, roofline = roofline_of(ctx.kernel_timing(), args.steps, args.config)
+    kernels, roofline = kernel_tables(step, args, ctx, args.config)
 
     # host-to-host rate (host SoA in, host results out: rk_classify), reported
     # beside value, never as it (SURVEY.md §8d's PCIe-inclusive timed region)

@@ -247,6 +247,9 @@ enum {
   RK_PH_EMIT = 9,       /* repeat flags + output order */
   RK_N_PHASES = 10
 };
+/* enable: 0 off; 1 phase events and every kernel launch timed; 2 + k: phase
+ * events and only kernel k's launches (rk_kernel_name(k)) -- the others record
+ * no events, so a timed run pays for few of them. */
 int rk_set_profiling(rk_ctx *ctx, int enable);
 int rk_get_phase_ms(const rk_ctx *ctx, double *ms /* [RK_N_PHASES] */,
                     uint32_t *calls /* nullable */);

@@ -388,8 +388,15 @@ class Context:
         'generic' (rk_set_pipeline)."""
         _check(load_library().rk_set_pipeline(self._h, {"auto": 0, "generic": 1}[pipeline]))
 
-    def set_profiling(self, on: bool = True) -> None:
-        _check(load_library().rk_set_profiling(self._h, int(on)))
+    def set_profiling(self, on: bool = True, only: str | None = None) -> None:
+        """Phase events and launch timing on/off; `only` = a kernel name
+        (rk_kernel_name) restricts the launch timing to that kernel."""
+        lib = load_library()
+        mode = int(bool(on))
+        if on and only:
+            names = [lib.rk_kernel_name(k).decode() for k in range(lib.rk_kernel_count())]
+            mode = 2 + names.index(only)
+        _check(lib.rk_set_profiling(self._h, mode))
 
     def reset_phases(self) -> None:
         _check(load_library().rk_reset_phases(self._h))

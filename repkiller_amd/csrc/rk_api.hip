@@ -901,7 +901,9 @@ extern "C" const char *rk_last_error(const rk_ctx *ctx) { return ctx ? ctx->err.
 
 extern "C" int rk_set_profiling(rk_ctx *ctx, int enable) {
   if (!ctx) return RK_E_ARG;
+  if (enable >= 2 + rk::KID_COUNT) return RK_E_ARG;
   ctx->profiling = enable != 0;
+  ctx->kt.only = enable >= 2 ? enable - 2 : -1;  // 2 + k: kernel k's launches only
   return RK_OK;
 }
 

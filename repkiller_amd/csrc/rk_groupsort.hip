@@ -1331,9 +1331,9 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   // algorithmic bytes of every tier (timing only): each member's (key, tag)
   // read, its tag written once at its final slot -- 16 B x the tier's members,
   // filled in from bm when the timings are collected
-  if (timing) g_ktimer->tier_counts = bm;
+  if (timing && g_ktimer->only < 0) g_ktimer->tier_counts = bm;  // read back at collection
   auto tier_slot = [&](int u) {
-    if (timing && g_ktimer->n > 0) g_ktimer->tier_slot[u] = g_ktimer->n - 1;
+    if (timing && g_ktimer->only < 0 && g_ktimer->n > 0) g_ktimer->tier_slot[u] = g_ktimer->n - 1;
   };
   (void)host_words;
   // fixed grids: every kernel reads its list range on the device

@@ -77,15 +77,19 @@ struct KernelTimer {
   const uint32_t *tier_counts;  // [tier][nblk] members per block, or null
   uint32_t tier_nblk;
   int tier_slot[TIERS];         // timer slot of each tier's launch (-1: none)
+  int only = -1;                // >= 0: time only this kernel's launches (rk_set_profiling)
 };
 extern thread_local KernelTimer *g_ktimer;
-inline void kt_begin(hipStream_t st) {
+// (a launch site that names its kernel in kt_begin stays timed when the timer
+// is restricted to that kernel; the others record no events then)
+inline void kt_begin(hipStream_t st, int kid = -1) {
   KernelTimer *t = g_ktimer;
-  if (t && t->n < KernelTimer::MAX) (void)hipEventRecord(t->ev[2 * t->n], st);
+  if (t && t->n < KernelTimer::MAX && (t->only < 0 || t->only == kid))
+    (void)hipEventRecord(t->ev[2 * t->n], st);
 }
 inline void kt_end(hipStream_t st, int kid, double bytes) {
   KernelTimer *t = g_ktimer;
-  if (t && t->n < KernelTimer::MAX) {
+  if (t && t->n < KernelTimer::MAX && (t->only < 0 || t->only == kid)) {
     (void)hipEventRecord(t->ev[2 * t->n + 1], st);
     t->kid[t->n] = kid;
     t->bytes[t->n] = bytes;

@@ -913,7 +913,7 @@ void launch_pass(const Src &src, const Dst &dst, uint32_t n, int shift, int db,
                  const uint32_t *ghist, uint32_t *status, uint32_t *ctr, hipStream_t st,
                  double bytes, uint32_t *clear_next = nullptr) {
   if (!n) return;
-  kt_begin(st);
+  kt_begin(st, KID_ONESWEEP);
   switch (db) {
     case 7: launch_pass_db<7>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
     case 8: launch_pass_db<8>(src, dst, n, shift, ghist, status, ctr, st, clear_next); break;
