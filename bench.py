@@ -14,9 +14,9 @@ over the 3 Gbp genome (rank r holds rows [r*50M, (r+1)*50M), each block seeded
 (xStart/10 slices, X/Y halo exchange, cross-slice roots, gid-range member sort;
 DESIGN.md "Multi-GPU") -- weak scaling.  The same run first measures
 `replicas`: every rank classifies its own independent 50M set (no data-path
-collective), reported beside the value (and as the value if the sharded leg
-fails, with the error).  A gloo barrier brackets every timed region and the
-max time over ranks is reported.
+collective), reported beside the value under `replicas`, never as it: if the
+sharded leg fails, `value` is null and the error is reported.  A gloo barrier
+brackets every timed region and the max time over ranks is reported.
 
 Rank 0 prints ONE JSON line.  Extra keys: `roofline` for the kernel with the
 most device time per step (algorithmic bytes per launch / HIP-event launch time
@@ -24,8 +24,12 @@ measured inside the timed steps -- only that kernel's launches carry events
 there, so the timers cost the step little; PMC HBM traffic from
 profiles/traffic.json), `kernels` (every kernel, from PROFILED_STEPS further
 steps with every launch timed, after the timed region),
-`cpu_baseline` (the reference built from its sources, oracle/_ref/ref_driver, on
-a bounded sample, 1 core), `phases_ms` (per-step device time per phase).
+`cpu_baseline` (1 core of this host: the in-repo restatement on the SAME
+arrays the GPU classified, result compared; the reference itself,
+oracle/_ref/ref_driver, on a bounded sample beside it), `parity` (the timed
+steps' result digest against the reference's, tests/golden/large_hashes.json),
+`host_to_host_fragments_per_s` (rk_classify from host buffers, PCIe included),
+`phases_ms` (per-step device time per phase).
 """
 from __future__ import annotations
 
@@ -119,45 +123,109 @@ def aggregate(world: int, n_local: int, dt_local: float) -> tuple[float, float]:
     return allsum(world, float(n_local)), allmax(world, dt_local)
 
 
-def cpu_baseline(cfg: dict, seconds_hint: float) -> dict | None:
+def reference_sample(cfg: dict, seconds_hint: float) -> dict | None:
     """The reference (oracle/_ref/ref_driver, built from /root/reference/src by
     oracle/ref.mk) on a bounded sample of the same workload: the cfg3 density
-    (fragments per bp) at 1/10 of the genome, so ~10-30 s of single-core work.
-    Falls back to the in-repo restatement (oracle/_build/rk_oracle, "port")."""
+    (fragments per bp) at 1/10 of the genome, so ~5-30 s of single-core work."""
     from oracle import rk_oracle as ro
-    ref = ro.REF_DRIVER if os.path.exists(ro.REF_DRIVER) else None
-    binary = ref or (ro.CLI if os.path.exists(ro.CLI) else None)
-    if binary is None:
-        try:
-            ro.build_oracle()
-            binary = ro.CLI
-        except Exception:
-            return None
+    if not os.path.exists(ro.REF_DRIVER):
+        return None
     scale = 10 if cfg["n"] >= 10_000_000 else 1
     n, L = cfg["n"] // scale, cfg["genome_len"] // scale
     f = rk.synth(n, L, seed=3)
     with tempfile.TemporaryDirectory() as d:
         inp = os.path.join(d, "sample.csv")
         rk.write_input_csv(inp, f, L, L)
-        out = "-" if ref else os.path.join(d, "out.csv")
-        p = subprocess.run([binary, inp, out, "0.3", "0.3"], capture_output=True, text=True,
-                           timeout=max(120.0, seconds_hint * 10))
+        p = subprocess.run([ro.REF_DRIVER, inp, "-", "0.3", "0.3"], capture_output=True,
+                           text=True, timeout=max(120.0, seconds_hint * 10))
     if p.returncode != 0:
         return None
     t = json.loads(p.stderr.strip().splitlines()[-1])
-    hot = t["group_s"] + t["diag_sort_s"] if ref else t["classify_s"]
-    cpu = subprocess.run(["sh", "-c", "grep -m1 'model name' /proc/cpuinfo | cut -d: -f2"],
-                         capture_output=True, text=True).stdout.strip()
-    out = {"value": round(n / hot, 1), "unit": "fragments/s", "cores": 1,
-           "kind": "reference" if ref else "port",
-           "sample": f"{n} fragments over {L} bp (cfg3 density, 1/{scale} of the genome), "
-                     f"ratios 0.3/0.3; timed region generate_fragment_groups + "
-                     f"generate_diagonal_func + sort_groups ({hot:.2f} s); host: {cpu}"}
+    hot = t["group_s"] + t["diag_sort_s"]
+    return {"value": round(n / hot, 1), "unit": "fragments/s", "cores": 1, "kind": "reference",
+            "sample": f"{n} fragments over {L} bp ("
+                      + (f"the config's density, 1/{scale} of the genome" if scale > 1
+                         else "the config's own size") + "), "
+                      f"ratios 0.3/0.3; timed region generate_fragment_groups + "
+                      f"generate_diagonal_func + sort_groups ({hot:.2f} s); host: {host_cpu()}"}
+
+
+def host_cpu() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg: dict, seconds_hint: float, same_input=None) -> dict | None:
+    """CPU baseline on this host, 1 core.
+
+    value: the in-repo restatement (oracle/rk_oracle.c, "port") timed on the SAME
+    arrays the GPU classified (same_input = (Frags, L, gpu result digest)), its
+    result compared with the GPU's.  Beside it: the reference itself on a
+    bounded sample (`reference_sample`), the reference's full-size rate from the
+    build container (`full_size`), and the restatement / reference time ratio on
+    the same full cfg3 input (tests/golden/large_hashes.json) that converts the
+    port's rate into a reference-equivalent one."""
+    from oracle import rk_oracle as ro
+    out = None
+    if same_input is not None:
+        f, L, gpu_digest = same_input
+        t0 = time.perf_counter()
+        rc, gid, rep, order, _ = ro.classify(f.x_start, f.y_start, f.length, f.strand, L, L,
+                                             0.3, 0.3)
+        dt = time.perf_counter() - t0
+        ratio = port_reference_ratio(cfg)
+        out = {"value": round(f.n / dt, 1), "unit": "fragments/s", "cores": 1, "kind": "port",
+               "sample": f"the full {f.n}-fragment input the GPU classified (same arrays, same "
+                         f"host), ratios 0.3/0.3; oracle/rk_oracle.c restatement, one thread "
+                         f"({dt:.2f} s); host: {host_cpu()}",
+               "same_result_as_gpu": bool(rc == 0 and arrays_sha256(order, gid, rep) == gpu_digest)}
+        if ratio:
+            out["port_over_reference_time"] = ratio
+            out["reference_equivalent_value"] = round(f.n / dt * ratio, 1)
+    sample = reference_sample(cfg, seconds_hint)
     full = full_size_reference(cfg)
-    if full:
-        full["sample_over_full"] = round(out["value"] / full["value"], 2)
+    if sample and full:
+        sample["sample_over_full"] = round(sample["value"] / full["value"], 2)
+    if out is None:
+        out = sample
+    elif sample:
+        out["reference_sample"] = sample
+    if out is not None and full:
         out["full_size"] = full
     return out
+
+
+def port_reference_ratio(cfg: dict):
+    """restatement time / reference time on the same full input, both measured
+    in the build container (tests/golden/large_hashes.json)."""
+    e = large_entry(cfg)
+    if not e or "oracle_classify_s" not in e or "ref_timing" not in e:
+        return None
+    t = e["ref_timing"]
+    return round(e["oracle_classify_s"] / (t["group_s"] + t["diag_sort_s"]), 3)
+
+
+def large_entry(cfg: dict):
+    name = next((k for k, v in CONFIGS.items() if v is cfg), None)
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "large_hashes.json")) as fh:
+            return json.load(fh).get(name or "")
+    except (OSError, ValueError):
+        return None
+
+
+def arrays_sha256(*arrs) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).view(np.uint8).data)
+    return h.hexdigest()
 
 
 def full_size_reference(cfg: dict) -> dict | None:
@@ -165,18 +233,14 @@ def full_size_reference(cfg: dict) -> dict | None:
     by tests/golden/make_golden_large.py (the reference binary classifying the
     full cfg3 CSV in the build container, 1 core): the sample's rate overstates
     it, since the reference's per-fragment cost grows with the set's size."""
-    name = next((k for k, v in CONFIGS.items() if v is cfg), None)
-    try:
-        with open(os.path.join(ROOT, "tests", "golden", "large_hashes.json")) as fh:
-            t = json.load(fh).get(name or "", {}).get("ref_timing")
-    except (OSError, ValueError):
-        return None
+    e = large_entry(cfg)
+    t = e.get("ref_timing") if e else None
     if not t:
         return None
     hot = t["group_s"] + t["diag_sort_s"]
     return {"value": round(t["frags"] / hot, 1), "unit": "fragments/s", "cores": 1,
             "kind": "reference",
-            "sample": f"the full {name} set ({t['frags']} fragments), timed region "
+            "sample": f"the full set ({t['frags']} fragments), timed region "
                       f"generate_fragment_groups + generate_diagonal_func + sort_groups "
                       f"({hot:.1f} s), measured in the build container "
                       f"(tests/golden/large_hashes.json ref_timing), not on this host"}
@@ -373,7 +437,10 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
     gid = torch.empty(n, dtype=torch.int32, device=dev)
     rep = torch.empty(n, dtype=torch.uint8, device=dev)
     order = torch.empty(n, dtype=torch.int32, device=dev)
-    del f
+    # the host arrays stay for the same-input CPU baseline (rank 0, one GPU)
+    keep_host = rank == 0 and world == 1 and not args.no_cpu and n <= 50_000_000
+    if not keep_host:
+        del f
 
     def step():
         return ctx.classify_device(x, y, ln, s, gid, rep, order, L, L, args.len_ratio,
@@ -392,7 +459,22 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
         host = host_legs(ctx, x, y, ln, s, L, args)
     per_step = {k: v[0] / max(1, v[1]) for k, v in phases.items()}
     value = frags_total * args.steps / dt_max
-    return {
+    # the result of the timed steps, digested (tests/test_large_configs.py's
+    # definition) and compared with the REFERENCE's result for this input where
+    # tests/golden/large_hashes.json pins it (cfg3: seed 3 = rank 0's set)
+    digest = arrays_sha256(order[:n_out].cpu().numpy().view(np.uint32),
+                           gid[:n_out].cpu().numpy().view(np.uint32), rep[:n_out].cpu().numpy())
+    e = large_entry(cfg)
+    pinned = (e is not None and e.get("synth", {}).get("seed") == rank_seed(rank)
+              and e["synth"].get("n") == n and e["synth"].get("genome_len") == L
+              and not cfg.get("synth"))
+    parity = {"result_sha256": digest,
+              "matches_reference_digest": (digest == e["result_sha256"]) if pinned else None,
+              "pinned_by": ("tests/golden/large_hashes.json (the reference's output for this "
+                            "input, reproduced byte-exact as CSV by test_cfg3_reference_csv)"
+                            if pinned else "no reference digest for this input")}
+    same_input = (f, L, digest) if keep_host else None
+    line = {
         "metric": METRIC,
         "value": round(value, 1),
         "unit": "fragments/s",
@@ -416,9 +498,11 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
         "device_ms_per_step": round(st["device_ms"], 3),
         "groups": n_groups, "grouped_fragments": n_out,
         "sweeps": {"x": st["x_sweeps"], "y": st["y_sweeps"], "jump_rounds": st["jump_rounds"]},
-        "pcie_inclusive_fragments_per_s": host["pageable"]["fragments_per_s"] if host else None,
+        "host_to_host_fragments_per_s": host["pageable"]["fragments_per_s"] if host else None,
         "host_to_host": host,
+        "parity": parity,
     }
+    return line, same_input
 
 
 def main():
@@ -432,8 +516,8 @@ def main():
     ap.add_argument("--pos-ratio", type=float, default=0.3)
     ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "sharded"],
                     help="auto: N=1 the single-GPU path, N>1 one fragment set sharded over the "
-                         "GPUs (independent replicas beside it, and the value if the sharded "
-                         "leg fails); replicas / sharded: that leg only")
+                         "GPUs (independent replicas beside it; value null if the sharded leg "
+                         "fails); replicas / sharded: that leg only")
     ap.add_argument("--sharded-timeout", type=float, default=240.0,
                     help="seconds the sharded leg may take before the line is printed without it")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
@@ -463,10 +547,11 @@ def main():
                 "hbm_algorithmic_GBps": sh["hbm_algorithmic_GBps"],
                 "roofline": sh["roofline"], "sharded": sh}
 
+    same_input = None
     if args.mode == "sharded":
         line = sharded_line(bench_sharded(args, cfg, rank, world, local, dev, ctx))
     else:
-        line = bench_single(args, cfg, rank, world, dev, ctx)
+        line, same_input = bench_single(args, cfg, rank, world, dev, ctx)
         if world > 1 and args.mode == "auto":
             # N > 1: the value is ONE comparison sharded over the GPUs (xStart/10
             # slices, RCCL exchanges); the independent replicas measured above
@@ -476,6 +561,8 @@ def main():
 
             def give_up():
                 if rank == 0:
+                    line["replicas"] = {"value": line["value"], "ms_per_step": line["ms_per_step"]}
+                    line["value"] = line["ms_per_step"] = line["roofline"] = None
                     line["sharded"] = {"error": f"timeout after {args.sharded_timeout} s"}
                     line["cpu_baseline"] = None
                     print(json.dumps(line), flush=True)
@@ -485,11 +572,22 @@ def main():
             dog.start()
             try:
                 sh = bench_sharded(args, cfg, rank, world, local, dev, ctx)
-            except Exception as e:  # noqa: BLE001 -- reported; the replicas line stands
+            except Exception as e:  # noqa: BLE001 -- reported with a null value
                 sh = {"error": repr(e)}
             dog.cancel()
             if "error" in sh:
+                # the sharded leg IS the N > 1 metric: no number for it; the
+                # independent replicas stay beside the null value, never as it
+                replicas = {k: line[k] for k in ("value", "ms_per_step", "scaling", "roofline",
+                                                 "phases_ms", "data")}
+                replicas["parallelism"] = line["config"]["parallelism"]
+                line["value"] = None
+                line["ms_per_step"] = None
+                line["hbm_algorithmic_GBps"] = None
+                line["roofline"] = None
+                line["config"]["parallelism"] = f"sharded x{world} ({args.comm}): FAILED"
                 line["sharded"] = sh
+                line["replicas"] = replicas
             else:
                 replicas = {k: line[k] for k in ("value", "ms_per_step", "scaling", "roofline",
                                                  "phases_ms", "data")}
@@ -499,7 +597,8 @@ def main():
     if rank != 0:
         return
     if not args.no_cpu and world == 1:
-        line["cpu_baseline"] = cpu_baseline(cfg, line["ms_per_step"] / 1e3 * args.steps)
+        line["cpu_baseline"] = cpu_baseline(cfg, line["ms_per_step"] / 1e3 * args.steps,
+                                            same_input)
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)

@@ -44,7 +44,8 @@ typedef enum {
   RK_E_NOMEM = -6,
   RK_E_HIP = -7,         /* a HIP runtime call failed; see rk_last_error */
   RK_E_NODEVICE = -8,    /* no usable gfx950 device */
-  RK_E_TOO_MANY = -9,    /* n >= 2^32 - 1 (32-bit row ids) */
+  RK_E_TOO_MANY = -9,    /* n >= 2^32 - 1 (32-bit row ids); rk_classify_sharded: one rank's
+                            Y range or gid range holds >= 2^30 records (30-bit pass counts) */
   RK_E_INTERNAL = -10,   /* a device-side consistency check failed */
   RK_E_PEER = -11,       /* rk_classify_sharded*: another rank of the comm failed; every
                             rank returns an error together (rk_last_error names the rank) */
@@ -208,6 +209,8 @@ typedef struct {
   uint32_t root_rounds;      /* cross-rank root resolution rounds */
   uint64_t bytes_sent;       /* payload bytes this rank sent */
   double ms_total, ms_ingress, ms_x, ms_y, ms_roots, ms_members; /* host wall */
+  uint32_t generic_driver;   /* 1: the generic driver ran (a row outside the 16-B record
+                                or a slice of >= 2^30 rows, or RK_SHARD_GENERIC=1) */
 } rk_shard_stats;
 
 /* in_dev: this rank's block of input rows (device SoA, FILE order); blocks are

@@ -120,7 +120,7 @@ class ShardStats(ctypes.Structure):
                 ("bytes_sent", ctypes.c_uint64), ("ms_total", ctypes.c_double),
                 ("ms_ingress", ctypes.c_double), ("ms_x", ctypes.c_double),
                 ("ms_y", ctypes.c_double), ("ms_roots", ctypes.c_double),
-                ("ms_members", ctypes.c_double)]
+                ("ms_members", ctypes.c_double), ("generic_driver", ctypes.c_uint32)]
 
 
 class SynthParams(ctypes.Structure):

@@ -39,6 +39,7 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
     "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32", "k_nw_order_hist",
     "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign", "k_nw_xcount", "k_nw_x_bits",
+    "k_heap_segments",
 };
 }  // namespace rk
 

@@ -263,7 +263,7 @@ void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, u
                ulonglong2 *rec, uint32_t *kept, uint32_t *err, hipStream_t st) {
   if (f.n)
   {
-    kt_begin(st);
+    kt_begin(st, KID_PREP);
     k_prep_keys<<<grid_for(f.n, 256, 2048), 256, 0, st>>>(f, vsize, max_x, max_y, pkey, rec, kept,
                                                            err);
     kt_end(st, KID_PREP, (rec ? 61.0 : 29.0) * f.n);  // x, y, len, strand in; key (+ 32-B record) out
@@ -272,19 +272,19 @@ void prep_keys(const Frags &f, uint64_t vsize, uint64_t max_x, uint64_t max_y, u
 void gather_proc(const Frags &f, Proc p, uint32_t m, uint32_t nbx, uint32_t nby, hipStream_t st) {
   if (!m) return;
   (void)f;
-  kt_begin(st);
+  kt_begin(st, KID_GATHER);
   k_gather_proc<<<grid_for(m, 256), 256, 0, st>>>(p, m, nbx, nby);
   kt_end(st, KID_GATHER, 84.0 * m);  // row + record in; ys, xrec, yrec, keyx, keyy out
 }
 void sort_keys(Proc p, uint32_t m, uint32_t *wide, hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_SORT_KEYS);
   k_sort_keys<<<grid_for(m, 256), 256, 0, st>>>(p, m, wide);
   kt_end(st, KID_SORT_KEYS, 32.0 * m);  // key, yStart, row in; (sort key, row) out
 }
 void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_CSR_FILL_X);
   k_csr_fill_x<<<grid_for(m, 256), 256, 0, st>>>(c, xrec, m, max_index);
   // id + record in; (centre, length,) packed record, neighbour code, state out
   kt_end(st, KID_CSR_FILL_X, (c.cen ? 46.0 : 30.0) * m);
@@ -292,14 +292,14 @@ void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, h
 void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
                 uint64_t max_index, hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_CSR_FILL_Y);
   k_csr_fill_y<<<grid_for(m, 256), 256, 0, st>>>(c, yrec, ylenhi, m, max_index);
   // id, Y record in; (centre, length,) packed record, neighbour code, state out
   kt_end(st, KID_CSR_FILL_Y, (c.cen ? 46.0 : 30.0) * m);
 }
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st) {
-  kt_begin(st);
+  kt_begin(st, KID_GROUP_OFFSETS);
   if ((reinterpret_cast<uintptr_t>(sgid) & 15) == 0)
     k_group_offsets<<<grid_for((m + 3) / 4, 256, 16384), 256, 0, st>>>(sgid, m, ngroups, goff);
   else
@@ -309,20 +309,20 @@ void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t 
 void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
                 hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_JUMP);
   k_jump<<<grid_for(m, 256, (size_t)1 << 20), 256, 0, st>>>(p, m, changed, isnew, err);
   kt_end(st, KID_JUMP, (isnew ? 16.0 : 12.0) * m);  // parent, root, parent written (+ new flag)
 }
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_ASSIGN_GID);
   k_assign_gid<<<grid_for(m, 256), 256, 0, st>>>(p, m, newrank);
   kt_end(st, KID_ASSIGN_GID, 12.0 * m);  // root, root's rank in; gid out
 }
 void build_records(uint32_t *gmem, const ulonglong2 *hrec, uint32_t m, uint64_t *key,
                    uint32_t *tag, hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_BUILD_RECORDS);
   k_build_records<<<grid_for(m, 256), 256, 0, st>>>(gmem, hrec, m, key, tag);
   kt_end(st, KID_BUILD_RECORDS, 36.0 * m);  // member, (key, row) in; key, tag, row out
 }
@@ -330,7 +330,7 @@ void emit_result(const uint32_t *otag, const uint32_t *sgid, const uint32_t *gof
                  const uint32_t *mrow, uint32_t m, uint32_t *out_gid, uint8_t *out_rep,
                  uint32_t *out_order, hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_EMIT);
   k_emit<<<grid_for(m, 256), 256, 0, st>>>(otag, sgid, goff, mrow, m, out_gid, out_rep,
                                            out_order);
   kt_end(st, KID_EMIT, 29.0 * m);  // slot, gid, group bounds, row in; gid, flag, order out

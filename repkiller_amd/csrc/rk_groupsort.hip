@@ -167,6 +167,12 @@ __device__ void heap_sort_segment(const V &v, uint32_t f, uint32_t l) {
 //    above its slot are written.
 constexpr uint32_t HEAP_BLOCK_MIN = 2048;  // smaller exhausted segments: one thread
 constexpr int HLV = 13;                    // heap levels in LDS
+// k_heap_segments keeps the heap's top HLV levels in LDS: (2^13 - 1) x (8 + 4)
+// B = 96 KB of static LDS, which needs gfx950's 160 KB per workgroup (64 KB
+// on gfx942 / gfx90a)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "rk_groupsort.hip: k_heap_segments needs gfx950 (160 KB of LDS per workgroup)"
+#endif
 constexpr uint32_t HTOP = (1u << HLV) - 1;
 constexpr int HR = 6;                      // levels per descent round (126 nodes)
 constexpr uint32_t HR_LAST = (1u << HR) - 2, HR_NODES = (2u << HR) - 2;  // 62, 126
@@ -1375,7 +1381,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     const uint32_t waves = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
     const int wp = cap <= 512 ? wpb : 1;
     const size_t slab = (lds_bytes(cap, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
-    kt_begin(sj);
+    kt_begin(sj, KID_SORT_LDS);
     if (wp == 4) {
       if (narrow_keys)
         k_sort_groups_lds<uint32_t, 4><<<waves / 4, 256, 4 * slab, sj>>>(
@@ -1396,11 +1402,11 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   };
   const int big0 = side ? NLDS - lds_big : NLDS;  // tiers [big0, NLDS) go first on side
   for (int j = NLDS - 1; j >= big0; --j) launch_lds(j, s2);
-  kt_begin(s2);
+  kt_begin(s2, KID_SORT_SMALL);
   k_sort_small<<<2048, 256, 0, s2>>>(tl, goff, key, tag, otag);
   kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
   tier_slot(0);
-  kt_begin(s2);
+  kt_begin(s2, KID_SORT_REG);
   k_sort_groups_reg<2><<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
   kt_end(s2, KID_SORT_REG, 0.0);
   tier_slot(1);
@@ -1413,7 +1419,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     return e ? atoi(e) : 1;
   }();
   auto launch_reg1 = [&](hipStream_t sj) {
-    kt_begin(sj);
+    kt_begin(sj, KID_SORT_REG);
     k_sort_groups_reg<1><<<4096, 256, 0, sj>>>(tl, 2, goff, key, tag, otag);
     kt_end(sj, KID_SORT_REG, 0.0);
     tier_slot(2);
@@ -1444,13 +1450,15 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   // kernels return at once when no group is that large
   k_clear_if_tier<<<1024, 256, 0, st>>>(tl, NTIER - 1, bnd, m);
   (void)hipMemsetAsync(heapq_n, 0, 4, st);
-  kt_begin(st);
+  kt_begin(st, KID_SORT_GLOBAL);
   k_sort_groups_split<<<2048, 256, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
                                             heapq_n, heapq);
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
+  kt_begin(st, KID_SORT_HEAP);
   k_heap_segments<<<64, 256, 0, st>>>(heapq_n, heapq, key, tag, otag);
-  kt_begin(st);
+  kt_end(st, KID_SORT_HEAP, 0.0);
+  kt_begin(st, KID_SORT_SEGS);
   {
     const size_t slab = (seg_lds_bytes(SPLIT_T, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
     if (wpb == 4) {

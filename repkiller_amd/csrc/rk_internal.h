@@ -59,7 +59,8 @@ enum KernelId : int {
   KID_ASSIGN_GID, KID_GROUP_OFFSETS, KID_BUILD_RECORDS, KID_SORT_SMALL, KID_SORT_REG, KID_SORT_LDS,
   KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
   KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_NW_HIST,
-  KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_NW_XBITS, KID_COUNT
+  KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_NW_XBITS,
+  KID_SORT_HEAP, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 // group-sort tiers (rk_groupsort.hip tier_of): <=16, <=32, <=64, four LDS caps, larger
@@ -80,9 +81,10 @@ struct KernelTimer {
   int only = -1;                // >= 0: time only this kernel's launches (rk_set_profiling)
 };
 extern thread_local KernelTimer *g_ktimer;
-// (a launch site that names its kernel in kt_begin stays timed when the timer
-// is restricted to that kernel; the others record no events then)
-inline void kt_begin(hipStream_t st, int kid = -1) {
+// Every launch site names its kernel in kt_begin and kt_end alike, so a timer
+// restricted to one kernel (rk_set_profiling(ctx, 2 + k)) records both events
+// of that kernel's launches and none of the others'
+inline void kt_begin(hipStream_t st, int kid) {
   KernelTimer *t = g_ktimer;
   if (t && t->n < KernelTimer::MAX && (t->only < 0 || t->only == kid))
     (void)hipEventRecord(t->ev[2 * t->n], st);
@@ -273,10 +275,14 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
                     uint64_t max_y, const uint32_t *xbits, hipStream_t st,
                     bool arrival_ids = false, const uint4 *src0 = nullptr);
 // the whole Y sort once the X axis is resolved: the X-hit bits (by processing
-// index) ride in the records from the first pass; the last writes CSR + states
+// index; with src0, by position in src0) ride in the records from the first
+// pass; the last writes CSR + states.  src0: the sharded driver's received Y
+// records, numbered by arrival in the first pass (yrec and tmp then only take
+// the intermediates)
 void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
                        const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
-                       uint64_t max_y, const uint32_t *xbits, hipStream_t st);
+                       uint64_t max_y, const uint32_t *xbits, hipStream_t st,
+                       const uint4 *src0 = nullptr);
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,
                  const uint32_t *xoff, Csr cx, uint32_t *xpos, uint4 *erec, uint32_t *ctrl,
                  uint32_t W, hipStream_t st, const uint4 *halo = nullptr, uint32_t G = 0);

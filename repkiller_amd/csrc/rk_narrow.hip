@@ -371,6 +371,22 @@ struct SrcYX12 {
   __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
 };
 
+// the same for the sharded driver's received Y records: the entry id becomes
+// the arrival index (SrcIdx12) and the bit comes by arrival index
+struct SrcIdxYX12 {
+  using rec_t = uint3;
+  const uint3 *in;
+  const uint64_t *xbits64;
+  __device__ __forceinline__ uint3 load(uint32_t i) const {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane(i) & ~63u;
+    const uint64_t w = xbits64[i0 >> 6];
+    const uint32_t hit = (uint32_t)(w >> (i - i0)) & 1u;
+    return make_uint3(__builtin_nontemporal_load(p), i, __builtin_nontemporal_load(p + 2) | hit << 31);
+  }
+  __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
+};
+
 // --- group members, last pass: gid order (stable: processing order inside) -
 // members {gid, row, sort key lo, hi} -> group of every slot, sort key, tag =
 // slot, file row
@@ -823,7 +839,7 @@ uint64_t *trace_slot(uint32_t tiles) {
     t.cap = (size_t)8 << 20;  // words
     if (hipMalloc(&t.buf, t.cap * 8) != hipSuccess) return t.buf = nullptr;
   }
-  const size_t need = (size_t)tiles * 6;
+  const size_t need = (size_t)tiles * 8;
   if (t.used + need > t.cap) return nullptr;
   uint64_t *p = t.buf + t.used;
   t.passes.push_back({t.used, tiles});
@@ -1011,7 +1027,7 @@ static void order_hist(const Rows &rows, uint32_t n, double row_bytes, uint64_t 
   if (!n) return;
   OrderHistArgs<Rows> args{rows, n, vsize, max_x, max_y, nby, to_digits(a), to_digits(y), ghist,
                            yhist, ctrl};
-  kt_begin(st);
+  kt_begin(st, KID_NW_HIST);
   k_nw_order_hist<Rows><<<grid_for(n, 256, 2048), 256, 0, st>>>(args);
   kt_end(st, KID_NW_HIST, row_bytes * n);  // the rows read once
 }
@@ -1083,7 +1099,7 @@ void nw_rec_hist(const void *recs, int rec_bytes, uint32_t n, uint32_t sub, cons
                  uint32_t *ghist, hipStream_t st) {
   if (!n) return;
   const uint32_t *w = reinterpret_cast<const uint32_t *>(recs);
-  kt_begin(st);
+  kt_begin(st, KID_NW_HIST);
   if (rec_bytes == 16)
     k_nw_rec_hist<4><<<grid_for(n, 256, 2048), 256, 0, st>>>(w, n, sub, to_digits(d), ghist);
   else if (rec_bytes == 12)
@@ -1146,15 +1162,23 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
 // reads the Y records in processing order together with their X-hit bits
 // (sequential bitmask words) and carries the bit in the records, so the last
 // pass writes the Y states from it instead of looking it up per record
+template <class Src0>
+static void y_after_x_first(const Src0 &s0, const DstCsr &dc, uint3 *out, bool last, uint32_t m,
+                            const Digits &D, const uint32_t *gh, uint32_t *stp, uint32_t *ctr,
+                            hipStream_t st, double bytes, uint32_t *nxt) {
+  if (last) launch_pass(s0, dc, m, D.shift[0], D.db[0], gh, stp, ctr, st, bytes, nxt);
+  else launch_pass(s0, DstRec12{out}, m, D.shift[0], D.db[0], gh, stp, ctr, st, bytes, nxt);
+}
 void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
                        const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
-                       uint64_t max_y, const uint32_t *xbits, hipStream_t st) {
+                       uint64_t max_y, const uint32_t *xbits, hipStream_t st, const uint4 *src0) {
   const Digits D = to_digits(y);
   const size_t sw = nw_status_words(m);
   (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
   const PassStatus ps = pass_status(status, m, D, 12);
   const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, nullptr, cy.state, true};
-  const uint3 *src = reinterpret_cast<const uint3 *>(yrec);
+  const uint3 *src = reinterpret_cast<const uint3 *>(src0 ? src0 : yrec);
+  const uint64_t *bits64 = reinterpret_cast<const uint64_t *>(xbits);
   for (int p = 0; p < D.passes; ++p) {
     ps.prepare(p, m, D, st);
     const bool last = p == D.passes - 1;
@@ -1162,11 +1186,10 @@ void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits
     uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes), *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist_of(yhist, p);
     const double bytes = (p == 0 ? 12.0 + 0.125 : 12.0) * m + (last ? 18.0 : 12.0) * m;
-    if (p == 0 && last)
-      launch_pass(SrcYX12{src, reinterpret_cast<const uint64_t *>(xbits)}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    if (p == 0 && src0)
+      y_after_x_first(SrcIdxYX12{src, bits64}, dc, out, last, m, D, gh, stp, ctr, st, bytes, nxt);
     else if (p == 0)
-      launch_pass(SrcYX12{src, reinterpret_cast<const uint64_t *>(xbits)}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st,
-                  bytes, nxt);
+      y_after_x_first(SrcYX12{src, bits64}, dc, out, last, m, D, gh, stp, ctr, st, bytes, nxt);
     else if (last)
       launch_pass(SrcRec12{src}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
     else
@@ -1254,7 +1277,7 @@ void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t
                 const uint4 *halo, uint32_t G) {
   (void)hipMemsetAsync(cc.cnts, 0, ((size_t)3 * cc.nch + 1) * 4, st);
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_NW_XCOUNT);
   k_nw_xcount<<<(m + XN_T * XN_ITEMS - 1) / (XN_T * XN_ITEMS), XN_T, 0, st>>>(
       RecView{halo, G, R}, m, cc.lgW, cc.nch, 10 * cc.W, cc.cnts);
   kt_end(st, KID_NW_XCOUNT, 16.0 * m);
@@ -1271,7 +1294,7 @@ void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint3
   uint2 *erk = reinterpret_cast<uint2 *>(erec);
   XChunkArgs a{RecView{halo, G, R}, m, W, lgW, nch, (maxlen / 2 + 9) / 10, max_x, nbx, xoff, cx,
                xpos, erk, reinterpret_cast<uint32_t *>(erk + m), ctrl};
-  kt_begin(st);
+  kt_begin(st, KID_NW_XCHUNK);
   k_nw_xchunk<<<(nch + XC_WAVES - 1) / XC_WAVES, 64 * XC_WAVES,
                 XC_WAVES * 2 * W * sizeof(uint32_t), st>>>(a);
   // records in (+ halo), X entries (key, id, packed record, code, state), their
@@ -1282,7 +1305,7 @@ void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint3
 void nw_x_bits(const uint32_t *xpos, const uint8_t *xstate, uint32_t m, uint32_t *bits,
                hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_NW_XBITS);
   k_nw_x_bits<<<grid_for(m, 256), 256, 0, st>>>(xpos, xstate, m, bits);
   kt_end(st, KID_NW_XBITS, 5.0 * m);
 }
@@ -1290,7 +1313,7 @@ void nw_x_bits(const uint32_t *xpos, const uint8_t *xstate, uint32_t m, uint32_t
 void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32_t m,
                hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_NW_FILLY);
   k_nw_fill_y<<<grid_for(m, 256), 256, 0, st>>>(ent, bits, state, m);
   kt_end(st, KID_NW_FILLY, 5.0 * m);
 }
@@ -1298,7 +1321,7 @@ void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32
 void nw_assign(const uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uint32_t m,
                const NwDigits &e, uint32_t *ehist, hipStream_t st) {
   if (!m) return;
-  kt_begin(st);
+  kt_begin(st, KID_NW_ASSIGN);
   k_nw_assign<<<grid_for(m, 256, 2048), 256, 0, st>>>(par, newrank, gidp, m, to_digits(e),
                                                       ehist);
   kt_end(st, KID_NW_ASSIGN, 12.0 * m);

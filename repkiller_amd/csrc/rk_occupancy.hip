@@ -1524,7 +1524,7 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
   if (rl.fast32) return;  // the first sweep flags the long runs and the windows itself
   (void)hipMemsetAsync(rl.wpend, 1, rl.nwin, st);
   (void)hipMemsetAsync(dev_count, 0, 4, st);
-  kt_begin(st);
+  kt_begin(st, KID_RUN_BOUNDS);
   k_run_bounds<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.nwin, rl.big, dev_count);
   kt_end(st, KID_RUN_BOUNDS, 4.0 * ax.m);  // keys read once (boundary writes not counted)
   (void)hipMemcpyAsync(host_words, dev_count, 4, hipMemcpyDeviceToHost, st);
@@ -1540,7 +1540,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
   // record and neighbour code of the 32-bit kernel); later sweeps only need
   // the window flags (their real work is what the first one left open)
   if (rl.nwin) {
-    kt_begin(st);
+    const int kid = rl.fast32 ? (first ? KID_SWEEP_FAST : KID_SWEEP_MORE) : KID_SWEEP_TILE;
+    kt_begin(st, kid);
     if (rl.fast32 && first) {
       if (ax.par_dev)
         k_sweep_fast<true><<<(rl.nwin + 3) / 4, 256, 0, st>>>(
@@ -1558,8 +1559,7 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     }
     else
       k_sweep_tile<<<(rl.nwin + 3) / 4, 256, 0, st>>>(ax, rl.wpend, rl.nwin, counters);
-    kt_end(st, rl.fast32 ? (first ? KID_SWEEP_FAST : KID_SWEEP_MORE) : KID_SWEEP_TILE,
-           first ? (rl.fast32 ? 26.0 : 30.0) * ax.m : (double)rl.nwin);
+    kt_end(st, kid, first ? (rl.fast32 ? 26.0 : 30.0) * ax.m : (double)rl.nwin);
 #ifdef RK_SWEEP_PROF
     if (rl.fast32 && first) {
       unsigned long long h[16];
@@ -1573,12 +1573,12 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
 #endif
   }
   if (rl.fast32) {  // the long-run count lives on the device: a fixed grid reads it
-    kt_begin(st);
+    kt_begin(st, KID_SWEEP_LONG);
     k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<const uint8_t *>(rl.big), rl.nwin,
                                          rpend, counters);
     kt_end(st, KID_SWEEP_LONG, 0.0);
   } else if (rl.nbig) {
-    kt_begin(st);
+    kt_begin(st, KID_SWEEP_WAVE);
     k_sweep_wave<<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,
                                                              counters);
     kt_end(st, KID_SWEEP_WAVE, 0.0);

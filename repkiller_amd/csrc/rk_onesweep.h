@@ -118,31 +118,19 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
   __shared__ R srec[LSLOTS];
   __shared__ uint32_t wcnt[NW][RADIX];  // per-wave digit counters, then per-wave starts
   __shared__ uint32_t lbase[RADIX];     // tile-local start of digit d
-  __shared__ uint32_t gbase[RADIX];     // global start of digit d (all tiles)
   __shared__ uint32_t gpos[RADIX];      // global position of the tile's first digit-d record
-  __shared__ uint32_t wsum[NW];
+  __shared__ uint32_t wsum[NW], gsum[NW];
   __shared__ uint32_t s_tile[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
+  const uint64_t tr_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
   if (threadIdx.x == 0) s_tile[0] = atomicAdd(tile_ctr, 1u);
-  // the digits' global starts: exclusive scan of the pass histogram
-  {
-    uint32_t g[DPT], gs = 0;
+  // this owner's digits' counts over the whole pass: their exclusive scan (the
+  // digits' global starts) rides on the tile-local scan of step 2, so the
+  // block's start waits only for its ticket
+  uint32_t gh[DPT];
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) g[j] = owner ? ghist[threadIdx.x * DPT + j] : 0u, gs += g[j];
-    uint32_t inc = gs;
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t o = __shfl_up(inc, off);
-      if (lane >= off) inc += o;
-    }
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    uint32_t at = inc - gs;
-    for (int k2 = 0; k2 < w; ++k2) at += wsum[k2];
-    if (owner)
-#pragma unroll
-      for (int j = 0; j < DPT; ++j) gbase[threadIdx.x * DPT + j] = at, at += g[j];
-  }
+  for (int j = 0; j < DPT; ++j) gh[j] = owner ? ghist[threadIdx.x * DPT + j] : 0u;
   __syncthreads();
   uint32_t tile = s_tile[0];
   if (tile >= tiles) return;
@@ -195,10 +183,11 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     const uint64_t tr1 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     // 2: thread t owns digits [t*DPT, (t+1)*DPT): tile totals (published at
     // once: later tiles may be waiting for them), wave starts, tile-local starts
-    uint32_t run[DPT], tsum = 0;
+    uint32_t run[DPT], tsum = 0, gs = 0;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       run[j] = 0;
+      gs += gh[j];
       if (!owner) continue;
       const uint32_t d = threadIdx.x * DPT + j;
       uint32_t r0 = 0;
@@ -212,19 +201,22 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
       tsum += r0;
       sw_store(&status[(size_t)tile * RADIX + d], (tile ? SW_AGG : SW_INC) | r0);
     }
-    uint32_t inc = tsum;
+    uint32_t inc = tsum, ginc = gs;
     for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t o = __shfl_up(inc, off);
-      if (lane >= off) inc += o;
+      const uint32_t o = __shfl_up(inc, off), go = __shfl_up(ginc, off);
+      if (lane >= off) inc += o, ginc += go;
     }
-    if (lane == 63) wsum[w] = inc;
+    if (lane == 63) wsum[w] = inc, gsum[w] = ginc;
     __syncthreads();
+    uint32_t gb[DPT];  // the global start of each owned digit
     {
-      uint32_t at = inc - tsum;
-      for (int k2 = 0; k2 < w; ++k2) at += wsum[k2];
-      if (owner)
+      uint32_t at = inc - tsum, gat = ginc - gs;
+      for (int k2 = 0; k2 < w; ++k2) at += wsum[k2], gat += gsum[k2];
 #pragma unroll
-        for (int j = 0; j < DPT; ++j) lbase[threadIdx.x * DPT + j] = at, at += run[j];
+      for (int j = 0; j < DPT; ++j) {
+        gb[j] = gat, gat += gh[j];
+        if (owner) lbase[threadIdx.x * DPT + j] = at, at += run[j];
+      }
     }
     __syncthreads();
     // sorted slot of every record (round 0's placed at once)
@@ -250,7 +242,7 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
 #pragma unroll
       for (int j = 0; j < DPT; ++j) {
         const uint32_t d = threadIdx.x * DPT + j;
-        gpos[d] = gbase[d] + (tile ? look_back(status, tile, RADIX, d, run[j]) : 0u);
+        gpos[d] = gb[j] + (tile ? look_back(status, tile, RADIX, d, run[j]) : 0u);
       }
     }
     __syncthreads();
@@ -298,13 +290,15 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     if (trace && threadIdx.x == 0) {  // RK_NW_TRACE: phase timestamps of this tile
       uint32_t xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      uint64_t *o = trace + (size_t)tile * 6;
+      uint64_t *o = trace + (size_t)tile * 8;
       o[0] = tr0;
       o[1] = tr1;
       o[2] = tr2;
       o[3] = __builtin_amdgcn_s_memrealtime();
       o[4] = xcc & 15u;
       o[5] = blockIdx.x;
+      o[6] = tr_entry;  // block start (the ticket, the digit starts, the loads' issue)
+      o[7] = 0;
     }
     tile = next;
     if (tile >= tiles) break;

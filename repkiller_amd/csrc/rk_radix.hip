@@ -259,7 +259,7 @@ template <int T, int I, int DB>
 void launch_pass(const uint32_t *ki, const uint32_t *vi, uint32_t n, int shift, uint32_t tiles,
                  uint32_t *counts, ScanScratch ss, uint32_t *ko, uint32_t *vo, hipStream_t st) {
   constexpr int RADIX = 1 << DB;
-  kt_begin(st);
+  kt_begin(st, KID_HIST);
   k_digit_hist<T, I, DB><<<tiles, T, 0, st>>>(ki, n, shift, tiles, counts);
   kt_end(st, KID_HIST, 4.0 * n);  // keys read once
   const uint32_t nb = (tiles + ROWS - 1) / ROWS;
@@ -268,7 +268,7 @@ void launch_pass(const uint32_t *ki, const uint32_t *vi, uint32_t n, int shift, 
   k_col_partial<DB><<<nb, RADIX, 0, st>>>(counts, tiles, part);
   k_col_digit<DB><<<RADIX, 256, 0, st>>>(part, nb, dtot);
   k_col_final<DB><<<nb, RADIX, 0, st>>>(counts, tiles, part, dtot);
-  kt_begin(st);
+  kt_begin(st, KID_SCATTER);
   k_digit_scatter<T, I, DB><<<tiles, T, 0, st>>>(ki, vi, n, shift, tiles, counts, ko, vo);
   kt_end(st, KID_SCATTER, (vi ? 16.0 : 12.0) * n);  // key (+value) read, key+value written
 }

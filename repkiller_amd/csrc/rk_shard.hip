@@ -802,7 +802,7 @@ struct Shard {
     uint32_t *cnt = take<uint32_t>(SL_PCNT, len);
     pp.off = take<uint32_t>(SL_POFF, len);
     zero(cnt + len - 1, 4);
-    kt_begin(st);
+    kt_begin(st, KID_PART);
     k_part_count<<<pp.nblk, 256, 0, st>>>(op, n, P, pp.nblk, cnt, pp.mcache, pp.mread);
     kt_end(st, KID_PART, 0.0);
     launched("k_part_count");
@@ -835,7 +835,7 @@ struct Shard {
     uint32_t *cnt = take<uint32_t>(SL_PCNT, len);
     pp.off = take<uint32_t>(SL_POFF, len);
     zero(cnt + len - 1, 4);
-    kt_begin(st);
+    kt_begin(st, KID_PART);
     k_part_count<<<pp.nblk, 256, 0, st>>>(op, n, P, pp.nblk, cnt, pp.mcache, pp.mread);
     kt_end(st, KID_PART, 0.0);
     launched("k_part_count");
@@ -868,7 +868,7 @@ struct Shard {
   }
   template <class Op>
   void emit(const Op &op, const PartPlan &pp) {
-    kt_begin(st);
+    kt_begin(st, KID_PART);
     k_part_scatter<<<pp.nblk, 256, 0, st>>>(op, pp.n, P, pp.nblk, pp.off, pp.mcache);
     kt_end(st, KID_PART, 0.0);
     launched("k_part_scatter");
@@ -911,7 +911,7 @@ struct Shard {
       if (q != me) bytes_sent += sb[q];
     double moved = 0;
     for (uint32_t q = 0; q < P; ++q) moved += (double)sb[q] + (double)rb[q];
-    kt_begin(st);
+    kt_begin(st, KID_EXCHANGE);
     const int rc = comm->alltoallv(send, sb, recv, rb, st);
     kt_end(st, KID_EXCHANGE, moved);  // bytes read + written (device time of the a2a)
     if (rc) {
@@ -1153,11 +1153,11 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
   uint32_t *cur = S.take<uint32_t>(SL_CUR, m + 1);
   if (m) {
     if (npar) {
-      kt_begin(S.st);
+      kt_begin(S.st, KID_SHARD_AUX);
       k_par_scatter<<<grid_for(npar, 256), 256, 0, S.st>>>(prr, npar, poff, m, parg, S.ctrl);
       kt_end(S.st, KID_SHARD_AUX, 0.0);
     }
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SHARD_AUX);
     k_local_par<<<grid_for(m, 256), 256, 0, S.st>>>(parg, m, poff, lpar, ext, isroot, S.ctrl);
     kt_end(S.st, KID_SHARD_AUX, 0.0);
     S.launched("parents");
@@ -1196,7 +1196,7 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
   }
   if (!links) {  // every chain ends in its own slice: no label rounds
     if (m) {
-      kt_begin(S.st);
+      kt_begin(S.st, KID_SHARD_AUX);
       k_final_gid_local<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, lrank, (uint32_t)goff, m, junk);
       kt_end(S.st, KID_SHARD_AUX, 12.0 * m);
       S.launched("k_final_gid_local");
@@ -1207,7 +1207,7 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
     return junk;
   }
   if (m) {
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SHARD_AUX);
     k_init_labels<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, ext, lrank, (uint32_t)goff, m, lab,
                                                         cur);
     kt_end(S.st, KID_SHARD_AUX, 0.0);
@@ -1254,7 +1254,7 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
   }
   uint32_t *gid_own = junk;  // the jump's scratch is free again
   if (m) {
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SHARD_AUX);
     k_final_gid<<<grid_for(m, 256), 256, 0, S.st>>>(lpar, lab, m, gid_own, S.ctrl);
     kt_end(S.st, KID_SHARD_AUX, 0.0);
     S.launched("k_final_gid");
@@ -1345,6 +1345,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
     }
     S.zero(S.ctrl, 256 * 4);
   }
+  ss.generic_driver = 1;
 
   // ---- 1: processing keys, slice bounds from the global xStart/10 histogram
   Frags f{in->x_start, in->y_start, in->length, in->strand, nl};
@@ -1372,7 +1373,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   pr.pkey = S.take<uint32_t>(SL_PKEY, m + 1);
   pr.row = S.take<uint32_t>(SL_ROW, m + 1);
   if (m) {
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SH_ROWKEYS);
     k_row_keys<<<grid_for(m, 256, 1024), 256, 0, S.st>>>(
         rec, m, pkey2, reinterpret_cast<unsigned long long *>(S.ctrl + 10));
     kt_end(S.st, KID_SH_ROWKEYS, 0.0);
@@ -1466,7 +1467,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   S.hip(hipEventRecord(ctx->fork, S.st), "fork");
   S.hip(hipStreamWaitEvent(S.st2, ctx->fork, 0), "fork wait");
   if (G) {
-    kt_begin(S.st2);
+    kt_begin(S.st2, KID_SHARD_AUX);
     k_fill_ghost_x<<<grid_for(G, 256), 256, 0, S.st2>>>(gh, G, xrec_f, keyx_f, nbx);
     kt_end(S.st2, KID_SHARD_AUX, 0.0);
     S.launched("k_fill_ghost_x");
@@ -1517,7 +1518,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   S.hip(hipEventRecord(ctx->fork, S.st), "fork");
   S.hip(hipStreamWaitEvent(S.st2, ctx->fork, 0), "fork wait");
   if (ny) {
-    kt_begin(S.st2);
+    kt_begin(S.st2, KID_SH_FILLY);
     k_fill_y<<<grid_for(ny, 256), 256, 0, S.st2>>>(yr, nullptr, ny, yrec_l, ylh_l, keyy_l, nby,
                                                    ycode, yb.b[me], yb.b[me + 1]);
     kt_end(S.st2, KID_SH_FILLY, 0.0);
@@ -1539,7 +1540,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   auto solve_x = [&](const GhostX *halo, uint32_t Gc) {
     const uint32_t base = G - Gc, n = Gc + m;
     if (Gc) {
-      kt_begin(S.st);
+      kt_begin(S.st, KID_SHARD_AUX);
       k_fill_ghost_x<<<grid_for(Gc, 256), 256, 0, S.st>>>(halo, Gc, xrec_f + base,
                                                          keyx_f + base, nbx);
       kt_end(S.st, KID_SHARD_AUX, 0.0);
@@ -1550,7 +1551,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
              (uint32_t)bit_length(2ull * nbx - 1), max_x, true, fast32};
     resolve(S, a, kXSlots, p);
     if (m) {
-      kt_begin(S.st);
+      kt_begin(S.st, KID_SH_XOWN);
       k_x_own<<<grid_for(m, 256), 256, 0, S.st>>>(yrec_f + G, halo, Gc, poff, m, xg);
       kt_end(S.st, KID_SH_XOWN, 0.0);
       S.launched("k_x_own");
@@ -1559,7 +1560,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   S.hip(hipStreamWaitEvent(S.st, ctx->aux, 0), "x sorted wait");
   sweep_axis(S, xa, xcsr, p);
   if (m) {
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SH_XOWN);
     k_x_own<<<grid_for(m, 256), 256, 0, S.st>>>(yrec_f + G, gh, G, poff, m, xg);
     kt_end(S.st, KID_SH_XOWN, 0.0);
     S.launched("k_x_own");
@@ -1630,7 +1631,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
     }
     S.hip(hipStreamWaitEvent(S.st, ctx->join, 0), "join wait");
     if (ny) {
-      kt_begin(S.st);
+      kt_begin(S.st, KID_SH_MERGE);
       k_merge_yx<<<grid_for(ny, 256), 256, 0, S.st>>>(ycode, xh, ny, yrec_l);
       kt_end(S.st, KID_SH_MERGE, 0.0);
       S.launched("k_merge_yx");
@@ -1638,7 +1639,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   }
   auto y_results = [&](const uint32_t *ymap, uint32_t c, const uint32_t *par) {
     if (!c) return;
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SH_YRES);
     k_y_results<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ycode, ymap, c, par, ystate, ywin);
     kt_end(S.st, KID_SH_YRES, 0.0);
     S.launched("k_y_results");
@@ -1648,7 +1649,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
   // a fixed-halo re-resolution: the selected records, sorted again on stream 1
   auto solve_y = [&](const uint32_t *ymap, uint32_t c) {
     if (!c) return;
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SH_FILLY);
     k_fill_y<<<grid_for(c, 256), 256, 0, S.st>>>(yr, ymap, c, yrec_l, ylh_l, keyy_l, nby,
                                                   ycode, 0, 0);
     kt_end(S.st, KID_SH_FILLY, 0.0);
@@ -1702,7 +1703,7 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
     uint32_t *tag = S.take<uint32_t>(SL_TAG, mr + 1);
     uint32_t *otag = S.take<uint32_t>(SL_OTAG, mr + 1);
     void *gsort = S.take<uint8_t>(SL_GSORT, groupsort_scratch_bytes(mr));
-    kt_begin(S.st);
+    kt_begin(S.st, KID_SHARD_AUX);
     k_mem_keys<<<grid_for(mr, 256), 256, 0, S.st>>>(mem, mr, g0, lg);
     kt_end(S.st, KID_SHARD_AUX, 0.0);
     S.launched("k_mem_keys");

@@ -358,6 +358,22 @@ T *exchange_nw(Shard &S, const T *send, const PartPlan &pp, int recv_slot, uint3
   return S.exchange<T>(send, pp, recv_slot, nrecv, from);
 }
 
+// the largest slice's row count: at one rank the kept rows, else the global
+// histogram's bins between each pair of slice bounds (the bounds lie on bins)
+static uint64_t slice_max_rows(const std::vector<uint64_t> &gh, const Bounds &sk, uint32_t shift,
+                               uint32_t P, uint64_t kept) {
+  if (P == 1) return kept;
+  const uint64_t unit = 1ull << shift;
+  uint64_t most = 0;
+  for (uint32_t q = 0; q < P; ++q) {
+    const uint64_t b0 = (sk.b[q] + unit - 1) >> shift, b1 = (sk.b[q + 1] + unit - 1) >> shift;
+    uint64_t c = 0;
+    for (uint64_t b = b0; b < b1 && b < gh.size(); ++b) c += gh[b];
+    most = c > most ? c : most;
+  }
+  return most;
+}
+
 int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, uint32_t P,
                         uint32_t me, uint64_t N, uint64_t row_base, int32_t lead_in,
                         rk_shard_result *out, std::chrono::steady_clock::time_point t0) {
@@ -381,7 +397,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   S.zero(S.ctrl + 25, 4);
   if (nl) {
     // more blocks when there is no slice histogram to flush (one rank)
-    kt_begin(st);
+    kt_begin(st, KID_SH_ROWKEYS);
     k_sh_rows<<<grid_for(nl, 256, P > 1 ? 1024 : 4096), 256, 0, st>>>(
         ShRowsArgs{f, vsize, max_x, max_y, shift, P > 1 ? hist : nullptr, S.ctrl});
     kt_end(st, KID_SH_ROWKEYS, 25.0 * nl);
@@ -405,6 +421,12 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
       for (uint32_t b = 0; b < NBINS; ++b) gh[b] += all[(size_t)q * NBINS + b];
   }
   const Bounds slice_keys = split_bounds(gh, shift, drop, P);
+  // the one-sweep passes' status words carry a 30-bit count (SW_VAL,
+  // rk_onesweep.h), as the single-device record pipeline's bound n < 2^30
+  // (record_eligible): a slice of 2^30 or more rows takes the generic driver.
+  // Every rank sees the same global histogram (the kept count at one rank), so
+  // the decision is agreed
+  if (slice_max_rows(gh, slice_keys, shift, P, flags[25]) >= (1ull << 30)) return RK_SHARD_FALLBACK;
 
   // ---- 2: rows -> slice owners as 16-B records (arrival order = file order);
   // the bounds lie on histogram bins (or at the end), so this rank's count per
@@ -488,6 +510,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   uint32_t ny = 0;
   const uint3 *yr = exchange_nw<uint3>(S, y_self ? yop.yrec : yop.out, ypp, SN_YR, &ny);
   ss.y_entries = ny;
+  // the Y ranges (+ halos) received: the same 30-bit bound on every rank's sort
+  S.agree(ny >= (1u << 30) ? (int)RK_E_TOO_MANY : (int)RK_OK);
   const uint64_t ylo = yb.b[me], yhi = yb.b[me + 1];
   uint8_t *ycode = S.take<uint8_t>(SL_YCODE, ny + 1);
   uint8_t *ystate = S.take<uint8_t>(SL_YSTATE, ny + 1);
@@ -518,20 +542,28 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
       nw_y_sort_tail(yB, yA, n, yd, yhist, ystat, cy, nby, max_y, bits, s, true,
                      reinterpret_cast<const uint4 *>(src));
   };
-  // RK_SH_YSERIAL=1: the Y head on the main stream, ahead of X (A/B)
-  static const bool y_serial = [] {
-    const char *e = getenv("RK_SH_YSERIAL");
+  // The Y sort runs after X, as on one device (nw_y_sort_after_x): its first
+  // pass carries the X-hit bit in the records, so no pass shares the device
+  // with the X axis and the last one needs no lookup.  Beside X on the second
+  // stream: the Y codes and the Y key histogram.  RK_SH_YEARLY=1: the round-3
+  // schedule (the head passes beside X, the tail looking the bits up)
+  static const bool y_early = [] {
+    const char *e = getenv("RK_SH_YEARLY");
     return e && e[0] == '1';
   }();
-  hipStream_t sy = y_serial ? st : st2;
+  hipStream_t sy = st2;
   S.hip(hipEventRecord(ctx->fork, st), "fork");
   S.hip(hipStreamWaitEvent(st2, ctx->fork, 0), "fork wait");
   if (ny) {
     k_sh_ycode<<<grid_for(ny, 256), 256, 0, sy>>>(yr, ny, nby, ylo, yhi, ycode);
     S.launched("k_sh_ycode");
   }
-  y_sort(yr, ny, nullptr, sy, true, false);
-  S.launched("Y sort head");
+  if (y_early) {
+    y_sort(yr, ny, nullptr, sy, true, false);
+    S.launched("Y sort head");
+  } else if (ny) {
+    nw_rec_hist(yr, 12, ny, 0, yd, yhist, sy);
+  }
   S.hip(hipEventRecord(ctx->join, st2), "join");
   ss.ms_y = ms_since(ty);
 
@@ -613,7 +645,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
                     S.ctrl + 64, S.ctrl + 4};
     uint32_t sweeps = 0;
     S.check(resolve_axis(ctx, ax, sc, true, &sweeps));
-    kt_begin(st);
+    kt_begin(st, KID_SH_XOWN);
     k_sh_x_own<<<grid_for(mx, 256), 256, 0, st>>>(xpos, cx.state, par, halo, Gc, m, poff, xg,
                                                   xused);
     kt_end(st, KID_SH_XOWN, 0.0);
@@ -684,7 +716,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     }
     S.hip(hipStreamWaitEvent(st, ctx->join, 0), "join wait");
     if (ny) {
-      kt_begin(st);
+      kt_begin(st, KID_SH_MERGE);
       k_sh_xhit_bits<<<grid_for(ny, 256), 256, 0, st>>>(xh, ny, ycode, ybits);
       kt_end(st, KID_SH_MERGE, 0.0);
       S.launched("k_sh_xhit_bits");
@@ -704,14 +736,19 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   };
   auto y_results = [&](const uint32_t *ymap, uint32_t c) {
     if (!c) return;
-    kt_begin(st);
+    kt_begin(st, KID_SH_YRES);
     k_sh_y_results<<<grid_for(c, 256), 256, 0, st>>>(yr, ycode, ymap, c, par_l, ystate, ywin,
                                                       poff, m, xg);
     kt_end(st, KID_SH_YRES, 0.0);
     S.launched("k_sh_y_results");
   };
-  y_sort(yr, ny, ybits, st, false, true);
-  S.launched("Y sort tail");
+  if (y_early) {
+    y_sort(yr, ny, ybits, st, false, true);
+  } else if (ny) {
+    nw_y_sort_after_x(yB, yA, ny, yd, yhist, ystat, cy, nby, max_y, ybits, st,
+                      reinterpret_cast<const uint4 *>(yr));
+  }
+  S.launched("Y sort");
   sweep_y(ny);
   y_results(nullptr, ny);
   // a fixed-halo re-resolution: the selected records sorted again on stream 1
@@ -774,6 +811,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     mem = narrow ? (const void *)exchange_nw<uint3>(S, (const uint3 *)mop.out, pp, SL_MEM, &mr)
                  : (const void *)exchange_nw<uint4>(S, (const uint4 *)mop.out, pp, SL_MEM, &mr);
   }
+  // the gid range's members: the same 30-bit bound on the member sort
+  S.agree(mr >= (1u << 30) ? (int)RK_E_TOO_MANY : (int)RK_OK);
   const uint32_t g0 = (uint32_t)gb.b[me], Gl = (uint32_t)(gb.b[me + 1] - gb.b[me]);
   uint32_t *ogid = S.take<uint32_t>(SL_OGID, mr + 1);
   uint8_t *orep = S.take<uint8_t>(SL_OREP, mr + 1);

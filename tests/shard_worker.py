@@ -26,13 +26,17 @@ def load_case(case):
     if case["kind"] == "synth":
         f = rk.synth(case["n"], case["L"], seed=case["seed"], family_frac=case.get("ff", 0.8),
                      copies=tuple(case.get("copies", (2, 30))))
+        if "long_row" in case:  # one row outside the 16-B record (length >= 2^24)
+            k = case["long_row"]
+            f.x_start[k], f.y_start[k], f.length[k] = 1000, 1000, (1 << 24) + 5
         return f, case["L"], case["L"]
     db = rk.FragmentsDatabase(case["path"])
     return db.frags, db.len_x_hdr, db.len_y_hdr
 
 
-def worker(rank, world, port, cases, q, comm_kind="host"):
+def worker(rank, world, port, cases, q, comm_kind="host", env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(env or {})  # read once by the library (e.g. RK_SHARD_GENERIC)
     import torch
     import torch.distributed as dist
     import repkiller_amd as rk

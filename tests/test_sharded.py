@@ -35,11 +35,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def run_ranks(world, cases, comm_kind="host", timeout=100):
+def run_ranks(world, cases, comm_kind="host", timeout=100, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=shard_worker.worker, args=(r, world, port, cases, q, comm_kind))
+    procs = [ctx.Process(target=shard_worker.worker,
+                         args=(r, world, port, cases, q, comm_kind, env))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -120,6 +121,48 @@ def test_sharded_matches_single_device(gpu_ctx, world):
             reruns += sum(s["x_reruns"] + s["y_reruns"] for s in stats)
     # the dense no-lead-in sets must have exercised the fixed-halo path
     assert reruns > 0
+
+
+def _check_vs_single_device(gpu_ctx, got, cases, world, generic):
+    for ci, case in enumerate(cases):
+        order, gid, rep, ng, stats = assemble(got, ci, world)
+        assert all(st["generic_driver"] == int(generic) for st in stats), (case, stats)
+        want, _, _, _ = reference(gpu_ctx, case)
+        assert ng == want.n_groups, case
+        assert np.array_equal(order, want.out_order), case
+        assert np.array_equal(gid, want.gid), case
+        assert np.array_equal(rep, want.repval), case
+
+
+# one row of ONE rank does not pack into the 16-B record (length >= 2^24): the
+# agreed flag of the record driver's first stage sends every rank to the
+# generic driver together (the hand-off: control words reset, then the generic
+# driver's own collectives after the record driver's first gathers)
+FALLBACK = [
+    dict(kind="synth", n=200_000, L=20_000_000, seed=31, long_row=199_990),  # last rank's rows
+    dict(kind="synth", n=200_000, L=20_000_000, seed=32, long_row=10),       # rank 0's rows
+    dict(kind="synth", n=100_000, L=10_000_000, seed=33, ff=0.95, copies=(100, 600),
+         long_row=50_000),
+]
+
+
+def test_sharded_fallback_to_generic(gpu_ctx):
+    got = run_ranks(2, FALLBACK)
+    _check_vs_single_device(gpu_ctx, got, FALLBACK, 2, generic=True)
+
+
+def test_sharded_generic_forced(gpu_ctx):
+    """RK_SHARD_GENERIC=1: the generic driver on the SYNTH sets (every row packs)."""
+    cases = [c for c in SYNTH if c.get("n", 1) <= 200_000 and c["kind"] == "synth"]
+    got = run_ranks(3, cases, env={"RK_SHARD_GENERIC": "1"})
+    _check_vs_single_device(gpu_ctx, got, cases, 3, generic=True)
+
+
+def test_sharded_record_driver_used(gpu_ctx):
+    """Every SYNTH set packs: the record driver classified them (not the fallback)."""
+    cases = SYNTH[:2]
+    got = run_ranks(2, cases)
+    _check_vs_single_device(gpu_ctx, got, cases, 2, generic=False)
 
 
 def _edge_cases():
