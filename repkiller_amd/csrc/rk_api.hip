@@ -39,7 +39,7 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
     "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32", "k_nw_order_hist",
     "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign", "k_nw_xcount", "k_nw_x_bits",
-    "k_heap_segments",
+    "k_heap_segments", "k_seg_fine (order)", "k_seg_fine (members)",
 };
 }  // namespace rk
 
@@ -63,6 +63,15 @@ void collect_kernel_timing(rk_ctx *ctx) {
       }
     }
     ctx->kt.tier_counts = nullptr;
+  }
+  bool any_units = false;
+  for (int i = 0; i < ctx->kt.n; ++i) any_units |= ctx->kt.unit_bytes[i] > 0.0;
+  if (any_units) {  // launches that counted their work on the device
+    std::vector<uint32_t> u(ctx->kt.n);
+    if (hipMemcpy(u.data(), ctx->kt.units, (size_t)ctx->kt.n * 4, hipMemcpyDeviceToHost) ==
+        hipSuccess)
+      for (int i = 0; i < ctx->kt.n; ++i)
+        if (ctx->kt.unit_bytes[i] > 0.0) ctx->kt.bytes[i] = ctx->kt.unit_bytes[i] * u[i];
   }
   for (int i = 0; i < ctx->kt.n; ++i) {
     float ms = 0;
@@ -329,6 +338,7 @@ struct NWork {
   uint8_t *wpend;
   uint32_t *scan;
   size_t scan_cap;
+  uint32_t *chist, *coff;  // the two-stage order sort's segment counts and starts
 };
 
 size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
@@ -370,6 +380,9 @@ size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
   w.rbeg_at = c.take<uint32_t>(n);
   w.scan_cap = rk::scan_blocks(n + 1) + 64;
   w.scan = c.take<uint32_t>(w.scan_cap);
+  // the two-stage order sort's segment counts and starts (<= n / 1536 + 1 each)
+  w.chist = c.take<uint32_t>(n / 1024 + 64);
+  w.coff = c.take<uint32_t>(n / 1024 + 64);
   return c.off;
 }
 
@@ -442,6 +455,10 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   hipStream_t st = ctx->stream, st2 = ctx->stream2;
   ctx->stats.n_in = n;
   const rk::NwDigits ad = rk::nw_plan(rk::bit_length(pl.vsize - 1));
+  // the processing order in two stages (coarse one-sweep passes + the segment
+  // kernel) when the rows are many enough; else LSD passes over every bit
+  const rk::NwOrderPlan op = rk::nw_order_split(n, pl.vsize, rk::bit_length(pl.vsize - 1));
+  const bool split = op.coarse.passes > 0;
   // the widest digit of the 12-B record sorts (Y axis, narrow members): 9
   // bits (7168 records per tile: 14 per digit segment) takes cfg3's 26-bit Y
   // key in 3 passes instead of 4 (RK_NW_YBITS=8 for measurements)
@@ -456,8 +473,8 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));
   HIPCHK(ctx, hipMemsetAsync(w.ahist, 0, 3 * 4096 * sizeof(uint32_t), st));
   mark(ctx, RK_PH_PREP);
-  rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, ad, yd, w.ahist, w.yhist, w.ctrl,
-                    st, wire);
+  rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, split ? op.coarse : ad, yd,
+                    w.ahist, w.yhist, w.ctrl, st, wire);
   HIPCHK(ctx, hipGetLastError());
   if ((rc = readback(ctx, w.ctrl, 9))) return rc;
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
@@ -487,8 +504,14 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   cc.nch = rk::nw_chunks(pl.nbx, cc.W);
   cc.cnts = w.xcnt;
   mark(ctx, RK_PH_ORDER);
-  rk::nw_order_sort(*in, pl.vsize, pl.nby, ad, w.ahist, w.astatus, w.Ra, w.Rb, w.yrec, st, wire);
-  rk::nw_x_count(w.Ra, m, cc, st);
+  if (split) {
+    // (the member records' buffer is free until the X chunk kernel)
+    rk::nw_order_sort_split(*in, m, pl.nby, op, w.ahist, w.astatus, w.Ra, w.Rb, w.yrec, w.erec,
+                            w.chist, w.coff, ss, &cc, pl.vsize, st, wire);
+  } else {
+    rk::nw_order_sort(*in, pl.vsize, pl.nby, ad, w.ahist, w.astatus, w.Ra, w.Rb, w.yrec, st, wire);
+    rk::nw_x_count(w.Ra, m, cc, st);
+  }
   rk::exclusive_scan_u32(w.xcnt, w.xoff, (size_t)3 * cc.nch + 1, ss, st);
   HIPCHK(ctx, hipGetLastError());
   // The Y axis is sorted once X is resolved (default): its first pass reads
@@ -579,15 +602,32 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     // 12-B member records take 9-bit digits too (a 25..27-bit gid in 3
     // passes); 16-B ones keep 8-bit digits
     const rk::NwDigits ed = rk::nw_plan(rk::bit_length(G ? G - 1 : 0), narrow_keys ? bits12 : 8);
+    // 12-B member records: the sort by gid in two stages (coarse passes, then
+    // the segment kernel, which also writes the group starts)
+    // RK_NW_MSPLIT=1 (measurement): the member sort in two stages
+    static const bool msplit_on = [] {
+      const char *e = getenv("RK_NW_MSPLIT");
+      return e && e[0] == '1';
+    }();
+    const rk::NwOrderPlan mp = narrow_keys && msplit_on
+                                   ? rk::nw_order_split(m, G, rk::bit_length(G ? G - 1 : 0))
+                                   : rk::NwOrderPlan{};
+    const bool msplit = mp.coarse.passes > 0;
     HIPCHK(ctx, hipMemsetAsync(w.ehist, 0, 4096 * sizeof(uint32_t), st));
     // gids into isnew's words (dead after the scan)
-    rk::nw_assign(w.par, w.newrank, w.isnew, m, ed, w.ehist, st);
+    rk::nw_assign(w.par, w.newrank, w.isnew, m, msplit ? mp.coarse : ed, w.ehist, st);
 
     // members (stable by gid => processing order), in-group order, flags
     if (prof) mark(ctx, RK_PH_MEMBERS);
-    rk::nw_member_sort(w.erec, w.isnew, w.Ra, w.Rb, m, ed, w.ehist, w.astatus, w.sgid, w.reckey,
-                       w.tag, w.mrow, narrow_keys, st);
-    rk::group_offsets(w.sgid, m, G, w.goff, st);
+    if (msplit) {
+      // (the order records and the Y records are done with)
+      rk::nw_member_sort_split(w.erec, w.isnew, w.Ra, w.Rb, w.yrec, m, G, mp, w.ehist, w.astatus,
+                               w.sgid, w.reckey, w.tag, w.mrow, w.goff, w.chist, w.coff, ss, st);
+    } else {
+      rk::nw_member_sort(w.erec, w.isnew, w.Ra, w.Rb, m, ed, w.ehist, w.astatus, w.sgid,
+                         w.reckey, w.tag, w.mrow, narrow_keys, st);
+      rk::group_offsets(w.sgid, m, G, w.goff, st);
+    }
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
     rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
                           ctx->host + 128, narrow_keys, st, st2, ctx->fork, ctx->join);
@@ -854,6 +894,10 @@ extern "C" int rk_create(rk_ctx **out, int device) {
     rk_destroy(ctx);
     return RK_E_HIP;
   }
+  if (hipMalloc((void **)&ctx->kt.units, rk::KernelTimer::MAX * sizeof(uint32_t)) != hipSuccess) {
+    rk_destroy(ctx);
+    return RK_E_HIP;
+  }
   // timing-only events: no system-scope fence at record (HIP's recommendation
   // for pure timing events; it keeps the instrumentation's own cost low)
   for (auto &e : ctx->kt.ev)
@@ -879,6 +923,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->io) (void)hipFree(ctx->io);
   if (ctx->ws_wide) (void)hipFree(ctx->ws_wide);
+  if (ctx->kt.units) (void)hipFree(ctx->kt.units);
   if (ctx->ws_nw) (void)hipFree(ctx->ws_nw);
   if (ctx->nw_small) (void)hipFree(ctx->nw_small);
   for (void *p : ctx->pool.ptr)
@@ -1062,16 +1107,24 @@ static int classify_wire(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p
   if (rc) return rc;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   const double t2 = rk::wall_ms();
-  std::vector<rk::IoPiece> down;
+  // the flags first; then the output order comes down while other threads
+  // rebuild the gids from the flags
+  std::vector<rk::IoPiece> flags, orders;
   for (uint32_t q = 0; q < npairs; ++q) {
     out[q].n_out = dres[q].n_out;
     out[q].n_groups = dres[q].n_groups;
-    down.push_back({out[q].out_order, dres[q].out_order, dres[q].n_out * 4});
-    down.push_back({out[q].repval, dres[q].repval, dres[q].n_out});
+    flags.push_back({out[q].repval, dres[q].repval, dres[q].n_out});
+    orders.push_back({out[q].out_order, dres[q].out_order, dres[q].n_out * 4});
   }
-  if ((rc = rk::io_d2h(ctx, down))) return rc;
-  for (uint32_t q = 0; q < npairs; ++q)
-    rk::gids_from_flags(ctx, out[q].repval, out[q].n_out, out[q].gid);
+  if ((rc = rk::io_d2h(ctx, flags))) return rc;
+  {
+    rk::GidJob job;
+    for (uint32_t q = 0; q < npairs; ++q)
+      rk::gids_from_flags_async(out[q].repval, out[q].n_out, out[q].gid, 8, job);
+    rc = rk::io_d2h(ctx, orders);
+    job.wait();
+  }
+  if (rc) return rc;
   ctx->stats.h2d_ms = t1 - t0;
   ctx->stats.d2h_ms = rk::wall_ms() - t2;
   ctx->stats.wire = 1;

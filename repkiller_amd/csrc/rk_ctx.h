@@ -6,6 +6,7 @@
 
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/repkiller_amd.h"
@@ -101,8 +102,18 @@ int io_d2h(rk_ctx *ctx, const std::vector<IoPiece> &pieces);
 // (length >= 2^24, yStart >= 2^35 or xStart >= 2^36)
 int io_h2d_rows(rk_ctx *ctx, const rk_frags_soa &in, void *dev);
 // gid[k] = (rows j <= k with flag[j] != 2) - 1: a new group starts at every
-// row whose repeat flag is not 2 (host threads)
-void gids_from_flags(rk_ctx *ctx, const uint8_t *flag, size_t n, uint32_t *gid);
+// row whose repeat flag is not 2; on `threads` threads of its own, started
+// now and joined by job.wait(), so it runs beside a transfer that keeps the
+// host pool busy
+struct GidJob {
+  std::vector<std::thread> th;
+  void wait() {
+    for (auto &t : th) t.join();
+    th.clear();
+  }
+  ~GidJob() { wait(); }
+};
+void gids_from_flags_async(const uint8_t *flag, size_t n, uint32_t *gid, int threads, GidJob &job);
 void io_destroy(rk_ctx *ctx);
 bool host_pinned(const void *p);
 double wall_ms();

@@ -60,7 +60,7 @@ enum KernelId : int {
   KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
   KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_NW_HIST,
   KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_NW_XBITS,
-  KID_SORT_HEAP, KID_COUNT
+  KID_SORT_HEAP, KID_NW_FINE, KID_NW_MFINE, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 // group-sort tiers (rk_groupsort.hip tier_of): <=16, <=32, <=64, four LDS caps, larger
@@ -79,6 +79,12 @@ struct KernelTimer {
   uint32_t tier_nblk;
   int tier_slot[TIERS];         // timer slot of each tier's launch (-1: none)
   int only = -1;                // >= 0: time only this kernel's launches (rk_set_profiling)
+  // launches whose work is known on the device only (k_sweep_long32: the
+  // entries of the long runs it walks): the kernel adds its units into
+  // units[slot], and the slot's algorithmic bytes are unit_bytes[slot] x that
+  // count, read back when the call's timings are collected
+  uint32_t *units = nullptr;    // device, MAX words (rk_create)
+  double unit_bytes[MAX];
 };
 extern thread_local KernelTimer *g_ktimer;
 // Every launch site names its kernel in kt_begin and kt_end alike, so a timer
@@ -95,8 +101,24 @@ inline void kt_end(hipStream_t st, int kid, double bytes) {
     (void)hipEventRecord(t->ev[2 * t->n + 1], st);
     t->kid[t->n] = kid;
     t->bytes[t->n] = bytes;
+    t->unit_bytes[t->n] = 0.0;
     t->n++;
   }
+}
+// the device word a launch adds its work units to (null when this launch is
+// not timed); call before kt_begin (the word is cleared on the stream), then
+// launch and kt_end_units
+inline uint32_t *kt_units(hipStream_t st, int kid) {
+  KernelTimer *t = g_ktimer;
+  if (!t || !t->units || t->n >= KernelTimer::MAX || !(t->only < 0 || t->only == kid)) return nullptr;
+  (void)hipMemsetAsync(t->units + t->n, 0, 4, st);
+  return t->units + t->n;
+}
+inline void kt_end_units(hipStream_t st, int kid, double bytes_per_unit) {
+  KernelTimer *t = g_ktimer;
+  const int slot = t ? t->n : -1;
+  kt_end(st, kid, 0.0);
+  if (t && t->n == slot + 1 && t->units) t->unit_bytes[slot] = bytes_per_unit;
 }
 
 // ----------------------------------------------------------- rk_radix.hip --
@@ -260,6 +282,33 @@ void nw_order_hist(const rk_frags_soa &in, uint64_t vsize, uint64_t max_x, uint6
 void nw_order_sort(const rk_frags_soa &in, uint64_t vsize, uint32_t nby, const NwDigits &a,
                    const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
                    hipStream_t st, const uint3 *wire = nullptr);
+// Sorts in two stages (rk_narrow.hip, k_seg_fine): C coarse bits by
+// one-sweep passes (coarse: their digits, shifted past the F fine bits), then
+// one block per coarse-key segment (nseg = 2^C) sorts its F fine bits in LDS.
+// The processing order's segment kernel writes the final records, the Y
+// records and -- given cc -- the X-chunk counts; the member sort's writes the
+// in-group sort arrays and the group starts.  passes == 0 in `coarse`: not
+// applicable (too few rows, or RK_NW_SPLIT=0).
+struct NwOrderPlan {
+  int C = 0, F = 0;
+  uint32_t nseg = 0;
+  NwDigits coarse{};
+};
+NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int bits);  // nkeys: key values in use
+void nw_order_sort_split(const rk_frags_soa &in, uint32_t m, uint32_t nby, const NwOrderPlan &op,
+                         const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
+                         uint4 *yrec, uint4 *tmp, uint32_t *chist, uint32_t *coff,
+                         ScanScratch ss, const NwChunkCounts *cc, uint64_t vsize, hipStream_t st,
+                         const uint3 *wire = nullptr);
+// the member sort in two stages (12-B member records: every sort key fits 32
+// bits): the in-group sort arrays as nw_member_sort writes them, and goff (G +
+// 1 group starts, group_offsets' job); t0 / t1 / t2: three scratch arrays of
+// m 12-B records
+void nw_member_sort_split(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1,
+                          uint4 *t2, uint32_t m, uint32_t G, const NwOrderPlan &mp,
+                          const uint32_t *ehist, uint32_t *status, uint32_t *sgid, uint64_t *key,
+                          uint32_t *tag, uint32_t *mrow, uint32_t *goff, uint32_t *chist,
+                          uint32_t *coff, ScanScratch ss, hipStream_t st);
 // (halo, G): the sharded driver's G lead-in records ahead of R (R holds m - G)
 void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st,
                 const uint4 *halo = nullptr, uint32_t G = 0);

@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -276,27 +277,29 @@ int io_h2d_rows(rk_ctx *ctx, const rk_frags_soa &in, void *dev) {
   return RK_OK;
 }
 
-void gids_from_flags(rk_ctx *ctx, const uint8_t *flag, size_t n, uint32_t *gid) {
+// two phases on `threads` threads (counts per range, then the fill); the
+// phases meet at a spin barrier on an atomic counter
+void gids_from_flags_async(const uint8_t *flag, size_t n, uint32_t *gid, int threads, GidJob &job) {
   if (!n) return;
-  HostPool *pool = ctx->ioe->pool;  // io_d2h built the engine
-  const int T = pool->size();
+  const int T = threads < 1 ? 1 : threads;
   const size_t share = (n + T - 1) / T;
-  std::vector<uint32_t> cnt(T + 1, 0);
-  pool->run([&](int t) {
-    const size_t lo = std::min(n, (size_t)t * share), hi = std::min(n, lo + share);
-    uint32_t c = 0;
-    for (size_t i = lo; i < hi; ++i) c += flag[i] != 2;
-    cnt[t + 1] = c;
-  });
-  for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
-  pool->run([&](int t) {
-    const size_t lo = std::min(n, (size_t)t * share), hi = std::min(n, lo + share);
-    uint32_t g = cnt[t];
-    for (size_t i = lo; i < hi; ++i) {
-      g += flag[i] != 2;
-      gid[i] = g - 1;
-    }
-  });
+  auto cnt = std::make_shared<std::vector<uint32_t>>(T + 1, 0u);
+  auto arrived = std::make_shared<std::atomic<int>>(0);
+  for (int t = 0; t < T; ++t)
+    job.th.emplace_back([=] {
+      const size_t lo = std::min(n, (size_t)t * share), hi = std::min(n, lo + share);
+      uint32_t c = 0;
+      for (size_t i = lo; i < hi; ++i) c += flag[i] != 2;
+      (*cnt)[t + 1] = c;
+      arrived->fetch_add(1, std::memory_order_acq_rel);
+      while (arrived->load(std::memory_order_acquire) < T) std::this_thread::yield();
+      uint32_t g = 0;
+      for (int k = 0; k <= t; ++k) g += (*cnt)[k];
+      for (size_t i = lo; i < hi; ++i) {
+        g += flag[i] != 2;
+        gid[i] = g - 1;
+      }
+    });
 }
 
 double wall_ms() {

@@ -197,37 +197,60 @@ __device__ __forceinline__ void wave_run_add(uint32_t v, uint32_t *arr) {
 // caller's SoA in HBM, or the 12-B wire rows rk_classify uploads (packed on
 // the host: {xStart lo 32, yStart lo 32, length (24) | reverse (1) | yStart
 // >> 32 (3) | xStart >> 32 (4)}, rk_io.hip)
+// (raw: the row's loads only; unpack: what is computed from them -- a Src
+// with raw_t has every item's loads issued before any is used, see k_onesweep)
 struct RowSoA {
   const uint64_t *x, *y, *len;
   const uint8_t *strand;
+  struct raw_t {
+    uint64_t x, y, L;
+    uint8_t s;
+  };
+  __device__ __forceinline__ raw_t raw(uint32_t i) const { return raw_t{x[i], y[i], len[i], strand[i]}; }
+  __device__ __forceinline__ void unpack(const raw_t &r, uint64_t &xs, uint64_t &ys, uint64_t &L,
+                                         uint32_t &s) const {
+    xs = r.x, ys = r.y, L = r.L;
+    s = r.s != 'f' ? 1u : 0u;
+  }
   __device__ __forceinline__ void row(uint32_t i, uint64_t &xs, uint64_t &ys, uint64_t &L,
                                       uint32_t &s) const {
-    xs = x[i], ys = y[i], L = len[i];
-    s = strand[i] != 'f' ? 1u : 0u;
+    unpack(raw(i), xs, ys, L, s);
   }
 };
 struct RowWire {
   const uint3 *w;
+  using raw_t = uint3;
+  __device__ __forceinline__ raw_t raw(uint32_t i) const {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(w + i);
+    return make_uint3(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
+                      __builtin_nontemporal_load(p + 2));
+  }
+  __device__ __forceinline__ void unpack(const raw_t &r, uint64_t &xs, uint64_t &ys, uint64_t &L,
+                                         uint32_t &s) const {
+    xs = (uint64_t)(r.z >> 28) << 32 | r.x;
+    ys = (uint64_t)((r.z >> 25) & 7u) << 32 | r.y;
+    L = r.z & 0xFFFFFFu;
+    s = (r.z >> 24) & 1u;
+  }
   __device__ __forceinline__ void row(uint32_t i, uint64_t &xs, uint64_t &ys, uint64_t &L,
                                       uint32_t &s) const {
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(w + i);
-    const uint32_t a = __builtin_nontemporal_load(p), b = __builtin_nontemporal_load(p + 1),
-                   c = __builtin_nontemporal_load(p + 2);
-    xs = (uint64_t)(c >> 28) << 32 | a;
-    ys = (uint64_t)((c >> 25) & 7u) << 32 | b;
-    L = c & 0xFFFFFFu;
-    s = (c >> 24) & 1u;
+    unpack(raw(i), xs, ys, L, s);
   }
 };
 template <class Rows>
 struct SrcFile {
   using rec_t = uint4;
+  static constexpr bool kPerRow = true;  // see load_items (rk_onesweep.h)
   Rows rows;
   uint64_t vsize;
   __device__ __forceinline__ uint4 load(uint32_t i) const {
     uint64_t xs, ys, L;
     uint32_t s;
     rows.row(i, xs, ys, L, s);
+    return pack(xs, ys, L, s, i);
+  }
+  __device__ __forceinline__ uint4 pack(uint64_t xs, uint64_t ys, uint64_t L, uint32_t s,
+                                        uint32_t i) const {
     const uint64_t pk = div_small(xs, 10);
     const uint32_t key = (uint32_t)(pk < vsize - 1 ? pk : vsize - 1);
     // (rows that do not pack were flagged by k_nw_order_hist: the generic
@@ -356,17 +379,38 @@ struct DstCsr {
 // wave loads 64 consecutive records from a multiple of 64 (k_onesweep's
 // layout: the tile and every wave's slice are multiples of 64 records), so
 // the wave's 64 bits are one uniform 8-B load
+// The bits come after the record loads (fixup): lane l < ITEMS loads the
+// word of the wave's item l (its 64 records are 64 consecutive fragments from
+// a multiple of 64), and item r takes its word by a lane read; lane j of
+// every item group is record j of the group.
+template <int ITEMS>
+__device__ __forceinline__ void merge_xhit(uint3 (&rec)[ITEMS], const uint64_t *xbits64,
+                                           uint32_t nwords, uint32_t base, uint32_t wbase) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w0 = (base + wbase - lane) >> 6;  // the wave's first item group
+  const uint64_t wd = lane < (uint32_t)ITEMS && w0 + lane < nwords ? xbits64[w0 + lane] : 0ull;
+  const uint32_t lo = (uint32_t)wd, hi = (uint32_t)(wd >> 32);
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t l = __builtin_amdgcn_readlane(lo, r), h = __builtin_amdgcn_readlane(hi, r);
+    const uint32_t bit = ((lane < 32 ? l >> lane : h >> (lane - 32)) & 1u);
+    rec[r].z |= bit << 31;
+  }
+}
 struct SrcYX12 {
   using rec_t = uint3;
+  static constexpr bool kFixup = true;
   const uint3 *in;
   const uint64_t *xbits64;
+  uint32_t nwords;  // bitmask words: (records + 63) / 64
   __device__ __forceinline__ uint3 load(uint32_t i) const {
     const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
-    const uint32_t i0 = __builtin_amdgcn_readfirstlane(i) & ~63u;
-    const uint64_t w = xbits64[i0 >> 6];
-    const uint32_t hit = (uint32_t)(w >> (i - i0)) & 1u;
     return make_uint3(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
-                      __builtin_nontemporal_load(p + 2) | hit << 31);
+                      __builtin_nontemporal_load(p + 2));
+  }
+  template <int ITEMS>
+  __device__ __forceinline__ void fixup(uint3 (&rec)[ITEMS], uint32_t base, uint32_t wbase) const {
+    merge_xhit<ITEMS>(rec, xbits64, nwords, base, wbase);
   }
   __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
 };
@@ -375,17 +419,398 @@ struct SrcYX12 {
 // the arrival index (SrcIdx12) and the bit comes by arrival index
 struct SrcIdxYX12 {
   using rec_t = uint3;
+  static constexpr bool kFixup = true;
   const uint3 *in;
   const uint64_t *xbits64;
+  uint32_t nwords;  // bitmask words: (records + 63) / 64
   __device__ __forceinline__ uint3 load(uint32_t i) const {
     const uint32_t *p = reinterpret_cast<const uint32_t *>(in + i);
-    const uint32_t i0 = __builtin_amdgcn_readfirstlane(i) & ~63u;
-    const uint64_t w = xbits64[i0 >> 6];
-    const uint32_t hit = (uint32_t)(w >> (i - i0)) & 1u;
-    return make_uint3(__builtin_nontemporal_load(p), i, __builtin_nontemporal_load(p + 2) | hit << 31);
+    return make_uint3(__builtin_nontemporal_load(p), i, __builtin_nontemporal_load(p + 2));
+  }
+  template <int ITEMS>
+  __device__ __forceinline__ void fixup(uint3 (&rec)[ITEMS], uint32_t base, uint32_t wbase) const {
+    merge_xhit<ITEMS>(rec, xbits64, nwords, base, wbase);
   }
   __device__ __forceinline__ uint32_t key(const uint3 &r) const { return r.x; }
 };
+
+// --- processing order in two stages --------------------------------------
+// (nw_order_sort with a split plan, nw_order_split): the one-sweep passes
+// sort the records by the COARSE key K >> F only (C = b - F bits: cfg3's
+// 29-bit key as 14 bits in two 7-bit passes instead of four passes), the last
+// of them also counting the records of every coarse key (DstRecHist: one
+// global atomic per run of equal keys in a wave's consecutive sorted slots);
+// the counts' scan places every segment (the records of one coarse key, ~3000
+// at cfg3).  k_seg_fine then sorts each segment by its F fine bits in
+// LDS -- one block per segment, LSD by digits of up to 8 bits ranked by wave
+// ballots, stable like a record pass -- and writes the final records, the Y
+// records (DstProc's job) and the X-chunk counts (k_nw_xcount's job, which
+// needs the final order).  A segment above the LDS capacity is sorted by the
+// same block through global memory (chunks of OF_CAP in order: stable) --
+// correct for any input, slow only for pathological ones.
+struct DstRecHist {
+  static constexpr bool kWave = true;
+  static constexpr bool kPre = false;
+  uint4 *out;
+  uint32_t *chist;  // records per coarse key
+  int F;
+  __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const { out[pos] = r; }
+  __device__ __forceinline__ void wave(const uint4 &r, bool live) const {
+    wave_run_add(live ? r.x >> F : NONE, chist);
+  }
+};
+
+// the same coarse-key counts over 12-B records (the member sort by gid)
+struct DstRec12Hist {
+  static constexpr bool kWave = true;
+  static constexpr bool kPre = false;
+  uint3 *out;
+  uint32_t *chist;
+  int F;
+  __device__ __forceinline__ void store(uint32_t pos, const uint3 &r) const {
+    uint32_t *p = reinterpret_cast<uint32_t *>(out + pos);
+    p[0] = r.x, p[1] = r.y, p[2] = r.z;
+  }
+  __device__ __forceinline__ void wave(const uint3 &r, bool live) const {
+    wave_run_add(live ? r.x >> F : NONE, chist);
+  }
+};
+
+constexpr int OF_T = 512, OF_ITEMS = 8, OF_NW = OF_T / 64, OF_CAP = OF_T * OF_ITEMS;
+// the records inside the segment kernels as plain structs (kept in HIP's
+// vector types, the 16-B records' y/z/w went through a scratch array)
+struct P4 {
+  uint32_t x, y, z, w;
+};
+struct P3 {
+  uint32_t x, y, z;
+};
+template <class R>
+struct PodOf;
+template <>
+struct PodOf<uint4> {
+  using type = P4;
+  __device__ static __forceinline__ P4 from(const uint4 &v) { return P4{v.x, v.y, v.z, v.w}; }
+  __device__ static __forceinline__ uint4 to(const P4 &v) { return make_uint4(v.x, v.y, v.z, v.w); }
+};
+template <>
+struct PodOf<uint3> {
+  using type = P3;
+  __device__ static __forceinline__ P3 from(const uint3 &v) { return P3{v.x, v.y, v.z}; }
+  __device__ static __forceinline__ uint3 to(const P3 &v) { return make_uint3(v.x, v.y, v.z); }
+};
+template <class R>
+struct FineLds {
+  typename PodOf<R>::type srec[OF_CAP];
+  uint32_t wcnt[OF_NW][256];  // per-wave digit counters, then per-wave starts
+  uint32_t lbase[256];        // block-local digit starts
+  uint32_t run[256];          // global path: running digit offsets
+  uint32_t tot[256];          // global path: digit totals of a chunk / histogram
+  uint32_t wsum[OF_NW];
+};
+
+// Stable ranks of the block's records by digit d = (x >> shift) & (2^db - 1)
+// (x = the record's fine key): rec[r] sits at block index wbase + 64 r, live
+// below cnt.  Returns in rk[r] the record's slot among the wave's records of
+// its digit; afterwards L.wcnt[w][d] = wave w's start inside digit d, L.lbase[d]
+// = digit d's start in the block, L.tot[d] = its count.
+template <class R, class V>
+__device__ __forceinline__ void fine_rank(FineLds<R> &L, const V (&rec)[OF_ITEMS],
+                                          uint32_t (&rk)[OF_ITEMS], uint32_t (&dg)[OF_ITEMS],
+                                          uint32_t wbase, uint32_t cnt, uint32_t fmask, int shift,
+                                          int db) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t *mycnt = L.wcnt[w];
+  for (uint32_t d = lane; d < 256; d += 64) mycnt[d] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int r = 0; r < OF_ITEMS; ++r) {
+    const bool live = wbase + 64 * r < cnt;
+    const uint32_t d = live ? ((rec[r].x & fmask) >> shift) & ((1u << db) - 1u) : 0u;
+    dg[r] = d;
+    uint64_t peer = __ballot(live);
+    for (int b = 0; b < db; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peer &= bit ? bb : ~bb;
+    }
+    const uint32_t below = __popcll(peer & lt);
+    const uint32_t before = live ? mycnt[d] : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (live && below == 0) mycnt[d] = before + __popcll(peer);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    rk[r] = before + below;
+  }
+  __syncthreads();
+  // thread t < 256 owns digit t: the waves' starts inside it, then the block scan
+  const uint32_t t = threadIdx.x;
+  uint32_t tot = 0;
+  if (t < 256) {
+#pragma unroll
+    for (int k = 0; k < OF_NW; ++k) {
+      const uint32_t c = L.wcnt[k][t];
+      L.wcnt[k][t] = tot;
+      tot += c;
+    }
+  }
+  uint32_t inc = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if ((int)lane >= o) inc += v;
+  }
+  if (lane == 63) L.wsum[w] = inc;
+  __syncthreads();
+  if (t < 256) {
+    uint32_t at = inc - tot;
+    for (uint32_t k = 0; k < w; ++k) at += L.wsum[k];
+    L.lbase[t] = at;
+    L.tot[t] = tot;
+  }
+  __syncthreads();
+}
+
+// The processing order's emit: a position of the final order -- the record
+// and its Y record (DstProc), the X-chunk counts (k_nw_xcount's layout).
+// Every lane of the wave calls emit (first: the record's key differs from the
+// previous position's).
+// The X counts go to an LDS window of OE_WIN chunks from the segment's first
+// owner chunk (a segment spans 2^F xStart/10 keys: a few chunks), flushed with
+// one global atomic per non-zero bin after the segment (begin / end); a chunk
+// outside the window (a centre far past its xStart) takes a global atomic.
+// (The emit objects stay const: a kernel argument written to lives in scratch.)
+constexpr uint32_t OE_WIN = 256;
+struct OrderEmit {
+  static constexpr int kWin = 3 * OE_WIN;
+  DstProc dst;
+  uint32_t m;      // kept rows: the X counts take positions below m
+  uint32_t *cnts;  // X-chunk counts, or null
+  uint32_t lgW, nch, kdiv;
+  // the window's first chunk, after clearing the window
+  __device__ __forceinline__ uint32_t begin(uint32_t *win, uint32_t key0) const {
+    for (uint32_t j = threadIdx.x; j < (uint32_t)kWin; j += blockDim.x) win[j] = 0;
+    __syncthreads();
+    return key0 / kdiv;
+  }
+  __device__ __forceinline__ void emit(uint32_t *win, uint32_t w0, uint32_t pos, const uint4 &r,
+                                       bool live, bool) const {
+    if (live) dst.store(pos, r);
+    if (cnts) {
+      const bool kept = live && pos < m;
+      uint32_t vx = NONE, vo = NONE;
+      if (kept) {
+        const uint32_t cx = (uint32_t)((rec_x(r) + rec_len(r) / 2) / 100) >> lgW;
+        const uint32_t co = r.x / kdiv, st = rec_strand(r);
+        if (cx - w0 < OE_WIN) vx = st * OE_WIN + (cx - w0);
+        else atomicAdd(&cnts[st * nch + cx], 1u);
+        if (co - w0 < OE_WIN) vo = 2 * OE_WIN + (co - w0);
+        else atomicAdd(&cnts[2 * nch + co], 1u);
+      }
+      wave_run_add(vx, win);
+      wave_run_add(vo, win);
+    }
+  }
+  __device__ __forceinline__ void end(uint32_t *win, uint32_t w0) const {
+    __syncthreads();
+    if (!cnts) return;
+    for (uint32_t j = threadIdx.x; j < (uint32_t)kWin; j += blockDim.x) {
+      const uint32_t v = win[j];
+      if (!v) continue;
+      const uint32_t part = j / OE_WIN, ch = w0 + (j - part * OE_WIN);
+      atomicAdd(&cnts[part * nch + ch], v);
+    }
+  }
+};
+// The member sort's emit: the in-group sort arrays (DstMembers) and the group
+// starts (k_group_offsets' job: a group starts where the gid changes; the
+// last position closes goff[G] = m)
+struct MemberEmit {
+  static constexpr int kWin = 1;
+  uint32_t *sgid, *tag, *mrow;
+  uint64_t *key;
+  uint32_t *goff;
+  uint32_t G, m;
+  __device__ __forceinline__ uint32_t begin(uint32_t *, uint32_t) const { return 0; }
+  __device__ __forceinline__ void end(uint32_t *, uint32_t) const {}
+  __device__ __forceinline__ void emit(uint32_t *, uint32_t, uint32_t pos, const uint3 &r,
+                                       bool live, bool first) const {
+    if (!live) return;
+    sgid[pos] = r.x;
+    mrow[pos] = r.y;
+    key[pos] = r.z;
+    tag[pos] = pos;
+    if (first) goff[r.x] = pos;
+    if (pos + 1 == m) goff[G] = m;
+  }
+};
+
+// One block per segment: the F fine bits of its records, LSD by digits of up
+// to 8 bits, in LDS (at most OF_CAP records).  A larger segment is listed in
+// big (big[0] = count) for k_seg_big: kept apart, the LDS kernel's registers
+// hold no global-memory path (with it inline the records spilled to scratch).
+template <class R>
+struct SegArgs {
+  const R *in;          // sorted by coarse key, stable
+  R *A, *B;             // k_seg_big's buffers, its last pass landing in A
+  const uint32_t *off;  // nseg + 1 segment starts
+  uint32_t nseg;
+  int F;                // fine bits (>= 1)
+  uint32_t *big;        // [0] count, then the segments above OF_CAP
+};
+template <class R, class E>
+__global__ void __launch_bounds__(OF_T) __attribute__((amdgpu_waves_per_eu(4)))
+k_seg_fine(const SegArgs<R> a, const E e) {
+  __shared__ FineLds<R> L;
+  __shared__ uint32_t ewin[E::kWin];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, t = threadIdx.x;
+  const uint32_t wbase = w * (OF_CAP / OF_NW) + lane;
+  const uint32_t fmask = a.F >= 32 ? 0xFFFFFFFFu : (1u << a.F) - 1u;
+  const int np = (a.F + 7) / 8;
+  using P = PodOf<R>;
+  typename P::type rec[OF_ITEMS];
+  uint32_t rk[OF_ITEMS], dg[OF_ITEMS];
+  for (uint32_t sg = blockIdx.x; sg < a.nseg; sg += gridDim.x) {
+    const uint32_t s0 = a.off[sg], cnt = a.off[sg + 1] - s0;
+    if (cnt == 0) continue;
+    if (cnt > (uint32_t)OF_CAP) {
+      if (t == 0) a.big[1 + atomicAdd(&a.big[0], 1u)] = sg;
+      continue;
+    }
+#pragma unroll
+    for (int r = 0; r < OF_ITEMS; ++r) {
+      const uint32_t i = wbase + 64 * r;
+      rec[r] = P::from(a.in[s0 + (i < cnt ? i : cnt - 1)]);  // (dead lanes: a copy, no branch)
+    }
+    // LSD passes over the fine key; the last placement is the final order
+    for (int q = 0; q < np; ++q) {
+      const int shift = 8 * q, db = a.F - shift < 8 ? a.F - shift : 8;
+      fine_rank(L, rec, rk, dg, wbase, cnt, fmask, shift, db);
+#pragma unroll
+      for (int r = 0; r < OF_ITEMS; ++r)
+        if (wbase + 64 * r < cnt) L.srec[L.lbase[dg[r]] + L.wcnt[w][dg[r]] + rk[r]] = rec[r];
+      __syncthreads();
+      if (q + 1 < np) {
+#pragma unroll
+        for (int r = 0; r < OF_ITEMS; ++r) {
+          const uint32_t i = wbase + 64 * r;
+          rec[r] = L.srec[i < cnt ? i : cnt - 1];  // (unconditional: the array stays in VGPRs)
+        }
+        __syncthreads();
+      }
+    }
+    const uint32_t w0 = e.begin(ewin, L.srec[0].x);
+    for (uint32_t j0 = 0; j0 < cnt; j0 += OF_T) {
+      const uint32_t j = j0 + t;
+      const bool live = j < cnt;
+      const R r = P::to(L.srec[live ? j : cnt - 1]);
+      const bool first = live && (j == 0 || L.srec[j - 1].x != r.x);
+      e.emit(ewin, w0, s0 + j, r, live, first);
+    }
+    e.end(ewin, w0);
+    __syncthreads();  // the next segment reuses the LDS
+  }
+}
+
+// The listed segments above OF_CAP, one block each: the same passes through
+// global memory, chunk by chunk in order (stable); the last lands in A.  A
+// segment whose fine keys are all equal (one huge group of the member sort)
+// is already in order.
+template <class R, class E>
+__global__ void __launch_bounds__(OF_T) k_seg_big(const SegArgs<R> a, const E e) {
+  __shared__ FineLds<R> L;
+  __shared__ uint32_t ewin[E::kWin];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, t = threadIdx.x;
+  const uint32_t wbase = w * (OF_CAP / OF_NW) + lane;
+  const uint32_t fmask = a.F >= 32 ? 0xFFFFFFFFu : (1u << a.F) - 1u;
+  const int np = (a.F + 7) / 8;
+  using P = PodOf<R>;
+  typename P::type rec[OF_ITEMS];
+  uint32_t rk[OF_ITEMS], dg[OF_ITEMS];
+  const uint32_t nbig = a.big[0];
+  for (uint32_t k = blockIdx.x; k < nbig; k += gridDim.x) {
+    const uint32_t sg = a.big[1 + k];
+    const uint32_t s0 = a.off[sg], cnt = a.off[sg + 1] - s0;
+    const R *src = a.in + s0;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t j = t; j < cnt; j += OF_T) {
+      const uint32_t x = src[j].x & fmask;
+      lo = x < lo ? x : lo;
+      hi = x > hi ? x : hi;
+    }
+    if (t == 0) L.run[0] = 0xFFFFFFFFu, L.run[1] = 0;
+    __syncthreads();
+    atomicMin(&L.run[0], lo);
+    atomicMax(&L.run[1], hi);
+    __syncthreads();
+    const bool sorted = L.run[0] == L.run[1];
+    __syncthreads();
+    for (int q = 0; q < (sorted ? 0 : np); ++q) {
+      const int shift = 8 * q, db = a.F - shift < 8 ? a.F - shift : 8;
+      R *dst = ((np - 1 - q) % 2 == 0) ? a.A + s0 : a.B + s0;
+      // the pass' digit histogram over the segment, its scan into running starts
+      if (t < 256) L.tot[t] = 0;
+      __syncthreads();
+      for (uint32_t j = t; j < cnt; j += OF_T)
+        atomicAdd(&L.tot[((src[j].x & fmask) >> shift) & ((1u << db) - 1u)], 1u);
+      __syncthreads();
+      {
+        const uint32_t tot = t < 256 ? L.tot[t] : 0u;
+        uint32_t inc = tot;
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t v = __shfl_up(inc, o);
+          if ((int)lane >= o) inc += v;
+        }
+        if (lane == 63) L.wsum[w] = inc;
+        __syncthreads();
+        if (t < 256) {
+          uint32_t at = inc - tot;
+          for (uint32_t k2 = 0; k2 < w; ++k2) at += L.wsum[k2];
+          L.run[t] = at;
+        }
+        __syncthreads();
+      }
+      for (uint32_t c0 = 0; c0 < cnt; c0 += OF_CAP) {
+        const uint32_t cc = cnt - c0 < (uint32_t)OF_CAP ? cnt - c0 : (uint32_t)OF_CAP;
+#pragma unroll
+        for (int r = 0; r < OF_ITEMS; ++r) {
+          const uint32_t i = wbase + 64 * r;
+          rec[r] = P::from(src[c0 + (i < cc ? i : cc - 1)]);
+        }
+        fine_rank(L, rec, rk, dg, wbase, cc, fmask, shift, db);
+#pragma unroll
+        for (int r = 0; r < OF_ITEMS; ++r)
+          if (wbase + 64 * r < cc) dst[L.run[dg[r]] + L.wcnt[w][dg[r]] + rk[r]] = P::to(rec[r]);
+        __syncthreads();
+        if (t < 256) L.run[t] += L.tot[t];
+        __syncthreads();
+      }
+      // this block's global writes before its next reads of them: one CU,
+      // one L1 -- the barrier's workgroup-scope release/acquire suffices (an
+      // agent-scope fence would write the L2 back)
+      __syncthreads();
+      src = dst;
+    }
+    const R *fin = sorted ? a.in + s0 : a.A + s0;
+    const uint32_t w0 = e.begin(ewin, fin[0].x);
+    for (uint32_t j0 = 0; j0 < cnt; j0 += OF_T) {
+      const uint32_t j = j0 + t;
+      const bool live = j < cnt;
+      const R r = fin[live ? j : cnt - 1];
+      const bool first = live && (j == 0 || fin[j - 1].x != r.x);
+      e.emit(ewin, w0, s0 + j, r, live, first);
+    }
+    e.end(ewin, w0);
+    __syncthreads();
+  }
+}
+
+template <class R, class E>
+static void launch_seg(const SegArgs<R> &a, const E &e, hipStream_t st) {
+  (void)hipMemsetAsync(a.big, 0, 4, st);
+  k_seg_fine<<<a.nseg < 65536u ? a.nseg : 65536u, OF_T, 0, st>>>(a, e);
+  k_seg_big<<<256, OF_T, 0, st>>>(a, e);  // (returns at once when none is listed)
+}
 
 // --- group members, last pass: gid order (stable: processing order inside) -
 // members {gid, row, sort key lo, hi} -> group of every slot, sort key, tag =
@@ -1095,6 +1520,90 @@ void nw_order_sort_recs(const uint4 *in, uint32_t m, uint32_t nby, uint32_t base
   nw_order_passes(SrcRec{in}, 16.0, m, nby, base, a, ghist, status, Ra, Rb, yrec, st);
 }
 
+// The two-stage plan (see k_seg_fine): F fine bits for the segment
+// kernel -- as many as keep the average segment (n rows over the nkeys key
+// values, 2^F keys per segment) at most NW_SEG_TARGET rows, 3/4 of the LDS
+// capacity (cfg3: ~2730 rows; the global-memory path stays rare) -- and
+// C = b - F coarse bits for the one-sweep passes.  passes = 0: the LSD passes
+// over all b bits (too few rows, or RK_NW_SPLIT=0).
+constexpr uint32_t NW_SEG_TARGET = OF_CAP * 3 / 4;
+NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int b) {
+  NwOrderPlan o{};
+  static const bool on = [] {
+    const char *e = getenv("RK_NW_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  int F = 0;
+  while (F < b && (double)n * (double)(2ull << F) <= (double)NW_SEG_TARGET * (double)nkeys) ++F;
+  const int C = b - F;
+  if (!on || F < 1 || C < 1 || C > 24) return o;
+  o.F = F;
+  o.C = C;
+  o.coarse = nw_plan(C);
+  for (int p = 0; p < o.coarse.passes; ++p) o.coarse.shift[p] += o.F;
+  o.nseg = (uint32_t)1 << C;
+  return o;
+}
+
+// the coarse passes (the last writes Rb and counts the coarse keys into
+// chist, 2^C + 1 words, zeroed here), the scan into segment starts, the fine
+// kernel into Ra (+ Y records, + the X-chunk counts into cc.cnts when given,
+// zeroed here)
+template <class Src1>
+static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n, uint32_t m,
+                                  uint32_t nby, const NwOrderPlan &op, const uint32_t *ghist,
+                                  uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
+                                  uint4 *tmp, uint32_t *chist, uint32_t *coff, ScanScratch ss,
+                                  const NwChunkCounts *cc, hipStream_t st) {
+  const Digits D = to_digits(op.coarse);
+  const size_t sw = nw_status_words(n);
+  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  (void)hipMemsetAsync(chist, 0, ((size_t)op.nseg + 1) * 4, st);
+  const PassStatus ps = pass_status(status, n, D);
+  for (int p = 0; p < D.passes; ++p) {
+    uint4 *out = ((D.passes - 1 - p) % 2 == 0) ? Rb : Ra;  // the last coarse pass lands in Rb
+    const uint4 *src = ((D.passes - p) % 2 == 0) ? Rb : Ra;
+    ps.prepare(p, n, D, st);
+    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
+    uint32_t *ctr = status + sw - 64 + p;
+    const uint32_t *gh = ghist + p * 1024;
+    const bool last = p == D.passes - 1;
+    const DstRecHist dh{out, chist, op.F};
+    const double bytes = (p == 0 ? in_bytes : 16.0) * n + 16.0 * n;
+    if (p == 0 && last) launch_pass(first, dh, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else if (p == 0) launch_pass(first, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else if (last) launch_pass(SrcRec{src}, dh, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+  }
+  exclusive_scan_u32(chist, coff, (size_t)op.nseg + 1, ss, st);
+  OrderEmit oe{DstProc{Ra, reinterpret_cast<uint3 *>(yrec), nby, 0u}, m, nullptr, 0, 0, 0};
+  if (cc) {
+    (void)hipMemsetAsync(cc->cnts, 0, ((size_t)3 * cc->nch + 1) * 4, st);
+    oe.cnts = cc->cnts;
+    oe.lgW = cc->lgW;
+    oe.nch = cc->nch;
+    oe.kdiv = 10 * cc->W;
+  }
+  kt_begin(st, KID_NW_FINE);
+  // (the counts are free after the scan: the list of segments above OF_CAP)
+  launch_seg(SegArgs<uint4>{Rb, Ra, tmp, coff, op.nseg, op.F, chist}, oe, st);
+  // records in and out, Y records out (the X counts: no extra reads)
+  kt_end(st, KID_NW_FINE, 44.0 * n);
+}
+void nw_order_sort_split(const rk_frags_soa &in, uint32_t m, uint32_t nby, const NwOrderPlan &op,
+                         const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
+                         uint4 *yrec, uint4 *tmp, uint32_t *chist, uint32_t *coff,
+                         ScanScratch ss, const NwChunkCounts *cc, uint64_t vsize, hipStream_t st,
+                         const uint3 *wire) {
+  if (wire)
+    nw_order_passes_split(SrcFile<RowWire>{RowWire{wire}, vsize}, 12.0, (uint32_t)in.n, m, nby,
+                          op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
+  else
+    nw_order_passes_split(
+        SrcFile<RowSoA>{RowSoA{in.x_start, in.y_start, in.length, in.strand}, vsize}, 25.0,
+        (uint32_t)in.n, m, nby, op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
+}
+
 void nw_rec_hist(const void *recs, int rec_bytes, uint32_t n, uint32_t sub, const NwDigits &d,
                  uint32_t *ghist, hipStream_t st) {
   if (!n) return;
@@ -1187,9 +1696,11 @@ void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits
     const uint32_t *gh = ghist_of(yhist, p);
     const double bytes = (p == 0 ? 12.0 + 0.125 : 12.0) * m + (last ? 18.0 : 12.0) * m;
     if (p == 0 && src0)
-      y_after_x_first(SrcIdxYX12{src, bits64}, dc, out, last, m, D, gh, stp, ctr, st, bytes, nxt);
+      y_after_x_first(SrcIdxYX12{src, bits64, (m + 63) / 64}, dc, out, last, m, D, gh, stp, ctr,
+                      st, bytes, nxt);
     else if (p == 0)
-      y_after_x_first(SrcYX12{src, bits64}, dc, out, last, m, D, gh, stp, ctr, st, bytes, nxt);
+      y_after_x_first(SrcYX12{src, bits64, (m + 63) / 64}, dc, out, last, m, D, gh, stp, ctr, st,
+                      bytes, nxt);
     else if (last)
       launch_pass(SrcRec12{src}, dc, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
     else
@@ -1245,6 +1756,44 @@ void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t
   else
     nw_member_passes<uint4, SrcMem16, SrcRec, DstRec>(SrcMem16{erk, ehi, gidp}, t0, t1, m, e,
                                                       ehist, status, fin, st);
+}
+
+void nw_member_sort_split(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1,
+                          uint4 *t2, uint32_t m, uint32_t G, const NwOrderPlan &mp,
+                          const uint32_t *ehist, uint32_t *status, uint32_t *sgid, uint64_t *key,
+                          uint32_t *tag, uint32_t *mrow, uint32_t *goff, uint32_t *chist,
+                          uint32_t *coff, ScanScratch ss, hipStream_t st) {
+  const uint2 *erk = reinterpret_cast<const uint2 *>(erec);
+  uint3 *a = reinterpret_cast<uint3 *>(t0), *b = reinterpret_cast<uint3 *>(t1),
+        *c = reinterpret_cast<uint3 *>(t2);
+  const Digits D = to_digits(mp.coarse);
+  const size_t sw = nw_status_words(m);
+  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
+  (void)hipMemsetAsync(chist, 0, ((size_t)mp.nseg + 1) * 4, st);
+  const PassStatus ps = pass_status(status, m, D, 12);
+  const SrcMem12 s1{erk, gidp};
+  const uint3 *src = nullptr;
+  for (int p = 0; p < D.passes; ++p) {
+    uint3 *out = ((D.passes - 1 - p) % 2 == 0) ? b : a;  // the last coarse pass lands in b
+    ps.prepare(p, m, D, st);
+    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
+    uint32_t *ctr = status + sw - 64 + p;
+    const uint32_t *gh = ehist + p * 1024;
+    const bool last = p == D.passes - 1;
+    const DstRec12Hist dh{out, chist, mp.F};
+    const double bytes = 24.0 * m;
+    if (p == 0 && last) launch_pass(s1, dh, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else if (p == 0) launch_pass(s1, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else if (last) launch_pass(SrcRec12{src}, dh, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    src = out;
+  }
+  exclusive_scan_u32(chist, coff, (size_t)mp.nseg + 1, ss, st);
+  kt_begin(st, KID_NW_MFINE);
+  launch_seg(SegArgs<uint3>{b, a, c, coff, mp.nseg, mp.F, chist},
+             MemberEmit{sgid, tag, mrow, key, goff, G, m}, st);
+  // records in; gid, row, key (8 B), tag out; the group starts
+  kt_end(st, KID_NW_MFINE, 32.0 * m + 4.0 * G);
 }
 
 // the member sort of the sharded driver: received {gid, row, key ...} records

@@ -1260,7 +1260,7 @@ __device__ uint32_t wave_find_begin(const Axis &ax, uint32_t before, uint32_t ke
 // windows and walks their long runs in turn.
 __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lflag,
                                                       uint32_t nwin, uint8_t *rpend,
-                                                      uint32_t *counters) {
+                                                      uint32_t *counters, uint32_t *work) {
   __shared__ LongLds s_l[4];
   const uint32_t lane = threadIdx.x & 63;
   LongLds &L = s_l[threadIdx.x >> 6];
@@ -1280,6 +1280,7 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
       if (!rpend[beg]) continue;
       const uint32_t key = ax.key[beg];
       const uint32_t end = wave_find_end(ax, beg + LONG_RUN, key, lane);
+      if (work && lane == 0) atomicAdd(work, end - beg);  // entries walked (kernel timer)
       uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
       const bool has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
       if (has_lo) lo_e = beg, lo_b = wave_find_begin(ax, beg, key - 1, lane);
@@ -1573,10 +1574,13 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
 #endif
   }
   if (rl.fast32) {  // the long-run count lives on the device: a fixed grid reads it
+    // algorithmic bytes per entry of a walked run: its packed record (8 B),
+    // id (4 B), state read and write (2 B) and winner (4 B)
+    uint32_t *work = kt_units(st, KID_SWEEP_LONG);  // (its clear ahead of the start event)
     kt_begin(st, KID_SWEEP_LONG);
     k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<const uint8_t *>(rl.big), rl.nwin,
-                                         rpend, counters);
-    kt_end(st, KID_SWEEP_LONG, 0.0);
+                                         rpend, counters, work);
+    kt_end_units(st, KID_SWEEP_LONG, 18.0);
   } else if (rl.nbig) {
     kt_begin(st, KID_SWEEP_WAVE);
     k_sweep_wave<<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,

@@ -7,6 +7,8 @@
 // word.  Dst: store(pos, rec); kWave / wave(rec, live) (see rk_narrow.hip).
 #pragma once
 
+#include <type_traits>
+
 // ---------------------------------------------------------------------------
 // tile status words of the decoupled look-backs: 2 flag bits + a 30-bit count
 constexpr uint32_t SW_AGG = 1u << 30, SW_INC = 2u << 30, SW_VAL = (1u << 30) - 1;
@@ -47,6 +49,36 @@ __device__ __forceinline__ void sw_store(uint32_t *p, uint32_t v) {
 #define RK_LB_SLEEP 1
 #endif
 constexpr uint32_t LB_BATCH = RK_LB_BATCH;
+
+// Tile loads.  Every lane loads (dead ones a copy of the tile's last record):
+// no branch around a load, which made the compiler wait for each item's
+// round trip before issuing the next (SrcYX12's merged X-hit bit: 14 serial
+// HBM round trips in the tile prologue).  A Src with kPerRow keeps the
+// guarded per-item form (SrcFile: computing the records from every item's
+// raw columns at once spills 22-53 VGPRs under the 128-VGPR bound; per item
+// it waits for each item's round trip, in the first order pass only).  A Src
+// with kFixup adds per-wave extras after the loads (SrcYX12: the X-hit
+// bitmask words, one vector load for all items).
+template <class S, class = void>
+struct has_per_row : std::false_type {};
+template <class S>
+struct has_per_row<S, std::void_t<decltype(S::kPerRow)>> : std::true_type {};
+template <class S, class = void>
+struct has_fixup : std::false_type {};
+template <class S>
+struct has_fixup<S, std::void_t<decltype(S::kFixup)>> : std::true_type {};
+template <int ITEMS, class Src, class R>
+__device__ __forceinline__ void load_items(const Src &src, R (&rec)[ITEMS], uint32_t base,
+                                           uint32_t wbase, uint32_t cnt) {
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t i = wbase + r * 64;
+    if constexpr (has_per_row<Src>::value) rec[r] = i < cnt ? src.load(base + i) : R{};
+    else rec[r] = src.load(base + (i < cnt ? i : cnt - 1));
+  }
+  if constexpr (has_fixup<Src>::value) src.template fixup<ITEMS>(rec, base, wbase);
+}
+
 __device__ __forceinline__ uint32_t look_back(uint32_t *status, uint32_t tile, uint32_t stride,
                                               uint32_t slot, uint32_t mine) {
   uint32_t acc = 0;
@@ -95,8 +127,12 @@ __device__ __forceinline__ uint32_t look_back(uint32_t *status, uint32_t tile, u
 // one, and a tile's look-back only waits for smaller tiles, each of which is
 // held by a running block that publishes it without waiting for larger ones.
 // Src: load(i) -> record i, key(rec); Dst: store(pos, rec).
+// (two blocks per CU: 4 waves per SIMD at 512 threads -- at most 128 VGPRs,
+// which the branch-free tile loads would exceed unbounded)
 template <int T, int ITEMS, int DB, bool PERSIST, class Src, class Dst>
-__global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, uint32_t tiles,
+__global__ void __launch_bounds__(T)
+__attribute__((amdgpu_waves_per_eu(T >= 512 && ITEMS <= 14 ? 4 : 1)))
+k_onesweep(Src src, Dst dst, uint32_t n, uint32_t tiles,
                                                 int shift, const uint32_t *__restrict__ ghist,
                                                 uint32_t *__restrict__ status,
                                                 uint32_t *__restrict__ tile_ctr,
@@ -140,11 +176,7 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
   {
     const uint32_t tile0 = tile * (uint32_t)TILE;
     const uint32_t cnt = n - tile0 < (uint32_t)TILE ? n - tile0 : (uint32_t)TILE;
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t i = wbase + r * 64;
-      rec[r] = i < cnt ? src.load(tile0 + i) : R{};
-    }
+    load_items<ITEMS>(src, rec, tile0, wbase, cnt);
   }
   uint32_t *mycnt = wcnt[w];
   for (uint32_t it = 0;; ++it) {
@@ -232,11 +264,7 @@ __global__ void __launch_bounds__(T) k_onesweep(Src src, Dst dst, uint32_t n, ui
     if (next < tiles) {
       const uint32_t n0 = next * (uint32_t)TILE;
       const uint32_t ncnt = n - n0 < (uint32_t)TILE ? n - n0 : (uint32_t)TILE;
-#pragma unroll
-      for (int r = 0; r < ITEMS; ++r) {
-        const uint32_t i = wbase + r * 64;
-        rec[r] = i < ncnt ? src.load(n0 + i) : R{};
-      }
+      load_items<ITEMS>(src, rec, n0, wbase, ncnt);
     }
     if (owner) {
 #pragma unroll

@@ -389,6 +389,26 @@ def test_dense_x_chunks(gpu_ctx):
     assert st["pipeline"] == 1 and st["record_fallback"] == 0
 
 
+def test_order_split_paths(gpu_ctx):
+    """The processing order in two stages (coarse one-sweep passes, then one
+    block per coarse-key segment sorting its fine bits, k_nw_order_fine): the
+    segments in LDS (two fine passes here, F = 15), and segments above the LDS
+    capacity (4096 rows) sorted through global memory, with one fine pass
+    (test_dense_x_chunks) and with two (here): bit-exact with the oracle."""
+    L = 10_000_000
+    f = rk.synth(60_000, L, seed=66)
+    gpu_vs_oracle(gpu_ctx, f, L, L)
+    assert gpu_ctx.stats()["pipeline"] == 1
+    rng = np.random.default_rng(67)
+    k = 20_000  # xStart < 300 kbp: one coarse segment of ~21k rows
+    g = rk.Frags(np.concatenate([f.x_start, rng.integers(1, 300_000, k).astype(np.uint64)]),
+                 np.concatenate([f.y_start, rng.integers(1, L - 1000, k).astype(np.uint64)]),
+                 np.concatenate([f.length, rng.integers(20, 400, k).astype(np.uint64)]),
+                 np.concatenate([f.strand, rng.choice(np.array([ord("f"), ord("r")], np.uint8), k)]))
+    gpu_vs_oracle(gpu_ctx, g, L, L)
+    assert gpu_ctx.stats()["pipeline"] == 1
+
+
 @pytest.mark.parametrize("pos", [1, 63, 65, 1000, 19_999])
 def test_wide_length_detected_in_any_lane(pctx, pos):
     """A single length >= 2^31 at any row position switches to the 64-bit
@@ -413,7 +433,8 @@ print(h.hexdigest(), r.n_groups)
 """
 
 
-@pytest.mark.parametrize("env", ["RK_GS_BIG=0", "RK_GS_BIG=4", "RK_GS_REG1=0", "RK_NW_MINBITS=8"])
+@pytest.mark.parametrize("env", ["RK_GS_BIG=0", "RK_GS_BIG=4", "RK_GS_REG1=0", "RK_NW_MINBITS=8",
+                                 "RK_NW_SPLIT=0"])
 def test_schedule_switches_bit_identical(gpu_ctx, env):
     """The measurement switches only move work between streams or change the
     radix of a pass: the result must not change.  300k rows at cfg3 density

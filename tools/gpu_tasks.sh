@@ -1,0 +1,98 @@
+#!/bin/bash
+# GPU-box command tasks for gpurun (run from the repo root).  Every GPU step
+# has its own time limit and a task stops at its first failure.
+#
+#   bash tools/gpu_tasks.sh TASK OUTDIR [ARGS...]
+#
+#   suite     smoke() and the whole GPU suite, as the driver runs them
+#   bench     the driver's bench command (cfg3, 20 steps, CPU baseline)
+#   refresh   bench + rocprofv3 --kernel-trace --stats of it + the PMC passes
+#             (tools/pmc_run.sh) + cfg5 on one GPU + the ratio-pair batch
+#   cfg5      tools/cfg5_check.py (1B fragments: timing, determinism,
+#             properties) and the cfg5 bench line
+#   ablib     record-pipeline parity, then benches of the working tree's
+#             library interleaved with tools/mb/base (a build of an earlier
+#             HEAD) through RK_LIB
+#   abenv     the same with environment variants: ARGS = "VAR=a" "VAR=b" ...
+#   trace     per-tile phase times of every record pass (RK_NW_TRACE)
+#   shard     sharded parity tests (+ the large sharded digests with ARGS=large)
+#             and the world-1 sharded bench
+#   rehearse  the N > 1 bench line on one GPU: two ranks on device 0 over gloo
+#             host callbacks, the RCCL attempt (RCCL refuses two ranks on one
+#             GPU: value null with the error), the world-1 sharded leg
+#   serial    per-kernel times with every kernel on one stream (RK_ONE_STREAM=1)
+export TMPDIR=/tmp
+TASK=$1
+O=${2:-gpurun_out/$TASK}
+shift 2
+mkdir -p $O
+
+bench() {  # bench NAME [bench args...]
+  local name=$1
+  shift
+  timeout -k 10 600 python3 bench.py "$@" > $O/$name.json 2> $O/$name.err
+}
+
+case $TASK in
+suite)
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+  timeout -k 10 1100 python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 2
+  ;;
+bench)
+  bench bench --gpus 1 --steps 20 --warmup 5 || exit 1
+  ;;
+refresh)
+  bench bench --gpus 1 --steps 20 --warmup 5 || exit 1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o p -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $O/prof.log 2>&1 || exit 2
+  bash tools/pmc_run.sh $O/pmc --no-cpu --steps 3 --warmup 1 || exit 3
+  bench bench_cfg5 --gpus 1 --config cfg5 --steps 3 --warmup 1 --no-cpu || exit 4
+  timeout -k 10 600 python3 tools/pairs_bench.py > $O/pairs.json 2> $O/pairs.err || exit 5
+  ;;
+cfg5)
+  timeout -k 10 600 python3 -u tools/cfg5_check.py --out $O/cfg5_check.json > $O/cfg5_check.log 2>&1 || exit 1
+  bench bench_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
+  ;;
+ablib)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  for rep in 1 2 3; do
+    RK_LIB=repkiller_amd/librepkiller_amd.so bench new_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 2
+    RK_LIB=tools/mb/base/librepkiller_amd.so bench base_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 3
+  done
+  ;;
+abenv)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  for rep in 1 2; do
+    i=0
+    for E in "$@"; do
+      i=$((i+1))
+      env $E timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $O/v${i}_$rep.json 2> $O/v${i}_$rep.err || exit 2
+    done
+  done
+  ;;
+trace)
+  RK_NW_TRACE=$O/trace.bin timeout -k 10 300 python3 bench.py --no-cpu --steps 2 --warmup 1 > $O/bt.json 2> $O/bt.err || exit 1
+  python3 tools/nw_trace.py $O/trace.bin > $O/trace.txt 2>&1
+  rm -f $O/trace.bin
+  ;;
+shard)
+  timeout -k 10 600 python3 -u -m pytest tests/test_sharded.py -x -q --timeout 300 --timeout-method thread > $O/sharded_tests.log 2>&1 || exit 1
+  if [ "$1" = large ]; then
+    timeout -k 10 900 python3 -u -m pytest tests/test_large_configs.py -x -q -k sharded --timeout 600 --timeout-method thread > $O/large_tests.log 2>&1 || exit 2
+  fi
+  bench sharded_w1 --mode sharded --steps 20 --warmup 5 --no-cpu || exit 3
+  ;;
+rehearse)
+  RK_BENCH_SAME_GPU=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --config cfg2 --comm host --steps 3 --warmup 1 > $O/host2.json 2> $O/host2.err || exit 1
+  RK_BENCH_SAME_GPU=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --config cfg2 --steps 3 --warmup 1 --sharded-timeout 60 > $O/rccl2.json 2> $O/rccl2.err
+  echo "rccl2 exit $?" > $O/rccl2.rc
+  bench sharded_w1 --mode sharded --no-cpu --steps 5 --warmup 2 || exit 3
+  ;;
+serial)
+  RK_ONE_STREAM=1 bench cfg3 --no-cpu || exit 1
+  RK_ONE_STREAM=1 bench cfg5 --config cfg5 --no-cpu --steps 2 --warmup 1 || exit 2
+  ;;
+*)
+  echo "unknown task $TASK" >&2
+  exit 64
+  ;;
+esac
