@@ -248,9 +248,13 @@ def full_size_reference(cfg: dict) -> dict | None:
 
 def load_traffic(kernel: str, config: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/pmc_run.sh -> profiles/traffic.json), only when they were measured on
-    this run's config; otherwise None (not measured for this workload)."""
+    (tools/pmc_run.sh -> profiles/traffic.json, or traffic_<config>.json for
+    another config), only when they were measured on this run's config;
+    otherwise None (not measured for this workload)."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
+    alt = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
+    if os.path.exists(alt):
+        path = alt
     try:
         with open(path) as fh:
             t = json.load(fh)

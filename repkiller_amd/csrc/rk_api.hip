@@ -381,8 +381,8 @@ size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
   w.scan_cap = rk::scan_blocks(n + 1) + 64;
   w.scan = c.take<uint32_t>(w.scan_cap);
   // the two-stage order sort's segment counts and starts (<= n / 1536 + 1 each)
-  w.chist = c.take<uint32_t>(n / 1024 + 64);
-  w.coff = c.take<uint32_t>(n / 1024 + 64);
+  w.chist = c.take<uint32_t>(rk::nw_seg_words(n));
+  w.coff = c.take<uint32_t>(rk::nw_seg_words(n));
   return c.off;
 }
 

@@ -584,9 +584,29 @@ __device__ void reg_batch(const V &v, bool in, int bl, uint32_t bm, int len, int
     reg_finish<GLOBAL, uint32_t, V>(v, in, bl, bm, len, d, lane, k, t, out);
 }
 
+// The lanes that sort one group: the whole wavefront (W = 64), or one half of
+// it (W = 32: two groups per wavefront, each half with its own LDS slab and
+// stack).  Halves diverge freely -- a ballot sees only the lanes still running
+// that code -- so every mask is shifted down to the half's own lanes.  With
+// two groups per instruction stream the fixed part of every partition (the
+// median by one lane, the stopper search, the cut, the stack) and the
+// segments of <= 32 members cost half the issue slots per group.
+template <int W>
+struct GLanes {
+  uint32_t lane;  // [0, W)
+  uint32_t base;  // this group's first lane in the wavefront (0 or 32)
+  __device__ __forceinline__ uint64_t ballot(bool p) const {
+    return W == 64 ? (uint64_t)__ballot(p) : ((uint64_t)__ballot(p) >> base) & 0xffffffffull;
+  }
+  __device__ __forceinline__ uint32_t bcast(uint32_t x) const {  // from lane 0 of the group
+    return (uint32_t)__shfl((int)x, (int)base);
+  }
+};
+
 // wavefront-parallel __unguarded_partition_pivot on [f, l); returns the cut
-template <bool GLOBAL, class V>
-__device__ uint32_t wave_partition(const V &v, uint32_t f, uint32_t l, uint32_t lane) {
+template <bool GLOBAL, class V, int W>
+__device__ uint32_t wave_partition(const V &v, uint32_t f, uint32_t l, GLanes<W> L) {
+  const uint32_t lane = L.lane;
   // __move_median_to_first by lane 0 with every read issued up front (the
   // three candidates and the first slot, then the median's tag); the pivot
   // (the median's key) reaches the other lanes by a lane read, not from memory
@@ -615,21 +635,21 @@ __device__ uint32_t wave_partition(const V &v, uint32_t f, uint32_t l, uint32_t 
   }
   if (sizeof(p) == 8) {
     const uint64_t p64 = (uint64_t)p;
-    p = (typename V::key_t)((uint64_t)(uint32_t)__shfl((int)(uint32_t)p64, 0) |
-                            (uint64_t)(uint32_t)__shfl((int)(uint32_t)(p64 >> 32), 0) << 32);
+    p = (typename V::key_t)((uint64_t)L.bcast((uint32_t)p64) |
+                            (uint64_t)L.bcast((uint32_t)(p64 >> 32)) << 32);
   } else {
-    p = (typename V::key_t)(uint32_t)__shfl((int)(uint32_t)p, 0);
+    p = (typename V::key_t)L.bcast((uint32_t)p);
   }
   sync_mem<GLOBAL>();
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t nL = 0, nR = 0;
-  for (uint32_t c = f; c < l; c += 64) {
+  for (uint32_t c = f; c < l; c += W) {
     const uint32_t x = c + lane;
     const bool in = x < l;
     const typename V::key_t k = in ? v.K[x] : 0;
     const bool lf = in && x > f && !(k < p);
     const bool rf = in && !(p < k);
-    const uint64_t bl = __ballot(lf), br = __ballot(rf);
+    const uint64_t bl = L.ballot(lf), br = L.ballot(rf);
     if (lf) v.PL[nL + __popcll(bl & lt)] = x;
     if (rf) v.PR[nR + __popcll(br & lt)] = x;
     nL += __popcll(bl);
@@ -639,16 +659,16 @@ __device__ uint32_t wave_partition(const V &v, uint32_t f, uint32_t l, uint32_t 
   // K = first k with Lpos[k] >= Rpos[k]; Rpos[k] = PR[nR-1-k] (k-th from the right)
   const uint32_t lim = nL < nR ? nL : nR;
   uint32_t K = lim;
-  for (uint32_t c = 0; c < lim; c += 64) {
+  for (uint32_t c = 0; c < lim; c += W) {
     const uint32_t k = c + lane;
     const bool stop = k < lim && v.PL[k] >= v.PR[nR - 1 - k];
-    const uint64_t b = __ballot(stop);
+    const uint64_t b = L.ballot(stop);
     if (b) {
       K = c + (uint32_t)__ffsll((unsigned long long)b) - 1;
       break;
     }
   }
-  for (uint32_t c = 0; c < K; c += 64) {
+  for (uint32_t c = 0; c < K; c += W) {
     const uint32_t k = c + lane;
     if (k < K) vswap(v, v.PL[k], v.PR[nR - 1 - k]);
   }
@@ -680,15 +700,18 @@ __device__ unsigned long long g_gs_prof[8];
 
 // the whole libstdc++ std::sort of one group [0, n) of view v, then stable
 // leaf ranks written to out[0..n) (tags only)
-template <bool GLOBAL, class V>
+template <bool GLOBAL, class V, int W = 64>
 __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stack,
-                              Frame *smallq, Frame *heapq, uint32_t lane, int d0,
+                              Frame *smallq, Frame *heapq, GLanes<W> L, int d0,
                               uint32_t reg_max) {
+  static_assert(W == 64 || W == 32, "a wavefront or a half");
+  const uint32_t lane = L.lane;
+  if (W != 64) reg_max = 0;  // register batches assume the whole wavefront
   GS_T(0);
 #ifdef RK_GS_PROF
   uint64_t part_cyc = 0, nparts = 0;
 #endif
-  for (uint32_t x = lane; x < n; x += 64) v.B[x] = 0;
+  for (uint32_t x = lane; x < n; x += W) v.B[x] = 0;
   int sp = 0, nsmall = 0, nheap = 0;
   if (lane == 0) stack[0] = {0u, n, d0};
   sp = 1;
@@ -715,7 +738,7 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
 #ifdef RK_GS_PROF
       const uint64_t _p0 = __builtin_amdgcn_s_memtime();
 #endif
-      const uint32_t cut = wave_partition<GLOBAL, V>(v, f, l, lane);
+      const uint32_t cut = wave_partition<GLOBAL, V, W>(v, f, l, L);
 #ifdef RK_GS_PROF
       part_cyc += __builtin_amdgcn_s_memtime() - _p0;
       ++nparts;
@@ -732,7 +755,7 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
   uint64_t nbatch = 0;
 #endif
   // small segments, packed up to three per 64-lane batch
-  for (int q0 = 0; q0 < nsmall;) {
+  for (int q0 = 0; W == 64 && q0 < nsmall;) {
 #ifdef RK_GS_PROF
     ++nbatch;
 #endif
@@ -748,7 +771,7 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
   }
   sync_mem<GLOBAL>();
   GS_T(2);
-  for (int q = (int)lane; q < nheap; q += 64) heap_sort_segment(v, heapq[q].f, heapq[q].l);
+  for (int q = (int)lane; q < nheap; q += W) heap_sort_segment(v, heapq[q].f, heapq[q].l);
   sync_mem<GLOBAL>();
   // __final_insertion_sort == stable sort inside every leaf (segments
   // finished in registers are already written, B == 3).  A leaf is a B == 1
@@ -756,16 +779,16 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
   // ballot over this chunk's B and one over the next chunk's, and the rank
   // reads are independent (one LDS round trip).
   uint32_t carry = 0;  // start of the leaf still open at the end of the previous chunk
-  for (uint32_t c = 0; c < n; c += 64) {
+  for (uint32_t c = 0; c < n; c += W) {
     const uint32_t x = c + lane;
     const uint8_t b = x < n ? v.B[x] : 1;
-    const uint8_t bn = x + 64 < n ? v.B[x + 64] : 1;
-    const uint64_t bd = __ballot(b != 0), bdn = __ballot(bn != 0);
+    const uint8_t bn = x + W < n ? v.B[x + W] : 1;
+    const uint64_t bd = L.ballot(b != 0), bdn = L.ballot(bn != 0);
     const uint64_t upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
     const uint64_t le = bd & upto, gt = bd & ~upto;
     const uint32_t s = le ? c + 63 - (uint32_t)__clzll(le) : carry;
     const uint32_t e = gt ? c + (uint32_t)__builtin_ctzll(gt)
-                          : bdn ? c + 64 + (uint32_t)__builtin_ctzll(bdn) : c + 128;
+                          : bdn ? c + W + (uint32_t)__builtin_ctzll(bdn) : c + 2 * W;
     if (bd) carry = c + 63 - (uint32_t)__clzll(bd);
     if (x < n && b != 3) {
       if (b == 2) {
@@ -850,18 +873,25 @@ __host__ __device__ constexpr uint32_t lds_stack(uint32_t cap) {
 // WPB independent wavefronts per block, each with its own LDS slab of `slab`
 // bytes (a CU holds a bounded number of blocks, so one-wave blocks of the
 // small caps leave it with few resident wavefronts)
-template <class KT, int WPB>
-__global__ void __launch_bounds__(64 * WPB) k_sort_groups_lds(TierLists tl, int tier,
+// (W = 32: each half of a wavefront sorts its own group in its own slab)
+template <class KT, int WPB, int W = 64>
+__global__ void __launch_bounds__(64 * WPB)
+__attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_groups_lds(TierLists tl, int tier,
                                                               const uint32_t *goff,
                                                               const uint64_t *key,
                                                               const uint32_t *tag, uint32_t *otag,
                                                               uint32_t cap, uint32_t reg_max,
                                                               uint32_t slab) {
   extern __shared__ __align__(16) uint8_t smem_all[];
+  constexpr uint32_t GPW = 64 / W;  // groups per wavefront
   // the wavefront index in a scalar register: every LDS base stays uniform
-  const uint32_t lane = threadIdx.x & 63,
+  // (per half when W = 32)
+  const uint32_t wl = threadIdx.x & 63,
                  wv = WPB == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t *smem = smem_all + (size_t)wv * slab;
+  const uint32_t half = W == 64 ? 0u : wl / W;
+  const GLanes<W> L{wl & (W - 1), half * W};
+  const uint32_t lane = L.lane;
+  uint8_t *smem = smem_all + ((size_t)wv * GPW + half) * slab;
   const uint32_t nfr = cap / (THRESH + 1) + 2;
   KT *K = reinterpret_cast<KT *>(smem);
   uint32_t *T = reinterpret_cast<uint32_t *>(K + cap);
@@ -874,16 +904,17 @@ __global__ void __launch_bounds__(64 * WPB) k_sort_groups_lds(TierLists tl, int 
   const ViewT<KT, uint16_t> v{K, T, PL, PR, B};
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
-  for (uint32_t w = lo + blockIdx.x * WPB + wv; w < hi; w += gridDim.x * WPB) {
+  for (uint32_t w = lo + (blockIdx.x * WPB + wv) * GPW + half; w < hi;
+       w += gridDim.x * WPB * GPW) {
     const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
-    for (uint32_t x = lane; x < n; x += 64) {
+    for (uint32_t x = lane; x < n; x += W) {
       K[x] = (KT)key[b + x];
       T[x] = tag[b + x];
     }
     wave_sync();
-    wave_std_sort<false>(v, n, otag + b, stack, smallq, heapq, lane, 2 * (31 - __clz((int)n)),
-                         reg_max);
+    wave_std_sort<false, ViewT<KT, uint16_t>, W>(v, n, otag + b, stack, smallq, heapq, L,
+                                                 2 * (31 - __clz((int)n)), reg_max);
     wave_sync();
   }
 }
@@ -1161,7 +1192,8 @@ __global__ void __launch_bounds__(64 * WPB) k_sort_segments(TierLists tl, int ti
         T[y] = tag[x + y];
       }
       wave_sync();
-      wave_std_sort<false>(v, n, otag + x, stack, smallq, heapq, lane, (int)(h >> 16), reg_max);
+      wave_std_sort<false>(v, n, otag + x, stack, smallq, heapq, GLanes<64>{lane, 0u},
+                           (int)(h >> 16), reg_max);
       wave_sync();
     }
   }
@@ -1376,13 +1408,28 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     const char *e = getenv("RK_GS_WPB");
     return e && atoi(e) == 4 ? 4 : 1;
   }();
+  // LDS tiers up to `half_cap` members sort two groups per wavefront, one per
+  // half (RK_GS_HALF: that cap; default 0 = whole wavefronts everywhere).
+  // Measured at cfg3 with 256: LDS tiers 1.92-1.95 against 1.55 ms, group-sort
+  // phase 1.28-1.29 against 1.14-1.18 ms -- slower, kept as an option
+  static const uint32_t half_cap = [] {
+    const char *e = getenv("RK_GS_HALF");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
   auto launch_lds = [&](int j, hipStream_t sj) {
     const uint32_t cap = caps.c[j];
     const uint32_t waves = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
     const int wp = cap <= 512 ? wpb : 1;
     const size_t slab = (lds_bytes(cap, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
     kt_begin(sj, KID_SORT_LDS);
-    if (wp == 4) {
+    if (cap <= half_cap && 2 * slab <= 65536) {
+      if (narrow_keys)
+        k_sort_groups_lds<uint32_t, 1, 32><<<waves / 2, 64, 2 * slab, sj>>>(
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, 0u, (uint32_t)slab);
+      else
+        k_sort_groups_lds<uint64_t, 1, 32><<<waves / 2, 64, 2 * slab, sj>>>(
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, 0u, (uint32_t)slab);
+    } else if (wp == 4) {
       if (narrow_keys)
         k_sort_groups_lds<uint32_t, 4><<<waves / 4, 256, 4 * slab, sj>>>(
             tl, TIER_LDS0 + j, goff, key, tag, otag, cap, reg_max, (uint32_t)slab);

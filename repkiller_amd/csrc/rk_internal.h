@@ -295,6 +295,15 @@ struct NwOrderPlan {
   NwDigits coarse{};
 };
 NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int bits);  // nkeys: key values in use
+// words of each segment array (counts, starts) a split sort of n rows may use
+inline size_t nw_seg_words(uint32_t n) { return (size_t)n / 512 + 64; }
+// the same over records received by the sharded driver (processing index base
+// + position; no X-chunk counts); tmp: m records of scratch
+void nw_order_sort_recs_split(const uint4 *in, uint32_t m, uint32_t nby, uint32_t base,
+                              const NwOrderPlan &op, const uint32_t *ghist, uint32_t *status,
+                              uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
+                              uint32_t *coff, ScanScratch ss, const NwChunkCounts *cc,
+                              hipStream_t st);
 void nw_order_sort_split(const rk_frags_soa &in, uint32_t m, uint32_t nby, const NwOrderPlan &op,
                          const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
                          uint4 *yrec, uint4 *tmp, uint32_t *chist, uint32_t *coff,
@@ -310,6 +319,8 @@ void nw_member_sort_split(const uint4 *erec, const uint32_t *gidp, uint4 *t0, ui
                           uint32_t *tag, uint32_t *mrow, uint32_t *goff, uint32_t *chist,
                           uint32_t *coff, ScanScratch ss, hipStream_t st);
 // (halo, G): the sharded driver's G lead-in records ahead of R (R holds m - G)
+// the halo's G records added to counts already in cc.cnts (no clearing)
+void nw_x_count_add(const uint4 *halo, uint32_t G, const NwChunkCounts &cc, hipStream_t st);
 void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t st,
                 const uint4 *halo = nullptr, uint32_t G = 0);
 // arrival_ids: the first pass numbers the entries by position (the sharded

@@ -591,7 +591,7 @@ struct OrderEmit {
   __device__ __forceinline__ uint32_t begin(uint32_t *win, uint32_t key0) const {
     for (uint32_t j = threadIdx.x; j < (uint32_t)kWin; j += blockDim.x) win[j] = 0;
     __syncthreads();
-    return key0 / kdiv;
+    return cnts ? key0 / kdiv : 0u;
   }
   __device__ __forceinline__ void emit(uint32_t *win, uint32_t w0, uint32_t pos, const uint4 &r,
                                        bool live, bool) const {
@@ -1536,7 +1536,8 @@ NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int b) {
   int F = 0;
   while (F < b && (double)n * (double)(2ull << F) <= (double)NW_SEG_TARGET * (double)nkeys) ++F;
   const int C = b - F;
-  if (!on || F < 1 || C < 1 || C > 24) return o;
+  // (2^C + 1 segment counts must fit nw_seg_words(n): 2^C < 4n / NW_SEG_TARGET)
+  if (!on || F < 1 || C < 1 || C > 24 || ((size_t)1 << C) + 1 > nw_seg_words(n)) return o;
   o.F = F;
   o.C = C;
   o.coarse = nw_plan(C);
@@ -1551,7 +1552,8 @@ NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int b) {
 // zeroed here)
 template <class Src1>
 static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n, uint32_t m,
-                                  uint32_t nby, const NwOrderPlan &op, const uint32_t *ghist,
+                                  uint32_t nby, uint32_t base, const NwOrderPlan &op,
+                                  const uint32_t *ghist,
                                   uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
                                   uint4 *tmp, uint32_t *chist, uint32_t *coff, ScanScratch ss,
                                   const NwChunkCounts *cc, hipStream_t st) {
@@ -1576,7 +1578,7 @@ static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n
     else launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
   }
   exclusive_scan_u32(chist, coff, (size_t)op.nseg + 1, ss, st);
-  OrderEmit oe{DstProc{Ra, reinterpret_cast<uint3 *>(yrec), nby, 0u}, m, nullptr, 0, 0, 0};
+  OrderEmit oe{DstProc{Ra, reinterpret_cast<uint3 *>(yrec), nby, base}, m, nullptr, 0, 0, 0};
   if (cc) {
     (void)hipMemsetAsync(cc->cnts, 0, ((size_t)3 * cc->nch + 1) * 4, st);
     oe.cnts = cc->cnts;
@@ -1597,11 +1599,19 @@ void nw_order_sort_split(const rk_frags_soa &in, uint32_t m, uint32_t nby, const
                          const uint3 *wire) {
   if (wire)
     nw_order_passes_split(SrcFile<RowWire>{RowWire{wire}, vsize}, 12.0, (uint32_t)in.n, m, nby,
-                          op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
+                          0u, op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
   else
     nw_order_passes_split(
         SrcFile<RowSoA>{RowSoA{in.x_start, in.y_start, in.length, in.strand}, vsize}, 25.0,
-        (uint32_t)in.n, m, nby, op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
+        (uint32_t)in.n, m, nby, 0u, op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
+}
+void nw_order_sort_recs_split(const uint4 *in, uint32_t m, uint32_t nby, uint32_t base,
+                              const NwOrderPlan &op, const uint32_t *ghist, uint32_t *status,
+                              uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
+                              uint32_t *coff, ScanScratch ss, const NwChunkCounts *cc,
+                              hipStream_t st) {
+  nw_order_passes_split(SrcRec{in}, 16.0, m, m, nby, base, op, ghist, status, Ra, Rb, yrec, tmp,
+                        chist, coff, ss, cc, st);
 }
 
 void nw_rec_hist(const void *recs, int rec_bytes, uint32_t n, uint32_t sub, const NwDigits &d,
@@ -1830,6 +1840,14 @@ void nw_x_count(const uint4 *R, uint32_t m, const NwChunkCounts &cc, hipStream_t
   k_nw_xcount<<<(m + XN_T * XN_ITEMS - 1) / (XN_T * XN_ITEMS), XN_T, 0, st>>>(
       RecView{halo, G, R}, m, cc.lgW, cc.nch, 10 * cc.W, cc.cnts);
   kt_end(st, KID_NW_XCOUNT, 16.0 * m);
+}
+
+void nw_x_count_add(const uint4 *halo, uint32_t G, const NwChunkCounts &cc, hipStream_t st) {
+  if (!G) return;
+  kt_begin(st, KID_NW_XCOUNT);
+  k_nw_xcount<<<(G + XN_T * XN_ITEMS - 1) / (XN_T * XN_ITEMS), XN_T, 0, st>>>(
+      RecView{halo, G, halo}, G, cc.lgW, cc.nch, 10 * cc.W, cc.cnts);
+  kt_end(st, KID_NW_XCOUNT, 16.0 * G);
 }
 
 void nw_x_chunks(const uint4 *R, uint32_t m, uint32_t nbx, uint64_t max_x, uint32_t maxlen,

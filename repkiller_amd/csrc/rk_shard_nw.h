@@ -339,7 +339,7 @@ enum SlotNw : int {
   SN_HSEL, SN_SY, SN_YR, SN_YA, SN_YB, SN_XCNT, SN_XOFF, SN_XKEY, SN_XENT, SN_XPK, SN_XNBD,
   SN_XSTATE, SN_XPOS, SN_EREC, SN_PAR, SN_XGUSED, SN_YKEY, SN_YENT, SN_YPK, SN_YNBD, SN_YST,
   SN_XBITS, SN_PARL, SN_SMEM, SN_T0, SN_T1, SN_SGID, SN_MROW, SN_KEY, SN_TAG, SN_GOFF, SN_YSEL,
-  SN_SXH, SN_COUNT
+  SN_SXH, SN_CHIST, SN_COFF, SN_XCNT0, SN_COUNT
 };
 static_assert(SN_COUNT <= kPoolSlots, "rk_shard.hip kPoolSlots");
 
@@ -472,7 +472,32 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   uint32_t *astat = S.take<uint32_t>(SN_STAT, sw);
   uint4 *Ra = S.take<uint4>(SN_RA, m + 1), *Rb = S.take<uint4>(SN_RB, m + 1);
   uint4 *yown = S.take<uint4>(SN_YOWN, (size_t)m * 3 / 4 + 2);  // 12-B records
-  if (m) {
+  // the two-stage order sort (coarse passes, per-segment LDS sort) when the
+  // slice's key density suits it: the slice holds m rows over its own key
+  // span, and the coarse digits are absolute keys >> F
+  const NwOrderPlan op =
+      nw_order_split(m, slice_keys.b[me + 1] - slice_keys.b[me], bit_length(vsize - 1));
+  // the X axis' chunk width (step 6) from the slice's own rows: the fine
+  // kernel then counts the slice's X-chunk entries as it writes the order, and
+  // step 6 adds the halo's (when its width comes out the same)
+  const uint64_t span = (slice_keys.b[me + 1] - slice_keys.b[me]) / 10 + 2;
+  NwChunkCounts own_cc{};
+  own_cc.W = nw_chunk_width(m, (uint32_t)(span < nbx ? span : nbx));
+  while ((1u << own_cc.lgW) < own_cc.W) ++own_cc.lgW;
+  own_cc.nch = nw_chunks(nbx, own_cc.W);
+  bool own_counts = false;
+  if (m && op.nseg) {
+    uint32_t *chist = S.take<uint32_t>(SN_CHIST, nw_seg_words(m));
+    uint32_t *coff = S.take<uint32_t>(SN_COFF, nw_seg_words(m));
+    own_cc.cnts = S.take<uint32_t>(SN_XCNT0, (size_t)3 * own_cc.nch + 2);
+    nw_rec_hist(rin, 16, m, 0, op.coarse, ahist, st);
+    // rin is read by the first coarse pass only: the fine kernel's scratch
+    nw_order_sort_recs_split(rin, m, nby, poff, op, ahist, astat, Ra, Rb, yown,
+                             const_cast<uint4 *>(rin), chist, coff,
+                             S.scan_scratch(SL_PSCAN, (size_t)op.nseg + 1), &own_cc, st);
+    own_counts = true;
+    S.launched("order sort");
+  } else if (m) {
     nw_rec_hist(rin, 16, m, 0, ad, ahist, st);
     nw_order_sort_recs(rin, m, nby, poff, ad, ahist, astat, Ra, Rb, yown, st);
     S.launched("order sort");
@@ -609,7 +634,6 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   // ---- 6: X axis over [halo ; own] (the X-chunk kernel, no sort)
   uint32_t *xg = S.take<uint32_t>(SL_XG, m + 1);
   uint8_t *xused = S.take<uint8_t>(SN_XGUSED, G + 1);
-  const uint64_t span = (slice_keys.b[me + 1] - slice_keys.b[me]) / 10 + 2;
   uint32_t Gfin = 0;            // the halo of the last X solve
   const uint4 *hfin = nullptr;  // (its records: member records sit behind it)
   auto solve_x = [&](const uint4 *halo, uint32_t Gc) {
@@ -623,7 +647,13 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     cc.nch = nw_chunks(nbx, cc.W);
     cc.cnts = S.take<uint32_t>(SN_XCNT, (size_t)3 * cc.nch + 2);
     uint32_t *xoff = S.take<uint32_t>(SN_XOFF, (size_t)3 * cc.nch + 2);
-    nw_x_count(Ra, mx, cc, st, halo, Gc);
+    if (own_counts && cc.W == own_cc.W) {
+      (void)hipMemcpyAsync(cc.cnts, own_cc.cnts, ((size_t)3 * cc.nch + 1) * 4,
+                           hipMemcpyDeviceToDevice, st);
+      nw_x_count_add(halo, Gc, cc, st);
+    } else {
+      nw_x_count(Ra, mx, cc, st, halo, Gc);
+    }
     exclusive_scan_u32(cc.cnts, xoff, (size_t)3 * cc.nch + 1,
                        S.scan_scratch(SL_PSCAN, (size_t)3 * cc.nch + 1), st);
     Csr cx{};

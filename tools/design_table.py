@@ -1,18 +1,22 @@
 #!/usr/bin/env python3
-"""Regenerate DESIGN.md's kernel table from profiles/r3_bench.json (HIP-event
+"""Regenerate DESIGN.md's kernel table from profiles/r4_bench.json (HIP-event
 timing inside bench.py's timed steps, cfg3), profiles/traffic.json
-(PMC HBM bytes, cfg3) and profiles/r3_bench_cfg5.json (the same timing at cfg5,
+(PMC HBM bytes, cfg3) and profiles/r4_bench_cfg5.json (the same timing at cfg5,
 one GPU) when present."""
 import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
-BENCH, CFG5 = "r3_bench.json", "r3_bench_cfg5.json"
+BENCH, CFG5 = "r4_bench.json", "r4_bench_cfg5.json"
+# bench kernel name -> the PMC summary's name (tools/pmc_summary.py keys by k_\w+)
+PMC_NAME = {"k_seg_fine (order)": "k_seg_fine"}
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
-    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (4 processing-order passes, 8 + 7 + 7 + 7-bit digits at cfg3), 12-B records 7168 per tile (3 Y passes, 9 + 9 + 8 bits, after X: the first carries the X-hit bits, the last writes CSR + states; 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last order pass: 57; last Y pass: 30)"),
-    ("k_nw_xcount", "entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
+    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (2 coarse processing-order passes: the key's top 15 bits as 8 + 7 at cfg3, the second also counting each coarse key), 12-B records 7168 per tile (3 Y passes, 9 + 9 + 8 bits, after X: the first carries the X-hit bits, the last writes CSR + states; 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last Y pass: 30)"),
+    ("k_seg_fine (order)", "one block per coarse-key segment (<= 4096 records in LDS): the 14 fine bits by ballot-ranked LSD rounds, then the final records, the Y records and the X-chunk counts (an LDS window of chunk counters)", "44"),
+    ("k_seg_big", "segments above 4096 records: the same passes through global memory, one block each", "-"),
+    ("k_nw_xcount", "(RK_NW_SPLIT=0 only) entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
     ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "50"),
     ("k_sweep_fast", "occupancy decisions, first sweep: a wavefront per 64-position window, ballot rounds, 32-bit candidate tests", "26"),
     ("k_sweep_fast_more", "later sweeps: one wavefront per 64 windows handles the still-pending ones", "-"),
@@ -42,7 +46,7 @@ def main():
             "PMC HBM MB / launch | cfg5 ms / step |",
             "|---|---|---|---|---|---|---|"]
     for name, job, algo in JOBS:
-        kk, tr = k.get(name, {}), t.get(name, {})
+        kk, tr = k.get(name, {}), t.get(PMC_NAME.get(name, name), {})
         ln = kk.get("launches_per_step", 0)
         hb = tr.get("hbm_bytes_per_launch")
         c5 = k5.get(name, {}).get("ms_per_step")
@@ -50,13 +54,17 @@ def main():
                     f"{kk.get('ms_per_step', 0):.2f} | {kk.get('algo_GBps') or '-'} | "
                     f"{round(hb / 1e6) if hb else '-'} | {f'{c5:.1f}' if c5 else '-'} |")
     r = d["roofline"]
+    step_bytes = sum(v.get("launches_per_step", 0) *
+                     t.get(PMC_NAME.get(n, n), {}).get("hbm_bytes_per_launch", 0)
+                     for n, v in k.items())
     rows.append("")
     rows.append(f"Step: {d['ms_per_step']:.2f} ms ({d['value'] / 1e9:.2f} G fragments/s); "
                 f"roofline kernel `{r['kernel']}`: {r['launches_per_step']:g} launches, "
                 f"{r['launch_ms']:.3f} ms each on average, {r['achieved']:.0f} GB/s, frac "
                 f"{r['frac']:.3f}; PMC traffic "
                 f"{t.get(r['kernel'], {}).get('hbm_bytes_per_launch', 0) / 1e6:.0f} MB per launch "
-                f"against {r['algorithmic_bytes_per_launch'] / 1e6:.0f} MB algorithmic.")
+                f"against {r['algorithmic_bytes_per_launch'] / 1e6:.0f} MB algorithmic; "
+                f"PMC traffic of the listed kernels {step_bytes / 1e9:.1f} GB per step.")
     path = os.path.join(ROOT, "DESIGN.md")
     s = open(path).read()
     a, b = s.index(BEGIN) + len(BEGIN), s.index(END)

@@ -21,6 +21,8 @@
 #             host callbacks, the RCCL attempt (RCCL refuses two ranks on one
 #             GPU: value null with the error), the world-1 sharded leg
 #   serial    per-kernel times with every kernel on one stream (RK_ONE_STREAM=1)
+#   pmc5      the PMC passes at cfg5 (one timed step) -> OUTDIR/pmc5
+#   shprof    rocprofv3 --kernel-trace --stats of the world-1 sharded bench
 export TMPDIR=/tmp
 TASK=$1
 O=${2:-gpurun_out/$TASK}
@@ -90,6 +92,12 @@ rehearse)
 serial)
   RK_ONE_STREAM=1 bench cfg3 --no-cpu || exit 1
   RK_ONE_STREAM=1 bench cfg5 --config cfg5 --no-cpu --steps 2 --warmup 1 || exit 2
+  ;;
+pmc5)
+  bash tools/pmc_run.sh $O/pmc5 --config cfg5 --no-cpu --steps 1 --warmup 1 || exit 1
+  ;;
+shprof)
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shprof -o p -- python3 bench.py --mode sharded --no-cpu --steps 10 --warmup 3 > $O/shprof.json 2> $O/shprof.err || exit 1
   ;;
 *)
   echo "unknown task $TASK" >&2

@@ -6,7 +6,8 @@ corrects gfx950's FETCH_SIZE under-count of wide coalesced reads
 (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads exactly half the bytes of a
 16-B/lane streaming read).  Both raw and corrected values are printed; the
 correction is calibrated per access pattern, so the raw numbers are kept too.
-Writes profiles/traffic.json when --write is given.
+Writes profiles/traffic.json (cfg3) or profiles/traffic_<config>.json when
+--write is given (--config names the bench config the passes ran).
 """
 import collections
 import csv
@@ -63,7 +64,8 @@ def main():
                           "(MI355X_MICROARCH.md: gfx950 FETCH_SIZE counts half of a 16-B/lane "
                           "streaming read)",
                 "command": " ".join(args[1:]) or "python3 bench.py --no-cpu --steps 3 --warmup 1"}
-        with open("profiles/traffic.json", "w") as f:
+        name = "traffic.json" if config == "cfg3" else f"traffic_{config}.json"
+        with open(os.path.join("profiles", name), "w") as f:
             json.dump({"meta": meta, "config": config, "kernels": out}, f, indent=1,
                       sort_keys=True)
 
