@@ -57,9 +57,9 @@ void collect_kernel_timing(rk_ctx *ctx) {
         double mem = 0;
         for (uint32_t b = 0; b < nb; ++b) mem += h[(size_t)u * nb + b];
         const int sl = ctx->kt.tier_slot[u];
-        if (sl >= 0 && sl < ctx->kt.n) ctx->kt.bytes[sl] = 16.0 * mem;
+        if (sl >= 0 && sl < ctx->kt.n) ctx->kt.bytes[sl] = 12.0 * mem;
         const int s2 = u == GS_NTIER - 1 ? ctx->kt.tier_slot[GS_NTIER] : -1;  // phase B
-        if (s2 >= 0 && s2 < ctx->kt.n) ctx->kt.bytes[s2] = 16.0 * mem;
+        if (s2 >= 0 && s2 < ctx->kt.n) ctx->kt.bytes[s2] = 12.0 * mem;
       }
     }
     ctx->kt.tier_counts = nullptr;

@@ -577,7 +577,9 @@ __device__ void reg_batch(const V &v, bool in, int bl, uint32_t bm, int len, int
                           uint32_t lane, uint32_t *out) {
   const uint32_t mpos = bm + (uint32_t)((int)lane - bl);
   const uint64_t k = in ? (uint64_t)v.K[mpos] : ~0ull;
-  const uint32_t t = in ? v.T[mpos] : 0u;
+  // the group arrays' tags are positions (tag[x] == x, sort_groups_exact):
+  // not read from memory; LDS views hold the moved tags
+  const uint32_t t = in ? (GLOBAL ? mpos : v.T[mpos]) : 0u;
   if (sizeof(typename V::key_t) == 8 && __ballot(in && (k >> 32) != 0))
     reg_finish<GLOBAL, uint64_t, V>(v, in, bl, bm, len, d, lane, k, t, out);
   else
@@ -910,7 +912,7 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     for (uint32_t x = lane; x < n; x += W) {
       K[x] = (KT)key[b + x];
-      T[x] = tag[b + x];
+      T[x] = b + x;  // tags are positions
     }
     wave_sync();
     wave_std_sort<false, ViewT<KT, uint16_t>, W>(v, n, otag + b, stack, smallq, heapq, L,
@@ -1075,6 +1077,9 @@ __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tie
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     uint64_t *K = key + b;
     uint32_t *T = tag + b;
+    // the tags (positions) written here: phase A moves them in memory, phase
+    // B and the heap kernel read them back
+    for (uint32_t x = tid; x < n; x += 256) T[x] = b + x;
     int sp = 1;
     if (tid == 0) stack[0] = {0u, n, 2 * (31 - __clz((int)n))};
     __syncthreads();
@@ -1224,7 +1229,7 @@ __global__ void __launch_bounds__(256) k_sort_small(TierLists tl, const uint32_t
       const uint64_t kj = __shfl(k, j, 16);
       r += (uint32_t)j < n && (kj < k || (kj == k && (uint32_t)j < l));
     }
-    if (in) otag[b + r] = tag[b + l];
+    if (in) otag[b + r] = b + l;  // tags are positions
   }
 }
 
@@ -1366,8 +1371,8 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   exclusive_scan_u32(bc, boff, (size_t)NL * nblk + 1, ss, st);
   k_tier_lists<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, boff, list);
   const TierLists tl{list, boff, nblk};
-  // algorithmic bytes of every tier (timing only): each member's (key, tag)
-  // read, its tag written once at its final slot -- 16 B x the tier's members,
+  // algorithmic bytes of every tier (timing only): each member's key read, its
+  // tag (its position) written once at its final slot -- 12 B x the tier's members,
   // filled in from bm when the timings are collected
   if (timing && g_ktimer->only < 0) g_ktimer->tier_counts = bm;  // read back at collection
   auto tier_slot = [&](int u) {

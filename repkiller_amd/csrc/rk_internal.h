@@ -240,6 +240,9 @@ void build_records(uint32_t *gmem, const ulonglong2 *hrec, uint32_t m, uint64_t 
 size_t groupsort_scratch_bytes(uint32_t n);
 // libstdc++ std::sort of every group's (key, tag) records; sorted tags -> otag
 // (groups of one member are left unwritten: their slot holds its own tag).
+// Every record's tag is its position (tag[x] == x): the tiers compute it, and
+// `tag` is only the scratch array in which the groups above 2048 members move
+// their tags (written there first), so callers need not fill it.
 // gid_sorted: group id of every record; host_words: >= 16 pinned words;
 // narrow_keys: every key fits 32 bits (LDS tiers stage 4-byte keys).
 // side (optional): a second stream for the tiers of <= 64 members, forked

@@ -251,7 +251,10 @@ struct SrcFile {
   }
   __device__ __forceinline__ uint4 pack(uint64_t xs, uint64_t ys, uint64_t L, uint32_t s,
                                         uint32_t i) const {
-    const uint64_t pk = div_small(xs, 10);
+    // xs / 10 without a branch (div_small's 32-bit test waited for each row's
+    // load before the next one issued): ceil(2^67 / 10) * xs >> 67 is exact
+    // for every 64-bit xs
+    const uint64_t pk = __umul64hi(xs, 0xCCCCCCCCCCCCCCCDull) >> 3;
     const uint32_t key = (uint32_t)(pk < vsize - 1 ? pk : vsize - 1);
     // (rows that do not pack were flagged by k_nw_order_hist: the generic
     // pipeline takes over then)
@@ -364,10 +367,14 @@ struct DstCsr {
   __device__ __forceinline__ void store(uint32_t pos, const uint3 &r, uint32_t xw) const {
     key[pos] = r.x;
     ent[pos] = r.y;
-    const uint32_t b = r.x >= nb ? r.x - nb : r.x;
-    const uint64_t c = (uint64_t)b * 100 + ((r.z >> 24) & 0x7Fu);  // bucket * 100 + remainder
+    const uint32_t b = r.x >= nb ? r.x - nb : r.x, rem = (r.z >> 24) & 0x7Fu;
+    const uint64_t c = (uint64_t)b * 100 + rem;  // bucket * 100 + remainder
     pk[pos] = make_uint2((uint32_t)c, r.z & 0xFFFFFFu);
-    nbd[pos] = nbd_code_nw(c, max_index);
+    // nbd_code_nw(c, max_index) with c % 100 == rem and c >= 100 <=> b >= 1
+    // (no 64-bit remainder per record)
+    nbd[pos] = rem <= 1 && b >= 1 ? 1
+               : (rem == 99 && c < max_index) || (rem == 98 && c < max_index - 1) ? 2
+                                                                                   : 0;
     // with the X results: the Y states -- X hits sit in the Y lists
     // (commonFunctions.cpp:59), X misses query them
     if (hit_bit) state[pos] = (r.z >> 31) ? ST_ACTIVE : ST_UNKNOWN;
@@ -639,7 +646,6 @@ struct MemberEmit {
     sgid[pos] = r.x;
     mrow[pos] = r.y;
     key[pos] = r.z;
-    tag[pos] = pos;
     if (first) goff[r.x] = pos;
     if (pos + 1 == m) goff[G] = m;
   }
@@ -819,17 +825,16 @@ struct DstMembers {
   RK_NO_WAVE
   uint32_t *sgid, *tag, *mrow;
   uint64_t *key;
+  // (no tags: sort_groups_exact takes tag[x] == x without reading them)
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const {
     sgid[pos] = r.x;
     mrow[pos] = r.y;
     key[pos] = (uint64_t)r.w << 32 | r.z;
-    tag[pos] = pos;
   }
   __device__ __forceinline__ void store(uint32_t pos, const uint3 &r) const {
     sgid[pos] = r.x;
     mrow[pos] = r.y;
     key[pos] = r.z;
-    tag[pos] = pos;
   }
 };
 

@@ -70,11 +70,23 @@ struct has_fixup<S, std::void_t<decltype(S::kFixup)>> : std::true_type {};
 template <int ITEMS, class Src, class R>
 __device__ __forceinline__ void load_items(const Src &src, R (&rec)[ITEMS], uint32_t base,
                                            uint32_t wbase, uint32_t cnt) {
+  if constexpr (has_per_row<Src>::value) {
+    if (cnt == (uint32_t)(ITEMS * blockDim.x)) {  // a full tile: one base, constant offsets
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const uint32_t i = wbase + r * 64;
-    if constexpr (has_per_row<Src>::value) rec[r] = i < cnt ? src.load(base + i) : R{};
-    else rec[r] = src.load(base + (i < cnt ? i : cnt - 1));
+      for (int r = 0; r < ITEMS; ++r) rec[r] = src.load(base + wbase + r * 64);
+    } else {
+#pragma unroll
+      for (int r = 0; r < ITEMS; ++r) {
+        const uint32_t i = wbase + r * 64;
+        rec[r] = i < cnt ? src.load(base + i) : R{};
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t i = wbase + r * 64;
+      rec[r] = src.load(base + (i < cnt ? i : cnt - 1));
+    }
   }
   if constexpr (has_fixup<Src>::value) src.template fixup<ITEMS>(rec, base, wbase);
 }

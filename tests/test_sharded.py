@@ -158,6 +158,15 @@ def test_sharded_generic_forced(gpu_ctx):
     _check_vs_single_device(gpu_ctx, got, cases, 3, generic=True)
 
 
+def test_sharded_order_sort_unsplit(gpu_ctx):
+    """RK_NW_SPLIT=0: the slices' processing order by four LSD passes and the
+    X-chunk counts by their own kernel (the default splits the sort and counts
+    in the segment kernel) -- the same result."""
+    cases = [SYNTH[0], SYNTH[2], SYNTH[3]]
+    got = run_ranks(2, cases, env={"RK_NW_SPLIT": "0"})
+    _check_vs_single_device(gpu_ctx, got, cases, 2, generic=False)
+
+
 def test_sharded_record_driver_used(gpu_ctx):
     """Every SYNTH set packs: the record driver classified them (not the fallback)."""
     cases = SYNTH[:2]
