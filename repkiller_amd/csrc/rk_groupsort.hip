@@ -1423,6 +1423,8 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   }();
   auto launch_lds = [&](int j, hipStream_t sj) {
     const uint32_t cap = caps.c[j];
+    // (more blocks than stay resident: a grid capped at the resident blocks, or
+    // half of them, was slower -- group-sort phase 1.275 / 1.37 against 1.20 ms)
     const uint32_t waves = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
     const int wp = cap <= 512 ? wpb : 1;
     const size_t slab = (lds_bytes(cap, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
@@ -1454,14 +1456,25 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   };
   const int big0 = side ? NLDS - lds_big : NLDS;  // tiers [big0, NLDS) go first on side
   for (int j = NLDS - 1; j >= big0; --j) launch_lds(j, s2);
-  kt_begin(s2, KID_SORT_SMALL);
-  k_sort_small<<<2048, 256, 0, s2>>>(tl, goff, key, tag, otag);
-  kt_end(s2, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
-  tier_slot(0);
-  kt_begin(s2, KID_SORT_REG);
-  k_sort_groups_reg<2><<<4096, 256, 0, s2>>>(tl, 1, goff, key, tag, otag);
-  kt_end(s2, KID_SORT_REG, 0.0);
-  tier_slot(1);
+  // groups of 2..16 and 17..32 members: on `st` after the 33..64 tier
+  // (RK_GS_SMALL1=1, the default) or on `side` after its LDS tiers (0).  The
+  // side stream's two large LDS tiers are the longer chain (~0.96 against
+  // ~0.88 ms of kernel time on `st`): group-sort phase 1.20 -> 1.13 ms
+  static const int small_main = [] {
+    const char *e = getenv("RK_GS_SMALL1");
+    return e ? atoi(e) : 1;
+  }();
+  auto launch_small = [&](hipStream_t sj) {
+    kt_begin(sj, KID_SORT_SMALL);
+    k_sort_small<<<2048, 256, 0, sj>>>(tl, goff, key, tag, otag);
+    kt_end(sj, KID_SORT_SMALL, 0.0);  // bytes filled in from the tier sizes at collection
+    tier_slot(0);
+    kt_begin(sj, KID_SORT_REG);
+    k_sort_groups_reg<2><<<4096, 256, 0, sj>>>(tl, 1, goff, key, tag, otag);
+    kt_end(sj, KID_SORT_REG, 0.0);
+    tier_slot(1);
+  };
+  if (!small_main || !side) launch_small(s2);
   // the 33..64-member tier on `st` after its LDS tiers (RK_GS_REG1=1, the
   // default) or on `side` (0): the two streams' kernel time is then ~1.06 /
   // ~1.0 ms instead of 0.94 / 1.12 (cfg3 kernel trace); group-sort phase
@@ -1485,6 +1498,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     }
   }
   if (reg1_main && side) launch_reg1(st);
+  if (small_main && side) launch_small(st);
 #ifdef RK_GS_PROF
   {
     unsigned long long h[8];
