@@ -478,8 +478,10 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   const rk::NwDigits yd = rk::nw_plan(rk::bit_length(2ull * pl.nby - 1), bits12);
 
   HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
-  HIPCHK(ctx, hipMemsetAsync(w.ctrl, 0, (64 + rk::PEND_WORDS) * sizeof(uint32_t), st));
-  HIPCHK(ctx, hipMemsetAsync(w.ahist, 0, 3 * 4096 * sizeof(uint32_t), st));
+  // the control words and the order / Y / member digit histograms (ehist stays
+  // zero until the first pair's k_nw_assign), one launch
+  rk::zero_regions(st, {{w.ctrl, (64 + rk::PEND_WORDS) * sizeof(uint32_t)},
+                        {w.ahist, 3 * 4096 * sizeof(uint32_t)}});
   mark(ctx, RK_PH_PREP);
   rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, split ? op.coarse : ad, yd,
                     w.ahist, w.yhist, w.ctrl, st, wire);
@@ -582,10 +584,14 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::Proc pr{};
     pr.par = w.par;
     bool narrow_keys = true;
-    HIPCHK(ctx, hipMemsetAsync(w.isnew + m, 0, sizeof(uint32_t), st));
+    // (the first round's changed-count with the scan's end word, one launch;
+    // later pairs' member histograms too -- the first pair's are still zero)
+    rk::zero_regions(st, {{w.isnew + m, sizeof(uint32_t)},
+                          {w.ctrl + 5, sizeof(uint32_t)},
+                          {q > 0 ? w.ehist : nullptr, 4096 * sizeof(uint32_t)}});
     uint32_t rounds = 0, G = 0;
     for (;;) {
-      HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
+      if (rounds > 0) HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
       rk::jump_round(pr, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st);
       if (rounds == 0) {
         // the new-group flags are final after the first round: their scan
@@ -621,7 +627,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
                                    ? rk::nw_order_split(m, G, rk::bit_length(G ? G - 1 : 0))
                                    : rk::NwOrderPlan{};
     const bool msplit = mp.coarse.passes > 0;
-    HIPCHK(ctx, hipMemsetAsync(w.ehist, 0, 4096 * sizeof(uint32_t), st));
+    // (ehist: zero -- cleared at the start, or with the roots' words for q > 0)
     // gids into isnew's words (dead after the scan)
     rk::nw_assign(w.par, w.newrank, w.isnew, m, msplit ? mp.coarse : ed, w.ehist, st);
 

@@ -926,9 +926,10 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
 //
 // Phase A, one 256-thread block per group: the introsort loop on the group's
 // slice of global memory, but only segments of more than SPLIT_T members are
-// partitioned here, each by the whole block -- stopper lists from two
-// ballot passes (counts, then ranked writes; each wave owns a quarter of the
-// segment), K by a 256-ary search (the stop predicate Lpos[k] >= Rpos[k] is
+// partitioned here, each by the whole block -- stopper lists from one
+// ballot pass (each wave compacts its quarter's stoppers into that quarter's
+// slice; the k-th stopper is found through the four counts), K by a 256-ary
+// search (the stop predicate Lpos[k] >= Rpos[k] is
 // monotone in k), the K swaps in parallel.  A segment that reaches SPLIT_T
 // members or less is final for this phase: its start gets bnd = 1 and
 // head = length | depth << 16.  (A segment above SPLIT_T whose depth budget
@@ -947,6 +948,20 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
 constexpr uint32_t SPLIT_T = RK_SPLIT_T;
 constexpr int SPLIT_STACK = 72;  // one frame per level: 2 * log2(2^32) + slack
 
+// One pass over the segment: each wave compacts the stoppers of its quarter
+// into that quarter's own slice of PL / PR (a quarter holds at most as many
+// stoppers as positions), and the k-th stopper of the whole segment is found
+// through the four waves' counts -- the same lists as a counting pass followed
+// by ranked writes, without reading the keys twice.
+struct StopperMap {
+  uint32_t off[5];  // stoppers before wave w's slice (off[4] = total)
+  uint32_t at[4];   // wave w's slice start
+  __device__ __forceinline__ uint32_t pos(const uint32_t *P, uint32_t k) const {
+    const uint32_t w = (k >= off[1]) + (k >= off[2]) + (k >= off[3]);
+    return P[at[w] + (k - off[w])];
+  }
+};
+
 __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint32_t *PR,
                                     uint32_t f, uint32_t l, uint32_t *s_w) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -955,34 +970,11 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
   const uint64_t p = K[f];
   const uint32_t len = l - f;
   const uint32_t per = ((len + 3) / 4 + 255) & ~255u;  // a wave's share, 4 x 64 aligned
-  const uint32_t a = f + wv * per;
+  const uint32_t a = f + wv * per < l ? f + wv * per : l;
   const uint32_t e = a + per < l ? a + per : l;
   const uint64_t lt = (1ull << lane) - 1ull;
-  // pass 1: stopper counts of this wave's share
+  // the wave's stoppers, compacted into PL / PR [a, a + count)
   uint32_t cl = 0, cr = 0;
-  for (uint32_t c = a; c < e; c += 256) {
-    uint64_t k[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t x = c + 64 * u + lane;
-      k[u] = x < e ? K[x] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t x = c + 64 * u + lane;
-      cl += __popcll(__ballot(x < e && x > f && !(k[u] < p)));
-      cr += __popcll(__ballot(x < e && !(p < k[u])));
-    }
-  }
-  if (lane == 0) s_w[wv] = cl, s_w[4 + wv] = cr;
-  __syncthreads();
-  uint32_t nL = 0, nR = 0, oL = 0, oR = 0;
-#pragma unroll
-  for (uint32_t u = 0; u < 4; ++u) {
-    if (u < wv) oL += s_w[u], oR += s_w[4 + u];
-    nL += s_w[u], nR += s_w[4 + u];
-  }
-  // pass 2: ranked writes (PL ascending, PR ascending; PR is read from the right)
   for (uint32_t c = a; c < e; c += 256) {
     uint64_t k[4];
 #pragma unroll
@@ -996,13 +988,24 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
       const bool lf = x < e && x > f && !(k[u] < p);
       const bool rf = x < e && !(p < k[u]);
       const uint64_t bl = __ballot(lf), br = __ballot(rf);
-      if (lf) PL[f + oL + __popcll(bl & lt)] = x;
-      if (rf) PR[f + oR + __popcll(br & lt)] = x;
-      oL += __popcll(bl);
-      oR += __popcll(br);
+      if (lf) PL[a + cl + __popcll(bl & lt)] = x;
+      if (rf) PR[a + cr + __popcll(br & lt)] = x;
+      cl += __popcll(bl);
+      cr += __popcll(br);
     }
   }
+  if (lane == 0) s_w[wv] = cl, s_w[4 + wv] = cr;
   __syncthreads();
+  StopperMap ML, MR;
+  ML.off[0] = MR.off[0] = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u) {
+    ML.off[u + 1] = ML.off[u] + s_w[u];
+    MR.off[u + 1] = MR.off[u] + s_w[4 + u];
+    const uint32_t au = f + u * per;
+    ML.at[u] = MR.at[u] = au < l ? au : l;
+  }
+  const uint32_t nL = ML.off[4], nR = MR.off[4];
   // K = first k < lim with PL[k] >= PR[nR-1-k] (lim if none), 256 probes a round
   const uint32_t lim = nL < nR ? nL : nR;
   uint32_t lo = 0, hi = lim;  // K in [lo, hi]
@@ -1010,7 +1013,7 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
     const uint32_t span = hi - lo;
     const uint32_t k = lo + (uint32_t)(((uint64_t)span * tid) / 256);
     const bool probe = tid == 0 || k != lo + (uint32_t)(((uint64_t)span * (tid - 1)) / 256);
-    const bool stop = probe && PL[f + k] >= PR[f + nR - 1 - k];
+    const bool stop = probe && ML.pos(PL, k) >= MR.pos(PR, nR - 1 - k);
     if (tid == 0) s_w[8] = 0xFFFFFFFFu;
     __syncthreads();
     if (stop) atomicMin(&s_w[8], k);
@@ -1034,7 +1037,7 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
   }
   const uint32_t Kc = lo;
   for (uint32_t k = tid; k < Kc; k += 256) {
-    const uint32_t xa = PL[f + k], xb = PR[f + nR - 1 - k];
+    const uint32_t xa = ML.pos(PL, k), xb = MR.pos(PR, nR - 1 - k);
     const uint64_t ka = K[xa];
     K[xa] = K[xb];
     K[xb] = ka;
@@ -1044,10 +1047,13 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
   }
   uint32_t cut;
   if (Kc == 0) {
-    cut = PL[f];
+    cut = ML.pos(PL, 0);
   } else {
-    cut = PR[f + nR - Kc];
-    if (Kc < nL && PL[f + Kc] < cut) cut = PL[f + Kc];
+    cut = MR.pos(PR, nR - Kc);
+    if (Kc < nL) {
+      const uint32_t c2 = ML.pos(PL, Kc);
+      if (c2 < cut) cut = c2;
+    }
   }
   __syncthreads();
   return cut;

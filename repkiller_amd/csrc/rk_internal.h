@@ -4,6 +4,8 @@
 // order, groups, in-group order); each TU exports host-side launchers only, so
 // no relocatable device code is needed.
 #pragma once
+
+#include <initializer_list>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -297,6 +299,13 @@ struct NwOrderPlan {
   uint32_t nseg = 0;
   NwDigits coarse{};
 };
+// several regions cleared by one kernel launch (a memset launch each costs a
+// dispatch gap of ~4-9 us); null or empty regions are skipped
+struct ZeroRegion {
+  void *ptr;
+  size_t bytes;
+};
+void zero_regions(hipStream_t st, std::initializer_list<ZeroRegion> regs);
 NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int bits);  // nkeys: key values in use
 // words of each segment array (counts, starts) a split sort of n rows may use
 inline size_t nw_seg_words(uint32_t n) { return (size_t)n / 512 + 64; }

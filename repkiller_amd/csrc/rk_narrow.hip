@@ -1369,7 +1369,48 @@ void launch_pass(const Src &src, const Dst &dst, uint32_t n, int shift, int db,
   kt_end(st, KID_ONESWEEP, bytes);
 }
 
+// one launch clears up to ZR_MAX regions (blockIdx.y = region): 16-B stores
+// where the region is 16-B aligned, 4-B stores for the rest
+constexpr int ZR_MAX = 8;
+struct ZeroArgs {
+  uint32_t *p[ZR_MAX];
+  uint32_t words[ZR_MAX];
+};
+__global__ void __launch_bounds__(256) k_zero_regions(const ZeroArgs a) {
+  uint32_t *p = a.p[blockIdx.y];
+  const uint32_t n = a.words[blockIdx.y];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  uint32_t head = 0;
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    const uint32_t nv = n / 4;
+    uint4 *v = reinterpret_cast<uint4 *>(p);
+    for (uint32_t i = t; i < nv; i += stride) v[i] = make_uint4(0, 0, 0, 0);
+    head = nv * 4;
+  }
+  for (uint32_t i = head + t; i < n; i += stride) p[i] = 0;
+}
+
 }  // namespace
+
+void zero_regions(hipStream_t st, std::initializer_list<ZeroRegion> regs) {
+  ZeroArgs a{};
+  int k = 0;
+  uint32_t most = 0;
+  for (const ZeroRegion &r : regs) {
+    if (!r.ptr || !r.bytes) continue;
+    if (k == ZR_MAX || (r.bytes & 3) || r.bytes / 4 > 0xFFFFFFFFull) {
+      (void)hipMemsetAsync(r.ptr, 0, r.bytes, st);
+      continue;
+    }
+    a.p[k] = reinterpret_cast<uint32_t *>(r.ptr);
+    a.words[k] = (uint32_t)(r.bytes / 4);
+    most = a.words[k] > most ? a.words[k] : most;
+    ++k;
+  }
+  if (!k) return;
+  const uint32_t bx = (most / 4 + 255) / 256;
+  k_zero_regions<<<dim3(bx < 1 ? 1 : bx > 256 ? 256 : bx, (uint32_t)k), 256, 0, st>>>(a);
+}
 
 // ===========================================================================
 // host side
@@ -1432,12 +1473,17 @@ struct PassStatus {
   uint32_t *next(int p, int passes) const {
     return ahead && p + 1 < passes ? base + (size_t)((p + 1) & 1) * half : nullptr;
   }
-  // before pass p: the memset it still needs (none after a clear-ahead pass)
-  void prepare(int p, uint32_t n, const Digits &D, hipStream_t st) const {
-    if (ahead && p > 0) return;
+  // before pass p: the words it still needs cleared (none after a clear-ahead
+  // pass: {nullptr, 0})
+  ZeroRegion region(int p, uint32_t n, const Digits &D) const {
+    if (ahead && p > 0) return ZeroRegion{nullptr, 0};
     const size_t words =
         ahead ? half : (size_t)tiles_for(n, D.db[p], rec_bytes) * ((size_t)1 << D.db[p]);
-    (void)hipMemsetAsync(use(p), 0, words * 4, st);
+    return ZeroRegion{use(p), words * 4};
+  }
+  void prepare(int p, uint32_t n, const Digits &D, hipStream_t st) const {
+    const ZeroRegion r = region(p, n, D);
+    if (r.bytes) (void)hipMemsetAsync(r.ptr, 0, r.bytes, st);
   }
 };
 static PassStatus pass_status(uint32_t *status, uint32_t n, const Digits &D, int rec_bytes = 16) {
@@ -1564,13 +1610,17 @@ static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n
                                   const NwChunkCounts *cc, hipStream_t st) {
   const Digits D = to_digits(op.coarse);
   const size_t sw = nw_status_words(n);
-  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
-  (void)hipMemsetAsync(chist, 0, ((size_t)op.nseg + 1) * 4, st);
   const PassStatus ps = pass_status(status, n, D);
+  // one launch clears the passes' tile counters, the coarse-key counts, the
+  // first pass' status words and the X-chunk counts
+  zero_regions(st, {{status + sw - 64, 64 * 4},
+                    {chist, ((size_t)op.nseg + 1) * 4},
+                    ps.region(0, n, D),
+                    {cc ? cc->cnts : nullptr, cc ? ((size_t)3 * cc->nch + 1) * 4 : 0}});
   for (int p = 0; p < D.passes; ++p) {
     uint4 *out = ((D.passes - 1 - p) % 2 == 0) ? Rb : Ra;  // the last coarse pass lands in Rb
     const uint4 *src = ((D.passes - p) % 2 == 0) ? Rb : Ra;
-    ps.prepare(p, n, D, st);
+    if (p > 0) ps.prepare(p, n, D, st);
     uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
@@ -1584,8 +1634,7 @@ static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n
   }
   exclusive_scan_u32(chist, coff, (size_t)op.nseg + 1, ss, st);
   OrderEmit oe{DstProc{Ra, reinterpret_cast<uint3 *>(yrec), nby, base}, m, nullptr, 0, 0, 0};
-  if (cc) {
-    (void)hipMemsetAsync(cc->cnts, 0, ((size_t)3 * cc->nch + 1) * 4, st);
+  if (cc) {  // (the counts were cleared with the status words)
     oe.cnts = cc->cnts;
     oe.lgW = cc->lgW;
     oe.nch = cc->nch;
@@ -1698,13 +1747,14 @@ void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits
                        uint64_t max_y, const uint32_t *xbits, hipStream_t st, const uint4 *src0) {
   const Digits D = to_digits(y);
   const size_t sw = nw_status_words(m);
-  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
   const PassStatus ps = pass_status(status, m, D, 12);
+  // the passes' tile counters and the first pass' status words, one launch
+  zero_regions(st, {{status + sw - 64, 64 * 4}, ps.region(0, m, D)});
   const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, nullptr, cy.state, true};
   const uint3 *src = reinterpret_cast<const uint3 *>(src0 ? src0 : yrec);
   const uint64_t *bits64 = reinterpret_cast<const uint64_t *>(xbits);
   for (int p = 0; p < D.passes; ++p) {
-    ps.prepare(p, m, D, st);
+    if (p > 0) ps.prepare(p, m, D, st);
     const bool last = p == D.passes - 1;
     uint3 *out = reinterpret_cast<uint3 *>(p % 2 == 0 ? tmp : const_cast<uint4 *>(yrec));
     uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes), *ctr = status + sw - 64 + p;
@@ -1734,12 +1784,13 @@ static void nw_member_passes(const Src1 &s1, Rec *t0, Rec *t1, uint32_t m, const
                              hipStream_t st) {
   const Digits D = to_digits(dg);
   const size_t sw = nw_status_words(m);
-  (void)hipMemsetAsync(status + sw - 64, 0, 64 * 4, st);  // the passes' tile counters
   const PassStatus ps = pass_status(status, m, D, (int)sizeof(Rec));
+  // the passes' tile counters and the first pass' status words, one launch
+  zero_regions(st, {{status + sw - 64, 64 * 4}, ps.region(0, m, D)});
   const double rb = sizeof(Rec), in1 = sizeof(Rec) == 12 ? 12.0 : 16.0;
   const Rec *src = nullptr;
   for (int p = 0; p < D.passes; ++p) {
-    ps.prepare(p, m, D, st);
+    if (p > 0) ps.prepare(p, m, D, st);
     uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes);
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
