@@ -486,7 +486,34 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, split ? op.coarse : ad, yd,
                     w.ahist, w.yhist, w.ctrl, st, wire);
   HIPCHK(ctx, hipGetLastError());
-  if ((rc = readback(ctx, w.ctrl, 9))) return rc;
+  // The control words (errors, kept rows, pack flag, longest length) come back
+  // while the split sort's coarse passes run -- they need only n -- when the
+  // workspace is already large enough (a repeated call; the first call
+  // allocates it after the pack check, so an input that falls back to the
+  // generic pipeline never holds both).  A fallback or an error then leaves
+  // the coarse passes' output unused.
+  bool early = false;
+  if (split) {
+    Carve probe{nullptr};
+    NWork tmpw = w;
+    early = carve_nw(probe, pl.n, pl.nbx, tmpw) <= ctx->ws_nw_cap;
+  }
+  if (early) {
+    if ((rc = ensure_nw(ctx, pl.n, pl.nbx, w))) return rc;  // (no allocation)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->host, w.ctrl, 9 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               st));
+    HIPCHK(ctx, hipEventRecord(ctx->aux, st));
+    mark(ctx, RK_PH_ORDER);
+    // the X-chunk counts cleared for the widest chunking (64 buckets a chunk)
+    rk::nw_order_sort_split_coarse(
+        *in, op, w.ahist, w.astatus, w.Ra, w.Rb, w.chist,
+        rk::ZeroRegion{w.xcnt, ((size_t)3 * (pl.nbx / 64 + 2) + 1) * sizeof(uint32_t)},
+        pl.vsize, st, wire);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventSynchronize(ctx->aux));
+  } else if ((rc = readback(ctx, w.ctrl, 9))) {
+    return rc;
+  }
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
   if (ctx->host[3]) {  // some row does not pack into a record
     *fallback = true;
@@ -494,7 +521,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     return RK_OK;
   }
   // every row packs: now the workspace (~190 B per row)
-  if ((rc = ensure_nw(ctx, pl.n, pl.nbx, w))) return rc;
+  if (!early && (rc = ensure_nw(ctx, pl.n, pl.nbx, w))) return rc;
   rk::ScanScratch ss{w.scan, w.scan_cap};
   const uint32_t m = ctx->host[1], maxlen = ctx->host[4];
   ctx->stats.n_proc = m;
@@ -513,9 +540,12 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   while ((1u << cc.lgW) < cc.W) ++cc.lgW;
   cc.nch = rk::nw_chunks(pl.nbx, cc.W);
   cc.cnts = w.xcnt;
-  mark(ctx, RK_PH_ORDER);
-  if (split) {
+  if (!early) mark(ctx, RK_PH_ORDER);
+  if (early) {
     // (the member records' buffer is free until the X chunk kernel)
+    rk::nw_order_sort_split_fine((uint32_t)pl.n, m, pl.nby, op, w.Ra, w.Rb, w.yrec, w.erec,
+                                 w.chist, w.coff, ss, &cc, st);
+  } else if (split) {
     rk::nw_order_sort_split(*in, m, pl.nby, op, w.ahist, w.astatus, w.Ra, w.Rb, w.yrec, w.erec,
                             w.chist, w.coff, ss, &cc, pl.vsize, st, wire);
   } else {

@@ -307,6 +307,18 @@ struct ZeroRegion {
 };
 void zero_regions(hipStream_t st, std::initializer_list<ZeroRegion> regs);
 NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int bits);  // nkeys: key values in use
+// the same in two halves: the clears (+ `extra`) and the coarse passes, then
+// the scan and the segment kernel (cc->cnts cleared by the first half's
+// `extra`) -- the host can read the order histogram's control words back in
+// between, while the coarse passes run
+void nw_order_sort_split_coarse(const rk_frags_soa &in, const NwOrderPlan &op,
+                                const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
+                                uint32_t *chist, ZeroRegion extra, uint64_t vsize,
+                                hipStream_t st, const uint3 *wire = nullptr);
+void nw_order_sort_split_fine(uint32_t n, uint32_t m, uint32_t nby, const NwOrderPlan &op,
+                              uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
+                              uint32_t *coff, ScanScratch ss, const NwChunkCounts *cc,
+                              hipStream_t st);
 // words of each segment array (counts, starts) a split sort of n rows may use
 inline size_t nw_seg_words(uint32_t n) { return (size_t)n / 512 + 64; }
 // the same over records received by the sharded driver (processing index base

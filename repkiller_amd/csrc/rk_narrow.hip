@@ -1601,22 +1601,20 @@ NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int b) {
 // chist, 2^C + 1 words, zeroed here), the scan into segment starts, the fine
 // kernel into Ra (+ Y records, + the X-chunk counts into cc.cnts when given,
 // zeroed here)
+// the first half: the clears (tile counters, coarse-key counts, the first
+// pass' status words, `extra`) and the coarse passes, the last one counting
+// the coarse keys into chist
 template <class Src1>
-static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n, uint32_t m,
-                                  uint32_t nby, uint32_t base, const NwOrderPlan &op,
-                                  const uint32_t *ghist,
-                                  uint32_t *status, uint4 *Ra, uint4 *Rb, uint4 *yrec,
-                                  uint4 *tmp, uint32_t *chist, uint32_t *coff, ScanScratch ss,
-                                  const NwChunkCounts *cc, hipStream_t st) {
+static void nw_order_coarse(const Src1 &first, double in_bytes, uint32_t n, const NwOrderPlan &op,
+                            const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
+                            uint32_t *chist, ZeroRegion extra, hipStream_t st) {
   const Digits D = to_digits(op.coarse);
   const size_t sw = nw_status_words(n);
   const PassStatus ps = pass_status(status, n, D);
-  // one launch clears the passes' tile counters, the coarse-key counts, the
-  // first pass' status words and the X-chunk counts
   zero_regions(st, {{status + sw - 64, 64 * 4},
                     {chist, ((size_t)op.nseg + 1) * 4},
                     ps.region(0, n, D),
-                    {cc ? cc->cnts : nullptr, cc ? ((size_t)3 * cc->nch + 1) * 4 : 0}});
+                    extra});
   for (int p = 0; p < D.passes; ++p) {
     uint4 *out = ((D.passes - 1 - p) % 2 == 0) ? Rb : Ra;  // the last coarse pass lands in Rb
     const uint4 *src = ((D.passes - p) % 2 == 0) ? Rb : Ra;
@@ -1632,9 +1630,17 @@ static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n
     else if (last) launch_pass(SrcRec{src}, dh, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
     else launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
   }
+}
+// the second half: the counts' scan into segment starts, the segment kernel
+// into Ra (+ Y records, + the X-chunk counts into cc->cnts when given, which
+// the first half cleared)
+static void nw_order_fine(uint32_t n, uint32_t m, uint32_t nby, uint32_t base,
+                          const NwOrderPlan &op, uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp,
+                          uint32_t *chist, uint32_t *coff, ScanScratch ss,
+                          const NwChunkCounts *cc, hipStream_t st) {
   exclusive_scan_u32(chist, coff, (size_t)op.nseg + 1, ss, st);
   OrderEmit oe{DstProc{Ra, reinterpret_cast<uint3 *>(yrec), nby, base}, m, nullptr, 0, 0, 0};
-  if (cc) {  // (the counts were cleared with the status words)
+  if (cc) {
     oe.cnts = cc->cnts;
     oe.lgW = cc->lgW;
     oe.nch = cc->nch;
@@ -1646,26 +1652,42 @@ static void nw_order_passes_split(const Src1 &first, double in_bytes, uint32_t n
   // records in and out, Y records out (the X counts: no extra reads)
   kt_end(st, KID_NW_FINE, 44.0 * n);
 }
+static ZeroRegion counts_region(const NwChunkCounts *cc) {
+  return ZeroRegion{cc ? cc->cnts : nullptr, cc ? ((size_t)3 * cc->nch + 1) * 4 : 0};
+}
+void nw_order_sort_split_coarse(const rk_frags_soa &in, const NwOrderPlan &op,
+                                const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
+                                uint32_t *chist, ZeroRegion extra, uint64_t vsize,
+                                hipStream_t st, const uint3 *wire) {
+  if (wire)
+    nw_order_coarse(SrcFile<RowWire>{RowWire{wire}, vsize}, 12.0, (uint32_t)in.n, op, ghist,
+                    status, Ra, Rb, chist, extra, st);
+  else
+    nw_order_coarse(SrcFile<RowSoA>{RowSoA{in.x_start, in.y_start, in.length, in.strand}, vsize},
+                    25.0, (uint32_t)in.n, op, ghist, status, Ra, Rb, chist, extra, st);
+}
+void nw_order_sort_split_fine(uint32_t n, uint32_t m, uint32_t nby, const NwOrderPlan &op,
+                              uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
+                              uint32_t *coff, ScanScratch ss, const NwChunkCounts *cc,
+                              hipStream_t st) {
+  nw_order_fine(n, m, nby, 0u, op, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
+}
 void nw_order_sort_split(const rk_frags_soa &in, uint32_t m, uint32_t nby, const NwOrderPlan &op,
                          const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
                          uint4 *yrec, uint4 *tmp, uint32_t *chist, uint32_t *coff,
                          ScanScratch ss, const NwChunkCounts *cc, uint64_t vsize, hipStream_t st,
                          const uint3 *wire) {
-  if (wire)
-    nw_order_passes_split(SrcFile<RowWire>{RowWire{wire}, vsize}, 12.0, (uint32_t)in.n, m, nby,
-                          0u, op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
-  else
-    nw_order_passes_split(
-        SrcFile<RowSoA>{RowSoA{in.x_start, in.y_start, in.length, in.strand}, vsize}, 25.0,
-        (uint32_t)in.n, m, nby, 0u, op, ghist, status, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
+  nw_order_sort_split_coarse(in, op, ghist, status, Ra, Rb, chist, counts_region(cc), vsize, st,
+                             wire);
+  nw_order_fine((uint32_t)in.n, m, nby, 0u, op, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
 }
 void nw_order_sort_recs_split(const uint4 *in, uint32_t m, uint32_t nby, uint32_t base,
                               const NwOrderPlan &op, const uint32_t *ghist, uint32_t *status,
                               uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
                               uint32_t *coff, ScanScratch ss, const NwChunkCounts *cc,
                               hipStream_t st) {
-  nw_order_passes_split(SrcRec{in}, 16.0, m, m, nby, base, op, ghist, status, Ra, Rb, yrec, tmp,
-                        chist, coff, ss, cc, st);
+  nw_order_coarse(SrcRec{in}, 16.0, m, op, ghist, status, Ra, Rb, chist, counts_region(cc), st);
+  nw_order_fine(m, m, nby, base, op, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
 }
 
 void nw_rec_hist(const void *recs, int rec_bytes, uint32_t n, uint32_t sub, const NwDigits &d,
