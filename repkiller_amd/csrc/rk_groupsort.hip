@@ -62,13 +62,15 @@ __device__ __forceinline__ void sync_mem() {
 }
 
 // a group's working arrays: keys, tags, the stopper position lists and leaf
-// marks; the LDS tiers keep 32-bit keys (when every key fits) and 16-bit
-// positions, the global tier 64-bit keys and 32-bit positions
-template <class KT_, class PT_>
+// marks; the LDS tiers keep 32-bit keys (when every key fits), 16-bit
+// positions and 16-bit tags (positions inside the group: the output adds the
+// group's base), the global tier 64-bit keys and 32-bit positions and tags
+template <class KT_, class PT_, class TT_ = uint32_t>
 struct ViewT {
   using key_t = KT_;
+  using tag_t = TT_;
   KT_ *K;
-  uint32_t *T;
+  TT_ *T;
   PT_ *PL, *PR;  // stopper position lists (capacity n)
   uint8_t *B;    // 1 = leaf start, 2 = inside a heap-sorted segment
 };
@@ -102,7 +104,7 @@ __device__ void adjust_heap(const V &v, uint32_t base, long hole, long len,
   const long top = hole;
   long child = hole;
   typename V::key_t *K = v.K + base;
-  uint32_t *T = v.T + base;
+  typename V::tag_t *T = v.T + base;
   while (child < (len - 1) / 2) {
     child = 2 * (child + 1);
     if (K[child] < K[child - 1]) child--;
@@ -551,7 +553,8 @@ __device__ void reg_sort_core(const V &v, bool in, uint32_t mpos, int &sf, int &
 // positions are marked B = 3.
 template <bool GLOBAL, class KT, class V>
 __device__ void reg_finish(const V &v, bool in, int bl, uint32_t bm, int len, int d,
-                           uint32_t lane, uint64_t k64, uint32_t t, uint32_t *out) {
+                           uint32_t lane, uint64_t k64, uint32_t t, uint32_t *out,
+                           uint32_t tbase) {
   const int x = (int)lane;
   KT k = in ? (KT)k64 : (KT)~(KT)0;
   int sf = in ? bl : x, sl = in ? bl + len : x + 1;
@@ -567,23 +570,23 @@ __device__ void reg_finish(const V &v, bool in, int bl, uint32_t bm, int len, in
     r += (j < my) && (ky < k || (ky == k && y < x));
   }
   if (in) {
-    out[heaped ? mpos : bm + (uint32_t)(sf - bl) + r] = t;
+    out[heaped ? mpos : bm + (uint32_t)(sf - bl) + r] = tbase + t;
     if (v.B) v.B[mpos] = 3;
   }
 }
 
 template <bool GLOBAL, class V>
 __device__ void reg_batch(const V &v, bool in, int bl, uint32_t bm, int len, int d,
-                          uint32_t lane, uint32_t *out) {
+                          uint32_t lane, uint32_t *out, uint32_t tbase = 0) {
   const uint32_t mpos = bm + (uint32_t)((int)lane - bl);
   const uint64_t k = in ? (uint64_t)v.K[mpos] : ~0ull;
   // the group arrays' tags are positions (tag[x] == x, sort_groups_exact):
   // not read from memory; LDS views hold the moved tags
   const uint32_t t = in ? (GLOBAL ? mpos : v.T[mpos]) : 0u;
   if (sizeof(typename V::key_t) == 8 && __ballot(in && (k >> 32) != 0))
-    reg_finish<GLOBAL, uint64_t, V>(v, in, bl, bm, len, d, lane, k, t, out);
+    reg_finish<GLOBAL, uint64_t, V>(v, in, bl, bm, len, d, lane, k, t, out, tbase);
   else
-    reg_finish<GLOBAL, uint32_t, V>(v, in, bl, bm, len, d, lane, k, t, out);
+    reg_finish<GLOBAL, uint32_t, V>(v, in, bl, bm, len, d, lane, k, t, out, tbase);
 }
 
 // The lanes that sort one group: the whole wavefront (W = 64), or one half of
@@ -705,7 +708,7 @@ __device__ unsigned long long g_gs_prof[8];
 template <bool GLOBAL, class V, int W = 64>
 __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stack,
                               Frame *smallq, Frame *heapq, GLanes<W> L, int d0,
-                              uint32_t reg_max) {
+                              uint32_t reg_max, uint32_t tbase = 0) {
   static_assert(W == 64 || W == 32, "a wavefront or a half");
   const uint32_t lane = L.lane;
   if (W != 64) reg_max = 0;  // register batches assume the whole wavefront
@@ -768,7 +771,8 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
     while (j + 1 < q1 && (int)lane >= bl + (int)(smallq[j].l - smallq[j].f))
       bl += (int)(smallq[j].l - smallq[j].f), ++j;
     const Frame fr = smallq[j];
-    reg_batch<GLOBAL, V>(v, (int)lane < tot, bl, fr.f, (int)(fr.l - fr.f), fr.d, lane, out);
+    reg_batch<GLOBAL, V>(v, (int)lane < tot, bl, fr.f, (int)(fr.l - fr.f), fr.d, lane, out,
+                         tbase);
     q0 = q1;
   }
   sync_mem<GLOBAL>();
@@ -794,7 +798,7 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
     if (bd) carry = c + 63 - (uint32_t)__clzll(bd);
     if (x < n && b != 3) {
       if (b == 2) {
-        out[x] = v.T[x];
+        out[x] = tbase + v.T[x];
       } else {
         const typename V::key_t kx = v.K[x];
         uint32_t r = 0;
@@ -807,7 +811,7 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
         for (int j = 0; j < THRESH; ++j)
           r += (uint32_t)(s + j < e) &
                ((uint32_t)(ky[j] < kx) | ((uint32_t)(ky[j] == kx) & (uint32_t)(s + j < x)));
-        out[s + r] = v.T[x];
+        out[s + r] = tbase + v.T[x];
       }
     }
   }
@@ -896,14 +900,14 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
   uint8_t *smem = smem_all + ((size_t)wv * GPW + half) * slab;
   const uint32_t nfr = cap / (THRESH + 1) + 2;
   KT *K = reinterpret_cast<KT *>(smem);
-  uint32_t *T = reinterpret_cast<uint32_t *>(K + cap);
+  uint16_t *T = reinterpret_cast<uint16_t *>(K + cap);  // tags: positions in the group
   Frame *stack = reinterpret_cast<Frame *>(T + cap);
   Frame *smallq = stack + lds_stack(cap);
   Frame *heapq = smallq + nfr;
   uint16_t *PL = reinterpret_cast<uint16_t *>(heapq + nfr);
   uint16_t *PR = PL + cap;
   uint8_t *B = reinterpret_cast<uint8_t *>(PR + cap);
-  const ViewT<KT, uint16_t> v{K, T, PL, PR, B};
+  const ViewT<KT, uint16_t, uint16_t> v{K, T, PL, PR, B};
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
   for (uint32_t w = lo + (blockIdx.x * WPB + wv) * GPW + half; w < hi;
@@ -912,11 +916,12 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
     const uint32_t b = goff[g], n = goff[g + 1] - b;
     for (uint32_t x = lane; x < n; x += W) {
       K[x] = (KT)key[b + x];
-      T[x] = b + x;  // tags are positions
+      T[x] = (uint16_t)x;  // tags are positions (the output adds b)
     }
     wave_sync();
-    wave_std_sort<false, ViewT<KT, uint16_t>, W>(v, n, otag + b, stack, smallq, heapq, L,
-                                                 2 * (31 - __clz((int)n)), reg_max);
+    wave_std_sort<false, ViewT<KT, uint16_t, uint16_t>, W>(v, n, otag + b, stack, smallq, heapq,
+                                                           L, 2 * (31 - __clz((int)n)), reg_max,
+                                                           b);
     wave_sync();
   }
 }
@@ -1327,9 +1332,9 @@ __global__ void __launch_bounds__(256) k_tier_lists(const uint32_t *goff, uint32
   }
 }
 
-size_t lds_bytes(uint32_t cap, size_t key_bytes) {
+size_t lds_bytes(uint32_t cap, size_t key_bytes) {  // keys, 16-bit tags, PL, PR, B, frames
   const uint32_t nfr = cap / (THRESH + 1) + 2;
-  return (size_t)cap * (key_bytes + 4 + 2 + 2 + 1) + (lds_stack(cap) + 2 * nfr) * sizeof(Frame) +
+  return (size_t)cap * (key_bytes + 2 + 2 + 2 + 1) + (lds_stack(cap) + 2 * nfr) * sizeof(Frame) +
          16;
 }
 
@@ -1462,13 +1467,15 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   };
   const int big0 = side ? NLDS - lds_big : NLDS;  // tiers [big0, NLDS) go first on side
   for (int j = NLDS - 1; j >= big0; --j) launch_lds(j, s2);
-  // groups of 2..16 and 17..32 members: on `st` after the 33..64 tier
-  // (RK_GS_SMALL1=1, the default) or on `side` after its LDS tiers (0).  The
-  // side stream's two large LDS tiers are the longer chain (~0.96 against
-  // ~0.88 ms of kernel time on `st`): group-sort phase 1.20 -> 1.13 ms
+  // groups of 2..16 and 17..32 members: on `side` after its LDS tiers
+  // (RK_GS_SMALL1=0, the default) or on `st` after the 33..64 tier (1).  With
+  // 32-bit LDS tags the side stream's two large LDS tiers were the longer
+  // chain and 1 was faster (group-sort phase 1.20 -> 1.13 ms); with 16-bit
+  // tags (the 257..512 tier's slab 7.7 -> 6.7 KB: 24 resident wavefronts per
+  // CU instead of 20) 0 is: 1.07-1.08 against 1.15 ms
   static const int small_main = [] {
     const char *e = getenv("RK_GS_SMALL1");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   auto launch_small = [&](hipStream_t sj) {
     kt_begin(sj, KID_SORT_SMALL);

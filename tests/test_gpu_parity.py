@@ -433,7 +433,7 @@ print(h.hexdigest(), r.n_groups)
 """
 
 
-@pytest.mark.parametrize("env", ["RK_GS_BIG=0", "RK_GS_BIG=4", "RK_GS_REG1=0", "RK_GS_SMALL1=0",
+@pytest.mark.parametrize("env", ["RK_GS_BIG=0", "RK_GS_BIG=4", "RK_GS_REG1=0", "RK_GS_SMALL1=1",
                                  "RK_SWEEP_BLIND=1", "RK_NW_MINBITS=8",
                                  "RK_NW_SPLIT=0", "RK_GS_HALF=256", "RK_GS_HALF=2048"])
 def test_schedule_switches_bit_identical(gpu_ctx, env):
