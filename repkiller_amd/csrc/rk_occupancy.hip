@@ -1142,7 +1142,10 @@ __device__ __forceinline__ int below_count(uint64_t m) {  // set bits below this
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-constexpr int LCAP = 128;  // own-run list
+#ifndef RK_LCAP
+#define RK_LCAP 128
+#endif
+constexpr int LCAP = RK_LCAP;  // own-run list
 constexpr int NCAP = 64;   // neighbour-run list, per side
 
 struct LongLds {
