@@ -69,13 +69,13 @@ abcfg5)  # parity, then cfg5 / cfg3 against the HEAD build under tools/mb/base, 
   RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg5 --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 6
   ;;
 abcap)  # the long-run walk's own-list capacity at cfg5 (RK_LCAP builds under tools/mb/l*)
-  for v in l256 l512; do
+  for v in ${@:-l256 l512}; do
     RK_LIB=tools/mb/$v/librepkiller_amd.so bench ${v}_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 1
   done
   RK_LIB=repkiller_amd/librepkiller_amd.so bench main_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
   ;;
 absplit)  # phase A / B boundary at cfg5 (RK_SPLIT_T builds under tools/mb/s*)
-  for v in s1024 s2048; do
+  for v in ${@:-s1024 s2048}; do
     RK_LIB=tools/mb/$v/librepkiller_amd.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q -k std_sort --timeout 120 --timeout-method thread > $O/parity_$v.log 2>&1 || exit 1
     RK_LIB=tools/mb/$v/librepkiller_amd.so bench ${v}_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
   done
