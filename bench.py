@@ -8,11 +8,14 @@ flag and output order in HBM (the reference's generate_fragment_groups +
 generate_diagonal_func + sort_groups + repeat flag, commonFunctions.cpp:41-177).
 
 Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one process per GPU.
-`value` at N>1 (default `--mode auto`): ONE fragment set of 50M x N fragments
-over the 3 Gbp genome (rank r holds rows [r*50M, (r+1)*50M), each block seeded
-3+r) classified by rk_classify_sharded with RCCL all-to-alls over xGMI
-(xStart/10 slices, X/Y halo exchange, cross-slice roots, gid-range member sort;
-DESIGN.md "Multi-GPU") -- weak scaling.  The same run first measures
+`value` at N>1 (default `--mode auto`): the SAME 50M-fragment set as the N=1
+line (cfg3's seed-3 set, pinned by tests/golden/large_hashes.json), rank r
+holding file rows [50M r / N, 50M (r+1) / N), classified by rk_classify_sharded
+with RCCL all-to-alls over xGMI (xStart/10 slices, X/Y halo exchange,
+cross-slice roots, gid-range member sort; DESIGN.md "Multi-GPU") -- strong
+scaling.  After the timed region every rank's output share is gathered to rank
+0 and the whole result's digest is checked against the reference's (`parity`).
+The same run first measures
 `replicas`: every rank classifies its own independent 50M set (no data-path
 collective), reported beside the value under `replicas`, never as it: if the
 sharded leg fails, `value` is null and the error is reported.  A gloo barrier
@@ -60,11 +63,11 @@ CONFIGS = {
                  desc="cfg3: 50M fragments, 3 Gbp human-scale self-comparison"),
     # BASELINE.json configs[3] is quoted for 8 GPUs; its 200M fragments also fit
     # one MI355X (~62 GB of HBM), so it runs here as a single-GPU stress case
-    "cfg4": dict(n=200_000_000, genome_len=3_000_000_000, total=True,
+    "cfg4": dict(n=200_000_000, genome_len=3_000_000_000,
                  desc="cfg4: 200M fragments, 3 Gbp x 3 Gbp"),
     # BASELINE.json configs[4] is quoted for 8 GPUs ("streaming / HBM-spill");
     # its 1B fragments fit one MI355X's HBM too (run it with --no-cpu)
-    "cfg5": dict(n=1_000_000_000, genome_len=15_000_000_000, total=True,
+    "cfg5": dict(n=1_000_000_000, genome_len=15_000_000_000,
                  synth=dict(family_frac=0.95, copies=(100, 600)),
                  desc="cfg5: 1B fragments, 15 Gbp repeat-rich self-comparison"),
 }
@@ -87,6 +90,12 @@ def dist_setup():
             os.dup2(saved, 1)
             os.close(saved)
     return rank, world, local
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')} rank {os.environ.get('RANK', '0')}] {msg}",
+          file=sys.stderr, flush=True)
 
 
 def barrier(world):
@@ -353,45 +362,131 @@ def upload(f, dev):
             torch.from_numpy(f.strand).to(dev))
 
 
+def config_seed(name: str) -> int:
+    """The generator seed of a config's ONE fragment set: its number (cfg3 -> 3,
+    the seed tests/golden/large_hashes.json pins for cfg3 / cfg4)."""
+    return int(name[3:])
+
+
+def row_block(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Rank r's contiguous block of file-order rows of an n-row set."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def gather_result(world: int, rank: int, off: int, order, gid, rep, n_total: int):
+    """Every rank's share of the output (output rows [off, off + len(order)) of the
+    whole result) to rank 0, which returns the whole (order, gid, rep); other
+    ranks return None.  Shares must tile [0, n_total) exactly."""
+    order = np.ascontiguousarray(order, dtype=np.uint32)
+    gid = np.ascontiguousarray(gid, dtype=np.uint32)
+    rep = np.ascontiguousarray(rep, dtype=np.uint8)
+    k = len(order)
+    if world == 1:
+        assert off == 0 and k == n_total, (off, k, n_total)
+        return order, gid, rep
+    import torch.distributed as dist
+    meta = torch.tensor([off, k], dtype=torch.int64)
+    metas = [torch.empty(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(metas, meta)
+    spans = [(int(m[0]), int(m[1])) for m in metas]
+    kmax = max(1, max(c for _, c in spans))
+    buf = torch.zeros(9 * kmax, dtype=torch.uint8)
+    b = buf.numpy()
+    b[:4 * k] = order.view(np.uint8)
+    b[4 * kmax:4 * kmax + 4 * k] = gid.view(np.uint8)
+    b[8 * kmax:8 * kmax + k] = rep
+    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, bufs, dst=0)
+    if rank != 0:
+        return None
+    out_o, out_g = np.empty(n_total, np.uint32), np.empty(n_total, np.uint32)
+    out_r = np.empty(n_total, np.uint8)
+    pos = 0
+    for (o, c), t in sorted(zip(spans, bufs), key=lambda st: st[0][0]):
+        assert o == pos, f"output shares do not tile: share at {o}, expected {pos}"
+        a = t.numpy()
+        out_o[o:o + c] = a[:4 * c].view(np.uint32)
+        out_g[o:o + c] = a[4 * kmax:4 * kmax + 4 * c].view(np.uint32)
+        out_r[o:o + c] = a[8 * kmax:8 * kmax + c]
+        pos += c
+    assert pos == n_total, (pos, n_total)
+    return out_o, out_g, out_r
+
+
 def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
-    """ONE fragment set, rank r holding its block of rows: n x world rows (weak
-    scaling), or -- for the configs BASELINE quotes as one set over 8 GPUs
-    (cfg4, cfg5: `total`) -- the config's n rows split over the ranks (strong)."""
+    """ONE fragment set over the ranks (strong scaling): the config's own
+    single-seed set (cfg3: the 50M rows pinned by large_hashes.json), every
+    rank generating it deterministically and keeping its contiguous block of
+    file-order rows.  After the timed region every rank's output share goes to
+    rank 0, which checks the whole result's digest against the reference's.
+    cfg5 (1B rows: one whole copy per rank does not fit the host) is instead
+    world independently seeded blocks of n / world rows (no digest)."""
     n_cfg, L = cfg["n"], cfg["genome_len"]
-    total = cfg.get("total", False)
-    n = n_cfg // world + (1 if rank < n_cfg % world else 0) if total else n_cfg
-    f = rk.synth(n, L, seed=rank_seed(rank), **cfg.get("synth", {}))  # this rank's block
+    a, b = row_block(n_cfg, rank, world)
+    one_set = not cfg.get("synth")
+    if one_set:
+        f = rk.synth(n_cfg, L, seed=config_seed(args.config), with_ident=False)
+        f = rk.Frags(f.x_start[a:b], f.y_start[a:b], f.length[a:b], f.strand[a:b])
+    else:
+        f = rk.synth(b - a, L, seed=rank_seed(rank), with_ident=False, **cfg.get("synth", {}))
+    n = b - a
     x, y, ln, s = upload(f, dev)
     del f
+    log(f"sharded: rows [{a}, {b}) of {n_cfg} uploaded")
     comm = (rk.Comm.rccl(rank, world, local) if args.comm == "rccl"
             else rk.Comm.torch_host(rank, world))
+    log(f"sharded: {args.comm} comm up")
 
     def step():
         return rk.classify_sharded(ctx, comm, x, y, ln, s, L, L, args.len_ratio, args.pos_ratio,
                                    copy=False)
 
     out, dt = timed(step, args, world, ctx)
+    log(f"sharded: {args.steps} timed steps in {dt:.3f} s")
     frags_total, dt_max = aggregate(world, n, dt)
+    # the timed steps' result, before any further step runs
+    share = rk.shard_copy(ctx, out)
     st = rk.shard_stats(ctx)
     sent = allsum(world, float(st["bytes_sent"]))
     kernels, roofline = kernel_tables(step, args, ctx, f"{args.config}-sharded-x{world}")
     comm.close()
+    whole = gather_result(world, rank, out.out_offset, share.out_order, share.gid, share.repval,
+                          out.n_out_total)
+    log("sharded: result gathered")
+    parity = None
+    if rank == 0:
+        digest = arrays_sha256(*whole)
+        e = large_entry(cfg)
+        pinned = (one_set and e is not None
+                  and e.get("synth", {}).get("seed") == config_seed(args.config)
+                  and e["synth"].get("n") == n_cfg and e["synth"].get("genome_len") == L
+                  and e.get("len_ratio") == args.len_ratio and e.get("pos_ratio") == args.pos_ratio)
+        parity = {"result_sha256": digest,
+                  "matches_reference_digest": (digest == e["result_sha256"]) if pinned else None,
+                  "gathered_from_ranks": world,
+                  "pinned_by": ("tests/golden/large_hashes.json (the reference's output for this "
+                                "input; cfg4: the restatement's, pinned to the reference at cfg3)"
+                                if pinned else "no reference digest for this input")}
+        del whole
     value = frags_total * args.steps / dt_max
     n_all = int(frags_total)
     return {
         "value": round(value, 1), "unit": "fragments/s", "n_gpus": world,
         "ms_per_step": round(dt_max / args.steps * 1e3, 3),
-        "scaling": "strong" if total else "weak",
-        "workload": (f"ONE {n_all}-fragment set over a {L} bp genome, sharded over {world} GPUs"
-                     + (f" ({world} independently seeded blocks of ~{n} rows, cfg's size and "
-                        f"genome; not the single-seed set of the one-GPU {args.config} run)"
-                        if total else f" ({n} fragments per GPU; N=4 is cfg4's size)")),
+        "scaling": "strong",
+        "workload": (f"ONE {n_all}-fragment set over a {L} bp genome, sharded over {world} GPUs: "
+                     + (f"{args.config}'s single seed-{config_seed(args.config)} set (the "
+                        f"one-GPU line's input), rank r holding file rows "
+                        f"[{n_cfg} r / {world}, {n_cfg} (r+1) / {world})" if one_set else
+                        f"{world} independently seeded blocks of ~{n} rows (cfg's size and "
+                        f"genome; not the single-seed set of the one-GPU {args.config} run)")),
         "fragments_total": n_all, "comm": args.comm,
         "hbm_algorithmic_GBps": round(50 * value / 1e9, 3),
         "roofline": roofline, "kernels": kernels,
         "shard_rank0": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
         "exchange_bytes_per_step": round(sent),
         "groups": out.n_groups, "grouped_fragments": out.n_out_total,
+        "parity": parity,
     }
 
 
@@ -425,11 +520,16 @@ def host_legs(ctx, x, y, ln, s, L, args) -> dict:
         dt = time.perf_counter() - t0
         out[kind] = {"fragments_per_s": round(n * args.steps / dt, 1),
                      "ms_per_call": round(dt / args.steps * 1e3, 3),
-                     **{k: round(v / args.steps, 3) for k, v in acc.items()}}
+                     **{k: round(v / args.steps, 3) for k, v in acc.items()},
+                     # NUMA nodes (-1: unknown / unbound): the caller's input pages,
+                     # the packing threads' binding, the pinned staging slots, the GPU
+                     "numa": {k: st[f"numa_{k}"] for k in ("input", "threads", "staging",
+                                                           "gpu")}}
         del cols, f, res
     out["steps"] = args.steps
     out["note"] = ("host wall time per call; kernels_ms = HIP-event time of the device "
-                   "pipeline inside the call")
+                   "pipeline inside the call; the packing threads are bound to the node of "
+                   "the caller's pages (RK_IO_NUMA=0: unbound)")
     return out
 
 
@@ -450,7 +550,9 @@ def bench_single(args, cfg, rank, world, dev, ctx) -> dict:
         return ctx.classify_device(x, y, ln, s, gid, rep, order, L, L, args.len_ratio,
                                    args.pos_ratio)
 
+    log(f"single: {n} rows uploaded")
     (n_out, n_groups), dt = timed(step, args, world, ctx)
+    log(f"single: {args.steps} timed steps in {dt:.3f} s")
     frags_total, dt_max = aggregate(world, n, dt)
     phases = ctx.phases()
     st = ctx.stats()
@@ -541,15 +643,16 @@ def main():
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": sh["ms_per_step"],
                 "higher_is_better": True, "scaling": sh["scaling"], "vs_baseline": None,
                 "dtype": "u64/f64",
-                "data": f"synthetic (SURVEY.md §8d generator; rank r's block seeded 3+r), ONE "
-                        f"fragment set of {sh['fragments_total']} fragments",
+                "data": f"synthetic (SURVEY.md §8d generator), ONE fragment set of "
+                        f"{sh['fragments_total']} fragments",
                 "config": {"workload": sh["workload"],
                            "fragments_per_gpu": sh["fragments_total"] // world,
                            "genome_bp": cfg["genome_len"], "len_ratio": args.len_ratio,
                            "pos_ratio": args.pos_ratio,
                            "parallelism": f"sharded x{world} ({args.comm}): xStart/10 slices"},
                 "hbm_algorithmic_GBps": sh["hbm_algorithmic_GBps"],
-                "roofline": sh["roofline"], "sharded": sh}
+                "fragments_total": sh["fragments_total"],
+                "roofline": sh["roofline"], "parity": sh.pop("parity"), "sharded": sh}
 
     same_input = None
     if args.mode == "sharded":
@@ -601,6 +704,7 @@ def main():
     if rank != 0:
         return
     if not args.no_cpu and world == 1:
+        log("cpu baseline")
         line["cpu_baseline"] = cpu_baseline(cfg, line["ms_per_step"] / 1e3 * args.steps,
                                             same_input)
     else:

@@ -100,6 +100,10 @@ typedef struct {
                                records (order + flag back, gids rebuilt on the host), 0
                                when as the SoA */
   uint32_t reserved;
+  /* rk_classify*: NUMA nodes of the host side of the last upload (-1: unknown /
+     not bound): the caller's input pages, the node the packing threads were
+     bound to (RK_IO_NUMA=0: never bound), the pinned staging slots, the GPU */
+  int32_t numa_input, numa_threads, numa_staging, numa_gpu;
 } rk_stats;
 
 int rk_create(rk_ctx **ctx, int device);
@@ -211,6 +215,8 @@ typedef struct {
   double ms_total, ms_ingress, ms_x, ms_y, ms_roots, ms_members; /* host wall */
   uint32_t generic_driver;   /* 1: the generic driver ran (a row outside the 16-B record
                                 or a slice of >= 2^30 rows, or RK_SHARD_GENERIC=1) */
+  uint32_t order_split;      /* 1: this rank's slice took the two-stage order sort
+                                (coarse passes + per-segment LDS sort) */
 } rk_shard_stats;
 
 /* in_dev: this rank's block of input rows (device SoA, FILE order); blocks are

@@ -89,7 +89,9 @@ class Stats(ctypes.Structure):
                 ("device_ms", ctypes.c_double), ("pipeline", ctypes.c_uint32),
                 ("record_fallback", ctypes.c_uint32), ("h2d_ms", ctypes.c_double),
                 ("d2h_ms", ctypes.c_double), ("wire", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("reserved", ctypes.c_uint32), ("numa_input", ctypes.c_int32),
+                ("numa_threads", ctypes.c_int32), ("numa_staging", ctypes.c_int32),
+                ("numa_gpu", ctypes.c_int32)]
 
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -120,7 +122,8 @@ class ShardStats(ctypes.Structure):
                 ("bytes_sent", ctypes.c_uint64), ("ms_total", ctypes.c_double),
                 ("ms_ingress", ctypes.c_double), ("ms_x", ctypes.c_double),
                 ("ms_y", ctypes.c_double), ("ms_roots", ctypes.c_double),
-                ("ms_members", ctypes.c_double), ("generic_driver", ctypes.c_uint32)]
+                ("ms_members", ctypes.c_double), ("generic_driver", ctypes.c_uint32),
+                ("order_split", ctypes.c_uint32)]
 
 
 class SynthParams(ctypes.Structure):
@@ -653,15 +656,21 @@ def classify_sharded(ctx: "Context", comm: Comm, x, y, length, strand, len_x_hdr
                                  lead_in, ctypes.byref(res))
     if rc != RK_OK:
         raise RkError(rc, ctx.last_error())
-    out = None
+    out = ShardOutput(None, int(res.out_offset), int(res.n_out), int(res.n_out_total),
+                      int(res.n_groups), res)
     if copy:
-        k = int(res.n_out)
-        order, gid, rep = np.empty(k, np.uint32), np.empty(k, np.uint32), np.empty(k, np.uint8)
-        _check(lib.rk_shard_copy_result(ctx._h, ctypes.byref(res), _ptr(order), _ptr(gid),
-                                        _ptr(rep)), ctx.last_error())
-        out = ClassifyResult(gid, rep, order, int(res.n_groups))
-    return ShardOutput(out, int(res.out_offset), int(res.n_out), int(res.n_out_total),
-                       int(res.n_groups), res)
+        out.result = shard_copy(ctx, out)
+    return out
+
+
+def shard_copy(ctx: "Context", out: ShardOutput) -> ClassifyResult:
+    """Host copies of this rank's output share (rk_shard_copy_result) of the last
+    rk_classify_sharded call on ``ctx``; global file rows and group ids."""
+    k = out.n_out
+    order, gid, rep = np.empty(k, np.uint32), np.empty(k, np.uint32), np.empty(k, np.uint8)
+    _check(load_library().rk_shard_copy_result(ctx._h, ctypes.byref(out.raw), _ptr(order),
+                                               _ptr(gid), _ptr(rep)), ctx.last_error())
+    return ClassifyResult(gid, rep, order, out.n_groups)
 
 
 def classify_sharded_threads(f: Frags, ranks: int, len_x_hdr: int, len_y_hdr: int,

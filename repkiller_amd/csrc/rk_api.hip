@@ -39,7 +39,7 @@ const char *const kKernelNames[KID_COUNT] = {
     "k_row_keys (sharded)", "k_fill_y (sharded)", "k_y_results (sharded)", "k_x_own (sharded)",
     "k_merge_yx (sharded)", "k_sort_segments", "k_sweep_long32", "k_nw_order_hist",
     "k_onesweep", "k_nw_xchunk", "k_nw_fill_y", "k_nw_assign", "k_nw_xcount", "k_nw_x_bits",
-    "k_heap_segments", "k_seg_fine (order)", "k_seg_fine (members)",
+    "k_heap_segments", "k_seg_fine (order)", "k_seg_fine (members)", "k_seg_fine (Y)",
 };
 }  // namespace rk
 
@@ -476,6 +476,21 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     return b < 8 ? 8 : b > 9 ? 9 : b;
   }();
   const rk::NwDigits yd = rk::nw_plan(rk::bit_length(2ull * pl.nby - 1), bits12);
+  // The Y sort in two stages too (coarse passes + the segment kernel writing
+  // the CSR arrays) -- RK_NW_YSPLIT=0 restores the one-stage passes
+  static const bool ysplit_on = [] {
+    const char *e = getenv("RK_NW_YSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  static const bool y_overlap = [] {
+    const char *e = getenv("RK_Y_OVERLAP");
+    return e && e[0] == '1';
+  }();
+  const rk::NwOrderPlan yp = ysplit_on && !y_overlap
+                                 ? rk::nw_order_split(n, 2ull * pl.nby,
+                                                      rk::bit_length(2ull * pl.nby - 1))
+                                 : rk::NwOrderPlan{};
+  const bool ysplit = yp.coarse.passes > 0;
 
   HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
   // the control words and the order / Y / member digit histograms (ehist stays
@@ -483,8 +498,8 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   rk::zero_regions(st, {{w.ctrl, (64 + rk::PEND_WORDS) * sizeof(uint32_t)},
                         {w.ahist, 3 * 4096 * sizeof(uint32_t)}});
   mark(ctx, RK_PH_PREP);
-  rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, split ? op.coarse : ad, yd,
-                    w.ahist, w.yhist, w.ctrl, st, wire);
+  rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, split ? op.coarse : ad,
+                    ysplit ? yp.coarse : yd, w.ahist, w.yhist, w.ctrl, st, wire);
   HIPCHK(ctx, hipGetLastError());
   // The control words (errors, kept rows, pack flag, longest length) come back
   // while the split sort's coarse passes run -- they need only n -- when the
@@ -492,8 +507,10 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   // allocates it after the pack check, so an input that falls back to the
   // generic pipeline never holds both).  A fallback or an error then leaves
   // the coarse passes' output unused.
+  // (not after a call on this context fell back: an input that does not pack
+  // would run the coarse passes for nothing and book them to the order phase)
   bool early = false;
-  if (split) {
+  if (split && !ctx->nw_fell_back) {
     Carve probe{nullptr};
     NWork tmpw = w;
     early = carve_nw(probe, pl.n, pl.nbx, tmpw) <= ctx->ws_nw_cap;
@@ -518,8 +535,10 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   if (ctx->host[3]) {  // some row does not pack into a record
     *fallback = true;
     ctx->stats.record_fallback = 1;
+    ctx->nw_fell_back = true;
     return RK_OK;
   }
+  ctx->nw_fell_back = false;
   // every row packs: now the workspace (~190 B per row)
   if (!early && (rc = ensure_nw(ctx, pl.n, pl.nbx, w))) return rc;
   rk::ScanScratch ss{w.scan, w.scan_cap};
@@ -561,10 +580,6 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   // pass but the last on the second stream beside the X axis, the last one
   // looking up the X-hit bits (cfg3 11.0 ms against 11.2 with those passes
   // serial before X).
-  static const bool y_overlap = [] {
-    const char *e = getenv("RK_Y_OVERLAP");
-    return e && e[0] == '1';
-  }();
   if (y_overlap) {
     HIPCHK(ctx, hipEventRecord(ctx->fork, st));
     HIPCHK(ctx, hipStreamWaitEvent(st2, ctx->fork, 0));
@@ -597,6 +612,11 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
       HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
       rk::nw_y_sort_tail(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y,
                          w.xbits, st);
+    } else if (q == 0 && ysplit) {
+      // (the order records are done with after the X chunk kernel; the order
+      // sort's segment counts after its segment kernel)
+      rk::nw_y_sort_split_after_x(w.yrec, w.Rb, w.Ra, m, yp, w.yhist, w.ystatus, w.cy, pl.nby,
+                                  pl.max_y, w.xbits, w.chist, w.coff, ss, st);
     } else if (q == 0) {
       rk::nw_y_sort_after_x(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y,
                             w.xbits, st);
@@ -1172,6 +1192,7 @@ static int classify_wire(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *p
   ctx->stats.h2d_ms = t1 - t0;
   ctx->stats.d2h_ms = rk::wall_ms() - t2;
   ctx->stats.wire = 1;
+  rk::io_numa_stats(ctx, &ctx->stats);
   return RK_OK;
 }
 
@@ -1243,6 +1264,7 @@ extern "C" int rk_classify_pairs(rk_ctx *ctx, const rk_frags_soa *in, const rk_p
   if ((rc = rk::io_d2h(ctx, down))) return rc;
   ctx->stats.h2d_ms = t1 - t0;
   ctx->stats.d2h_ms = rk::wall_ms() - t2;
+  rk::io_numa_stats(ctx, &ctx->stats);
   return RK_OK;
 }
 

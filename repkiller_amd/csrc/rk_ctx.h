@@ -25,6 +25,7 @@ struct rk_pool {
 
 struct rk_ctx {
   int device = -1;
+  bool nw_fell_back = false;  // the last record-pipeline call handed over to the generic one
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;             // Y-axis sort, overlapped with the X sweeps
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -115,6 +116,8 @@ struct GidJob {
 };
 void gids_from_flags_async(const uint8_t *flag, size_t n, uint32_t *gid, int threads, GidJob &job);
 void io_destroy(rk_ctx *ctx);
+// the NUMA nodes of the last upload (rk_stats numa_*)
+void io_numa_stats(const rk_ctx *ctx, rk_stats *st);
 bool host_pinned(const void *p);
 double wall_ms();
 

@@ -62,7 +62,7 @@ enum KernelId : int {
   KID_SORT_GLOBAL, KID_EMIT, KID_PART, KID_EXCHANGE, KID_SHARD_AUX, KID_SH_ROWKEYS, KID_SH_FILLY,
   KID_SH_YRES, KID_SH_XOWN, KID_SH_MERGE, KID_SORT_SEGS, KID_SWEEP_LONG, KID_NW_HIST,
   KID_ONESWEEP, KID_NW_XCHUNK, KID_NW_FILLY, KID_NW_ASSIGN, KID_NW_XCOUNT, KID_NW_XBITS,
-  KID_SORT_HEAP, KID_NW_FINE, KID_NW_MFINE, KID_COUNT
+  KID_SORT_HEAP, KID_NW_FINE, KID_NW_MFINE, KID_NW_YFINE, KID_COUNT
 };
 extern const char *const kKernelNames[KID_COUNT];
 // group-sort tiers (rk_groupsort.hip tier_of): <=16, <=32, <=64, four LDS caps, larger
@@ -298,6 +298,7 @@ struct NwOrderPlan {
   int C = 0, F = 0;
   uint32_t nseg = 0;
   NwDigits coarse{};
+  uint32_t kbase = 0;  // subtracted from every key (a multiple of 2^F; 0 on one device)
 };
 // several regions cleared by one kernel launch (a memset launch each costs a
 // dispatch gap of ~4-9 us); null or empty regions are skipped
@@ -307,6 +308,7 @@ struct ZeroRegion {
 };
 void zero_regions(hipStream_t st, std::initializer_list<ZeroRegion> regs);
 NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int bits);  // nkeys: key values in use
+NwOrderPlan nw_order_split_range(uint32_t n, uint64_t klo, uint64_t khi);  // keys in [klo, khi)
 // the same in two halves: the clears (+ `extra`) and the coarse passes, then
 // the scan and the segment kernel (cc->cnts cleared by the first half's
 // `extra`) -- the host can read the order histogram's control words back in
@@ -363,6 +365,13 @@ void nw_y_sort_tail(const uint4 *yrec, const uint4 *tmp, uint32_t m, const NwDig
 // pass; the last writes CSR + states.  src0: the sharded driver's received Y
 // records, numbered by arrival in the first pass (yrec and tmp then only take
 // the intermediates)
+// the same in two stages (coarse passes + one block per coarse-key segment
+// writing the CSR arrays); yp = nw_order_split over the Y key; tmp2: m
+// records of scratch; chist / coff: 2^C + 1 words
+void nw_y_sort_split_after_x(uint4 *yrec, uint4 *tmp, uint4 *tmp2, uint32_t m,
+                             const NwOrderPlan &yp, const uint32_t *yhist, uint32_t *status,
+                             Csr cy, uint32_t nby, uint64_t max_y, const uint32_t *xbits,
+                             uint32_t *chist, uint32_t *coff, ScanScratch ss, hipStream_t st);
 void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits &y,
                        const uint32_t *yhist, uint32_t *status, Csr cy, uint32_t nby,
                        uint64_t max_y, const uint32_t *xbits, hipStream_t st,

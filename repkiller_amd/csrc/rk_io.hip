@@ -12,10 +12,16 @@
 // engine moves chunk k-1 (and, for results, the DMA of chunk k+NS overlaps the
 // host copy of chunk k out of its slot).  HIP's own pageable path stages
 // through one thread; the parallel host copy is what lifts it to PCIe rate.
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <memory>
@@ -108,6 +114,85 @@ void par_copy(HostPool *pool, void *dst, const void *src, size_t len) {
   else pool->run(job);
 }
 
+// ---- NUMA placement of the host side (a two-socket host: the caller's pages,
+// the packing threads, the staging slots and the GPU may sit on different
+// nodes).  No libnuma: move_pages(2) with no target nodes reports the node of
+// each page, sysfs the CPUs of a node and the node of the GPU's PCI device.
+
+// the majority node of up to 16 pages sampled over [p, p + bytes); -1 when
+// none is resident (or the query is unavailable)
+int range_node(const void *p, size_t bytes) {
+  if (!p || !bytes) return -1;
+  constexpr int K = 16;
+  void *pages[K];
+  int status[K];
+  const long psz = sysconf(_SC_PAGESIZE);
+  for (int k = 0; k < K; ++k) {
+    const uintptr_t a = (uintptr_t)p + (uintptr_t)(bytes / K) * (uintptr_t)k;
+    pages[k] = (void *)(a & ~(uintptr_t)(psz - 1));
+  }
+  if (syscall(SYS_move_pages, 0, (unsigned long)K, pages, nullptr, status, 0) != 0) return -1;
+  int best = -1, bestc = 0;
+  for (int k = 0; k < K; ++k) {
+    if (status[k] < 0) continue;
+    int c = 0;
+    for (int j = 0; j < K; ++j) c += status[j] == status[k];
+    if (c > bestc) best = status[k], bestc = c;
+  }
+  return best;
+}
+
+// CPUs of NUMA node `node` (sysfs cpulist "0-15,64-79"); false when unknown
+static bool node_cpus(int node, cpu_set_t *set) {
+  CPU_ZERO(set);
+  char path[96];
+  std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE *f = std::fopen(path, "r");
+  if (!f) return false;
+  char buf[4096];
+  const size_t len = std::fread(buf, 1, sizeof buf - 1, f);
+  std::fclose(f);
+  buf[len] = 0;
+  bool any = false;
+  for (char *q = buf; *q;) {
+    if (!std::isdigit((unsigned char)*q)) {
+      ++q;
+      continue;
+    }
+    long a = std::strtol(q, &q, 10), b = a;
+    if (*q == '-') b = std::strtol(q + 1, &q, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, set), any = true;
+  }
+  return any;
+}
+
+// the node of the device's PCI function (sysfs), -1 when unknown
+static int device_node(int device) {
+  char bus[64] = {};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  for (char *c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+  char path[160];
+  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE *f = std::fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
+
+// RK_IO_NUMA=0: leave the packing threads where the scheduler puts them
+bool numa_bind_enabled() {
+  static const bool on = [] {
+    const char *e = std::getenv("RK_IO_NUMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 }  // namespace
 
 struct IoEngine {
@@ -115,6 +200,31 @@ struct IoEngine {
   char *slot[NSLOT] = {};
   hipEvent_t ev[NSLOT] = {};
   HostPool *pool = nullptr;
+  cpu_set_t allowed;      // the process' CPUs when the engine was built
+  int bound = -1;         // node the pool threads are bound to (-1: not bound)
+  int last_input = -1;    // node of the last upload's input pages
+  int staging = -1;       // node of the pinned staging slots
+  int gpu = -1;           // node of the device
+  // bind the pool's threads to the CPUs of `node` that this process may use
+  // (nothing to bind to, or RK_IO_NUMA=0: they stay unbound)
+  void bind(int node) {
+    if (node == bound || !numa_bind_enabled()) return;
+    cpu_set_t set;
+    if (node < 0 || !node_cpus(node, &set)) return;
+    CPU_AND(&set, &set, &allowed);
+    if (CPU_COUNT(&set) == 0) return;
+    const std::function<void(int)> job = [&](int) {
+      (void)sched_setaffinity(0, sizeof set, &set);  // (0: the calling thread)
+    };
+    pool->run(job);
+    bound = node;
+  }
+  // before packing the caller's rows / copying its pages: the threads go to
+  // the node that holds them
+  void place(const void *p, size_t bytes) {
+    last_input = range_node(p, bytes);
+    bind(last_input);
+  }
   ~IoEngine() {
     if (io) (void)hipStreamSynchronize(io);
     for (auto &e : ev)
@@ -141,7 +251,19 @@ static int io_build(rk_ctx *ctx, IoEngine *e) {
     HIPCHK(ctx, hipEventCreateWithFlags(&e->ev[k], hipEventDisableTiming));
   }
   e->pool = new HostPool(io_threads());
+  CPU_ZERO(&e->allowed);
+  if (sched_getaffinity(0, sizeof e->allowed, &e->allowed) != 0) CPU_ZERO(&e->allowed);
+  e->staging = range_node(e->slot[0], SLOT);
+  e->gpu = device_node(ctx->device);
   return RK_OK;
+}
+
+void io_numa_stats(const rk_ctx *ctx, rk_stats *st) {
+  const IoEngine *e = ctx->ioe;
+  st->numa_input = e ? e->last_input : -1;
+  st->numa_threads = e ? e->bound : -1;
+  st->numa_staging = e ? e->staging : -1;
+  st->numa_gpu = e ? e->gpu : -1;
 }
 
 static int io_ready(rk_ctx *ctx) {
@@ -171,6 +293,11 @@ int io_h2d(rk_ctx *ctx, const std::vector<IoPiece> &pieces) {
   int rc = io_ready(ctx);
   if (rc) return rc;
   IoEngine &e = *ctx->ioe;
+  for (const IoPiece &pc : pieces)
+    if (pc.bytes && !host_pinned(pc.host)) {
+      e.place(pc.host, pc.bytes);  // (the first pageable column decides)
+      break;
+    }
   bool busy[NSLOT] = {};
   int k = 0;
   for (const IoPiece &pc : pieces) {
@@ -240,6 +367,7 @@ int io_h2d_rows(rk_ctx *ctx, const rk_frags_soa &in, void *dev) {
   if (rc) return rc;
   IoEngine &e = *ctx->ioe;
   const size_t n = in.n, per = SLOT / 12;
+  e.place(in.x_start, n * 8);  // the threads read the caller's columns
   bool busy[NSLOT] = {};
   int k = 0;
   std::atomic<bool> bad{false};
@@ -285,8 +413,10 @@ void gids_from_flags_async(const uint8_t *flag, size_t n, uint32_t *gid, int thr
   const size_t share = (n + T - 1) / T;
   auto cnt = std::make_shared<std::vector<uint32_t>>(T + 1, 0u);
   auto arrived = std::make_shared<std::atomic<int>>(0);
-  for (int t = 0; t < T; ++t)
-    job.th.emplace_back([=] {
+  int started = 0;
+  try {
+    for (int t = 0; t < T; ++t, ++started)
+      job.th.emplace_back([=] {
       const size_t lo = std::min(n, (size_t)t * share), hi = std::min(n, lo + share);
       uint32_t c = 0;
       for (size_t i = lo; i < hi; ++i) c += flag[i] != 2;
@@ -300,6 +430,18 @@ void gids_from_flags_async(const uint8_t *flag, size_t n, uint32_t *gid, int thr
         gid[i] = g - 1;
       }
     });
+  } catch (...) {
+    // a thread could not be started: release the ones already waiting at the
+    // barrier (their partial counts give wrong gids), join them, and rebuild
+    // every gid here -- no exception crosses the C ABI, nothing spins forever
+    arrived->fetch_add(T - started, std::memory_order_acq_rel);
+    job.wait();
+    uint32_t g = 0;
+    for (size_t i = 0; i < n; ++i) {
+      g += flag[i] != 2;
+      gid[i] = g - 1;
+    }
+  }
 }
 
 double wall_ms() {

@@ -115,11 +115,12 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 struct SrcRec {
   using rec_t = uint4;
   const uint4 *in;
+  uint32_t sub = 0;  // key base (the sharded driver's slice-relative coarse keys)
   __device__ __forceinline__ uint4 load(uint32_t i) const {
     const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(in + i));
     return make_uint4(v.x, v.y, v.z, v.w);
   }
-  __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x; }
+  __device__ __forceinline__ uint32_t key(const uint4 &r) const { return r.x - sub; }
 };
 // 12-B records (the Y axis' records, and the member records when every sort
 // key fits 32 bits), key = .x
@@ -461,9 +462,10 @@ struct DstRecHist {
   uint4 *out;
   uint32_t *chist;  // records per coarse key
   int F;
+  uint32_t sub = 0;  // key base (as SrcRec::sub)
   __device__ __forceinline__ void store(uint32_t pos, const uint4 &r) const { out[pos] = r; }
   __device__ __forceinline__ void wave(const uint4 &r, bool live) const {
-    wave_run_add(live ? r.x >> F : NONE, chist);
+    wave_run_add(live ? (r.x - sub) >> F : NONE, chist);
   }
 };
 
@@ -648,6 +650,20 @@ struct MemberEmit {
     key[pos] = r.z;
     if (first) goff[r.x] = pos;
     if (pos + 1 == m) goff[G] = m;
+  }
+};
+
+// The Y axis' emit: the occupancy CSR arrays and the Y states (DstCsr, the
+// X-hit bit carried in bit 31 of the record); a segment's positions are
+// consecutive, so the five arrays are written as whole lines
+struct CsrEmit {
+  static constexpr int kWin = 1;
+  DstCsr dc;
+  __device__ __forceinline__ uint32_t begin(uint32_t *, uint32_t) const { return 0; }
+  __device__ __forceinline__ void end(uint32_t *, uint32_t) const {}
+  __device__ __forceinline__ void emit(uint32_t *, uint32_t, uint32_t pos, const uint3 &r,
+                                       bool live, bool) const {
+    if (live) dc.store(pos, r, 0u);
   }
 };
 
@@ -1596,6 +1612,25 @@ NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int b) {
   o.nseg = (uint32_t)1 << C;
   return o;
 }
+// the same over the keys [klo, khi) of one slice (the sharded driver): the
+// coarse keys are (key - kbase) >> F with kbase = klo rounded down to 2^F, so
+// the segments cover the slice's span, not the whole key space, and the fine
+// bits stay the key's own low F bits
+NwOrderPlan nw_order_split_range(uint32_t n, uint64_t klo, uint64_t khi) {
+  if (khi <= klo) return NwOrderPlan{};
+  // F as nw_order_split picks it (capped by the absolute key's bits)
+  const int b = bit_length(khi - 1);
+  int F = 0;
+  while (F < b && (double)n * (double)(2ull << F) <= (double)NW_SEG_TARGET * (double)(khi - klo))
+    ++F;
+  const uint64_t kbase = klo & ~((1ull << F) - 1);
+  NwOrderPlan o = nw_order_split(n, khi - klo, bit_length(khi - 1 - kbase));
+  // (its F is at most this F -- the same density test, a smaller cap -- so
+  // kbase stays a multiple of 2^o.F)
+  if (o.nseg && (kbase & ((1ull << o.F) - 1))) return NwOrderPlan{};
+  o.kbase = (uint32_t)kbase;
+  return o;
+}
 
 // the coarse passes (the last writes Rb and counts the coarse keys into
 // chist, 2^C + 1 words, zeroed here), the scan into segment starts, the fine
@@ -1623,12 +1658,12 @@ static void nw_order_coarse(const Src1 &first, double in_bytes, uint32_t n, cons
     uint32_t *ctr = status + sw - 64 + p;
     const uint32_t *gh = ghist + p * 1024;
     const bool last = p == D.passes - 1;
-    const DstRecHist dh{out, chist, op.F};
+    const DstRecHist dh{out, chist, op.F, op.kbase};
     const double bytes = (p == 0 ? in_bytes : 16.0) * n + 16.0 * n;
     if (p == 0 && last) launch_pass(first, dh, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
     else if (p == 0) launch_pass(first, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
-    else if (last) launch_pass(SrcRec{src}, dh, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
-    else launch_pass(SrcRec{src}, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else if (last) launch_pass(SrcRec{src, op.kbase}, dh, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    else launch_pass(SrcRec{src, op.kbase}, DstRec{out}, n, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
   }
 }
 // the second half: the counts' scan into segment starts, the segment kernel
@@ -1686,7 +1721,8 @@ void nw_order_sort_recs_split(const uint4 *in, uint32_t m, uint32_t nby, uint32_
                               uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
                               uint32_t *coff, ScanScratch ss, const NwChunkCounts *cc,
                               hipStream_t st) {
-  nw_order_coarse(SrcRec{in}, 16.0, m, op, ghist, status, Ra, Rb, chist, counts_region(cc), st);
+  nw_order_coarse(SrcRec{in, op.kbase}, 16.0, m, op, ghist, status, Ra, Rb, chist,
+                  counts_region(cc), st);
   nw_order_fine(m, m, nby, base, op, Ra, Rb, yrec, tmp, chist, coff, ss, cc, st);
 }
 
@@ -1795,6 +1831,59 @@ void nw_y_sort_after_x(const uint4 *yrec, uint4 *tmp, uint32_t m, const NwDigits
                   nxt);
     src = out;
   }
+}
+
+// The same in two stages (round 5): the coarse passes over the Y key's top C
+// bits (the first carrying the X-hit bits, the last counting each coarse
+// key), then one block per coarse-key segment sorts the F fine bits in LDS
+// and writes the CSR arrays and the Y states (CsrEmit).  The last record pass
+// of the one-stage sort scattered the five CSR arrays over ~14-record digit
+// segments (1-B stores: partial lines); a segment writes them whole.
+// Buffers: yrec (records in processing order; later k_seg_big's A), tmp (the
+// last coarse pass' output), tmp2 (scratch: the other coarse pass, k_seg_big's
+// B); chist / coff: 2^C + 1 words each.
+void nw_y_sort_split_after_x(uint4 *yrec, uint4 *tmp, uint4 *tmp2, uint32_t m,
+                             const NwOrderPlan &yp, const uint32_t *yhist, uint32_t *status,
+                             Csr cy, uint32_t nby, uint64_t max_y, const uint32_t *xbits,
+                             uint32_t *chist, uint32_t *coff, ScanScratch ss, hipStream_t st) {
+  const Digits D = to_digits(yp.coarse);
+  const size_t sw = nw_status_words(m);
+  const PassStatus ps = pass_status(status, m, D, 12);
+  // the passes' tile counters, the first pass' status words, the coarse-key counts
+  zero_regions(st, {{status + sw - 64, 64 * 4},
+                    ps.region(0, m, D),
+                    {chist, ((size_t)yp.nseg + 1) * 4}});
+  uint3 *a = reinterpret_cast<uint3 *>(tmp), *b = reinterpret_cast<uint3 *>(tmp2);
+  const uint3 *src = reinterpret_cast<const uint3 *>(yrec);
+  const uint64_t *bits64 = reinterpret_cast<const uint64_t *>(xbits);
+  for (int p = 0; p < D.passes; ++p) {
+    if (p > 0) ps.prepare(p, m, D, st);
+    const bool last = p == D.passes - 1;
+    uint3 *out = ((D.passes - 1 - p) % 2 == 0) ? a : b;  // the last coarse pass lands in a
+    uint32_t *stp = ps.use(p), *nxt = ps.next(p, D.passes), *ctr = status + sw - 64 + p;
+    const uint32_t *gh = ghist_of(yhist, p);
+    const double bytes = (p == 0 ? 12.0 + 0.125 : 12.0) * m + 12.0 * m;
+    const DstRec12Hist dh{out, chist, yp.F};
+    if (p == 0) {
+      const SrcYX12 s0{src, bits64, (m + 63) / 64};
+      if (last) launch_pass(s0, dh, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+      else launch_pass(s0, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    } else if (last) {
+      launch_pass(SrcRec12{src}, dh, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
+    } else {
+      launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes,
+                  nxt);
+    }
+    src = out;
+  }
+  exclusive_scan_u32(chist, coff, (size_t)yp.nseg + 1, ss, st);
+  const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, nullptr, cy.state, true};
+  kt_begin(st, KID_NW_YFINE);
+  // (the counts are free after the scan: the list of segments above OF_CAP)
+  launch_seg(SegArgs<uint3>{a, reinterpret_cast<uint3 *>(yrec), b, coff, yp.nseg, yp.F, chist},
+             CsrEmit{dc}, st);
+  // records in; key, entry, packed record, neighbour code and state out
+  kt_end(st, KID_NW_YFINE, 30.0 * m);
 }
 
 // The member sort by gid: 12-B records {gid, row, key} when every sort key

@@ -474,9 +474,10 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   uint4 *yown = S.take<uint4>(SN_YOWN, (size_t)m * 3 / 4 + 2);  // 12-B records
   // the two-stage order sort (coarse passes, per-segment LDS sort) when the
   // slice's key density suits it: the slice holds m rows over its own key
-  // span, and the coarse digits are absolute keys >> F
-  const NwOrderPlan op =
-      nw_order_split(m, slice_keys.b[me + 1] - slice_keys.b[me], bit_length(vsize - 1));
+  // span, and the coarse digits are slice-relative, (key - kbase) >> F, so the
+  // segment table covers that span only
+  const NwOrderPlan op = nw_order_split_range(m, slice_keys.b[me], slice_keys.b[me + 1]);
+  ss.order_split = op.nseg ? 1u : 0u;
   // the X axis' chunk width (step 6) from the slice's own rows: the fine
   // kernel then counts the slice's X-chunk entries as it writes the order, and
   // step 6 adds the halo's (when its width comes out the same)
@@ -490,7 +491,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     uint32_t *chist = S.take<uint32_t>(SN_CHIST, nw_seg_words(m));
     uint32_t *coff = S.take<uint32_t>(SN_COFF, nw_seg_words(m));
     own_cc.cnts = S.take<uint32_t>(SN_XCNT0, (size_t)3 * own_cc.nch + 2);
-    nw_rec_hist(rin, 16, m, 0, op.coarse, ahist, st);
+    nw_rec_hist(rin, 16, m, op.kbase, op.coarse, ahist, st);
     // rin is read by the first coarse pass only: the fine kernel's scratch
     nw_order_sort_recs_split(rin, m, nby, poff, op, ahist, astat, Ra, Rb, yown,
                              const_cast<uint4 *>(rin), chist, coff,

@@ -435,7 +435,8 @@ print(h.hexdigest(), r.n_groups)
 
 @pytest.mark.parametrize("env", ["RK_GS_BIG=0", "RK_GS_BIG=4", "RK_GS_REG1=0", "RK_GS_SMALL1=1",
                                  "RK_SWEEP_BLIND=1", "RK_NW_MINBITS=8",
-                                 "RK_NW_SPLIT=0", "RK_GS_HALF=256", "RK_GS_HALF=2048"])
+                                 "RK_NW_SPLIT=0", "RK_GS_HALF=256", "RK_GS_HALF=2048",
+                                 "RK_NW_YSPLIT=0", "RK_NW_MSPLIT=1", "RK_Y_OVERLAP=1"])
 def test_schedule_switches_bit_identical(gpu_ctx, env):
     """The measurement switches only move work between streams or change the
     radix of a pass: the result must not change.  300k rows at cfg3 density

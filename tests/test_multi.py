@@ -62,6 +62,56 @@ def test_single_rank_is_local():
     assert bench.rank_seed(0) != bench.rank_seed(1)
 
 
+def _gather_worker(rank, world, port, q):
+    """bench.gather_result: rank r holds output rows [off_r, off_r + k_r) of one
+    whole result (ragged shares, one empty), rank 0 reassembles it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    bench.dist_setup()
+    n = 1000
+    rng = np.random.default_rng(7)
+    order = rng.permutation(n).astype(np.uint32)
+    gid = np.sort(rng.integers(0, 300, n)).astype(np.uint32)
+    rep = rng.integers(0, 3, n).astype(np.uint8)
+    # ragged shares; at world 3 rank 0's share is empty
+    cuts = {2: [0, 517, n], 3: [0, 0, 613, n]}[world]
+    a, b = cuts[rank], cuts[rank + 1]
+    whole = bench.gather_result(world, rank, a, order[a:b], gid[a:b], rep[a:b], n)
+    if rank == 0:
+        same = all(np.array_equal(u, v) for u, v in zip(whole, (order, gid, rep)))
+        q.put((rank, same, bench.arrays_sha256(*whole) == bench.arrays_sha256(order, gid, rep)))
+    else:
+        q.put((rank, whole is None, True))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_result_reassembles_shares(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(r[1] and r[2] for r in res), res
+
+
+def test_strong_scaling_blocks_tile_the_set():
+    import bench
+    n = 50_000_000
+    for world in (1, 2, 3, 4, 8):
+        blocks = [bench.row_block(n, r, world) for r in range(world)]
+        assert blocks[0][0] == 0 and blocks[-1][1] == n
+        assert all(blocks[r][1] == blocks[r + 1][0] for r in range(world - 1))
+    assert bench.config_seed("cfg3") == 3 and bench.config_seed("cfg4") == 4
+
+
 def _comm_worker(rank, world, port, q):
     """The gloo host-callback collectives behind rk.Comm.torch_host (the comm the
     multi-rank GPU tests run rk_classify_sharded on), called as the C side does."""

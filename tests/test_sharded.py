@@ -167,6 +167,27 @@ def test_sharded_order_sort_unsplit(gpu_ctx):
     _check_vs_single_device(gpu_ctx, got, cases, 2, generic=False)
 
 
+def test_sharded_y_early_schedule(gpu_ctx):
+    """RK_SH_YEARLY=1: the round-3 schedule of the slices' Y sort (its head passes
+    beside the X axis on the second stream) -- the same result."""
+    cases = [SYNTH[0], SYNTH[3]]
+    got = run_ranks(2, cases, env={"RK_SH_YEARLY": "1"})
+    _check_vs_single_device(gpu_ctx, got, cases, 2, generic=False)
+
+
+def test_sharded_order_split_at_cfg3_density(gpu_ctx):
+    """cfg3's density (50M rows over 3 Gbp) over 4 slices: every slice takes the
+    two-stage order sort.  Its coarse keys are slice-relative, so the segment
+    table covers one slice's key span (with absolute coarse keys a 1M-row slice
+    would need 2^11 segments against a 2017-word table and fall back to the
+    four LSD passes)."""
+    cases = [dict(kind="synth", n=4_000_000, L=240_000_000, seed=34)]
+    got = run_ranks(4, cases, timeout=200)
+    _check_vs_single_device(gpu_ctx, got, cases, 4, generic=False)
+    _, _, _, _, stats = assemble(got, 0, 4)
+    assert all(st["order_split"] == 1 for st in stats), stats
+
+
 def test_sharded_record_driver_used(gpu_ctx):
     """Every SYNTH set packs: the record driver classified them (not the fallback)."""
     cases = SYNTH[:2]

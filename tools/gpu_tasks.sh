@@ -6,6 +6,7 @@
 #
 #   suite     smoke() and the whole GPU suite, as the driver runs them
 #   bench     the driver's bench command (cfg3, 20 steps, CPU baseline)
+#   parity    tests/test_gpu_parity.py (both pipelines against the oracle)
 #   refresh   bench + rocprofv3 --kernel-trace --stats of it + the PMC passes
 #             (tools/pmc_run.sh) + cfg5 on one GPU + the ratio-pair batch
 #   cfg5      tools/cfg5_check.py (1B fragments: timing, determinism,
@@ -17,9 +18,11 @@
 #   trace     per-tile phase times of every record pass (RK_NW_TRACE)
 #   shard     sharded parity tests (+ the large sharded digests with ARGS=large)
 #             and the world-1 sharded bench
-#   rehearse  the N > 1 bench line on one GPU: two ranks on device 0 over gloo
-#             host callbacks, the RCCL attempt (RCCL refuses two ranks on one
-#             GPU: value null with the error), the world-1 sharded leg
+#   rehearse  the N > 1 bench line on one GPU: 2 and 4 ranks (ARGS) on device 0
+#             over gloo host callbacks, cfg3's one 50M set strong-scaled with
+#             its digest gathered; then the world-1 sharded leg
+#   rehearse_rccl  the same over RCCL (which refuses two ranks on one GPU:
+#             value null with the error)
 #   serial    per-kernel times with every kernel on one stream (RK_ONE_STREAM=1)
 #   pmc5      the PMC passes at cfg5 (one timed step) -> OUTDIR/pmc5
 #   shprof    rocprofv3 --kernel-trace --stats of the world-1 sharded bench
@@ -80,6 +83,9 @@ absplit)  # phase A / B boundary at cfg5 (RK_SPLIT_T builds under tools/mb/s*)
     RK_LIB=tools/mb/$v/librepkiller_amd.so bench ${v}_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
   done
   ;;
+parity)  # the record / generic pipelines against the oracle and the fixtures
+  timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  ;;
 ablib)
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
   for rep in 1 2 3; do
@@ -103,17 +109,21 @@ trace)
   rm -f $O/trace.bin
   ;;
 shard)
-  timeout -k 10 600 python3 -u -m pytest tests/test_sharded.py -x -q --timeout 300 --timeout-method thread > $O/sharded_tests.log 2>&1 || exit 1
+  timeout -k 10 600 python3 -u -m pytest tests/test_sharded.py -x -v --timeout 300 --timeout-method thread > $O/sharded_tests.log 2>&1 || exit 1
   if [ "$1" = large ]; then
     timeout -k 10 900 python3 -u -m pytest tests/test_large_configs.py -x -q -k sharded --timeout 600 --timeout-method thread > $O/large_tests.log 2>&1 || exit 2
   fi
   bench sharded_w1 --mode sharded --steps 20 --warmup 5 --no-cpu || exit 3
   ;;
-rehearse)
-  RK_BENCH_SAME_GPU=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --config cfg2 --comm host --steps 3 --warmup 1 > $O/host2.json 2> $O/host2.err || exit 1
+rehearse)  # ARGS: world sizes (default 2 4); cfg3's one 50M set strong-scaled, parity gathered
+  for W in ${@:-2 4}; do
+    RK_BENCH_SAME_GPU=1 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $W --master-addr 127.0.0.1 --master-port $((29610 + W)) bench.py --gpus $W --comm host --steps 2 --warmup 1 --sharded-timeout 500 > $O/host$W.json 2> $O/host$W.err || exit 1
+  done
+  bench sharded_w1 --mode sharded --no-cpu --steps 5 --warmup 2 || exit 3
+  ;;
+rehearse_rccl)  # RCCL refuses two ranks on one GPU: value null with the error
   RK_BENCH_SAME_GPU=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --config cfg2 --steps 3 --warmup 1 --sharded-timeout 60 > $O/rccl2.json 2> $O/rccl2.err
   echo "rccl2 exit $?" > $O/rccl2.rc
-  bench sharded_w1 --mode sharded --no-cpu --steps 5 --warmup 2 || exit 3
   ;;
 serial)
   RK_ONE_STREAM=1 bench cfg3 --no-cpu || exit 1
