@@ -217,6 +217,12 @@ typedef struct {
                                 or a slice of >= 2^30 rows, or RK_SHARD_GENERIC=1) */
   uint32_t order_split;      /* 1: this rank's slice took the two-stage order sort
                                 (coarse passes + per-segment LDS sort) */
+  uint32_t gathers;          /* all-gathers of host metadata this call (agreement points
+                                included) */
+  uint32_t exchanges;        /* all-to-alls of device blocks this call */
+  uint32_t host_syncs;       /* host waits for the device stream (readbacks) this call */
+  uint32_t agree_skipped;    /* receive-buffer agreements skipped: every rank's buffer
+                                was already large enough */
 } rk_shard_stats;
 
 /* in_dev: this rank's block of input rows (device SoA, FILE order); blocks are

@@ -123,7 +123,9 @@ class ShardStats(ctypes.Structure):
                 ("ms_ingress", ctypes.c_double), ("ms_x", ctypes.c_double),
                 ("ms_y", ctypes.c_double), ("ms_roots", ctypes.c_double),
                 ("ms_members", ctypes.c_double), ("generic_driver", ctypes.c_uint32),
-                ("order_split", ctypes.c_uint32)]
+                ("order_split", ctypes.c_uint32), ("gathers", ctypes.c_uint32),
+                ("exchanges", ctypes.c_uint32), ("host_syncs", ctypes.c_uint32),
+                ("agree_skipped", ctypes.c_uint32)]
 
 
 class SynthParams(ctypes.Structure):

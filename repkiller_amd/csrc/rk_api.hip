@@ -86,6 +86,7 @@ void collect_kernel_timing(rk_ctx *ctx) {
 }
 
 int readback(rk_ctx *ctx, const uint32_t *dev, uint32_t count) {
+  ++ctx->readbacks;
   HIPCHK(ctx, hipMemcpyAsync(ctx->host, dev, count * sizeof(uint32_t), hipMemcpyDeviceToHost,
                              ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));

@@ -26,6 +26,7 @@ struct rk_pool {
 struct rk_ctx {
   int device = -1;
   bool nw_fell_back = false;  // the last record-pipeline call handed over to the generic one
+  uint64_t readbacks = 0;     // readback() calls over the context's life (host waits)
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;             // Y-axis sort, overlapped with the X sweeps
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

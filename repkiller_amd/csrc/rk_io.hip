@@ -89,6 +89,7 @@ class HostPool {
 namespace {
 
 constexpr int NSLOT = 4;
+constexpr size_t PF_ROWS = 512;  // rows of u64 columns in one 4-KB page
 constexpr size_t SLOT = (size_t)32 << 20;
 
 int io_threads() {
@@ -380,6 +381,17 @@ int io_h2d_rows(rk_ctx *ctx, const rk_frags_soa &in, void *dev) {
       const size_t lo = (size_t)t * share, hi = std::min(cnt, lo + share);
       bool ok = true;
       for (size_t i = lo; i < hi; ++i) {
+        // software prefetch one 4-KB page ahead in each column: the hardware
+        // streamers stop at page boundaries, and page-locked buffers (torch
+        // pin_memory, hipHostMalloc) come in 4-KB pages where pageable ones
+        // are mostly transparent huge pages
+        if ((i & 7) == 0) {
+          const size_t f = a + i + PF_ROWS;
+          __builtin_prefetch(in.x_start + f);
+          __builtin_prefetch(in.y_start + f);
+          __builtin_prefetch(in.length + f);
+          if ((i & 63) == 0) __builtin_prefetch(in.strand + f);
+        }
         const uint64_t x = in.x_start[a + i], y = in.y_start[a + i], L = in.length[a + i];
         ok &= L < (1ull << 24) && y < (1ull << 35) && x < (1ull << 36);
         const uint32_t s = in.strand[a + i] != 'f' ? 1u : 0u;

@@ -1261,6 +1261,88 @@ __device__ uint32_t wave_find_begin(const Axis &ax, uint32_t before, uint32_t ke
 // most one can); the first sweep's window kernel sets the flags, so no
 // shared list (and no hot atomic counter) is needed.  One wavefront takes 64
 // windows and walks their long runs in turn.
+// Compacts the own-run list [0, nl) in place, dropping every ACTIVE entry
+// whose packed record equals that of a newer ACTIVE entry -- a later list
+// entry or an ACTIVE lane of the current chunk (act, rec: this lane) --; an
+// ACTIVE lane of the chunk with a newer twin in the chunk clears *keep.
+// Returns the new list length (the order of the survivors is kept).
+__device__ int list_dedup(LongLds &L, int nl, uint32_t lane, bool act, uint2 rec, bool &keep) {
+  constexpr int LS = LCAP / 64;  // list entries per lane: k = lane + 64 s
+  bool lk[LS];
+  uint2 lp[LS];
+  uint32_t lq[LS], le[LS];
+  uint8_t ls[LS];
+#pragma unroll
+  for (int s = 0; s < LS; ++s) {
+    const int k = (int)lane + 64 * s;
+    lk[s] = k < nl;
+    lp[s] = lk[s] ? L.lpk[k] : make_uint2(0, 0);
+    lq[s] = lk[s] ? L.lpos[k] : 0u;
+    le[s] = lk[s] ? L.lent[k] : 0u;
+    ls[s] = lk[s] ? L.lst[k] : (uint8_t)ST_HIT;
+  }
+  // one round per distinct record among the newest entries: the chunk's ACTIVE
+  // lanes, newest first, then the list's ACTIVE entries newest first
+  uint64_t a = __ballot(act);
+  while (a) {
+    const int v = 63 - __clzll(a);
+    const uint32_t px = (uint32_t)__builtin_amdgcn_readlane((int)rec.x, v),
+                   py = (uint32_t)__builtin_amdgcn_readlane((int)rec.y, v);
+    const bool same = act && rec.x == px && rec.y == py;
+    if (same && (int)lane != v) keep = false;  // (lanes below v: older)
+#pragma unroll
+    for (int s = 0; s < LS; ++s)
+      lk[s] = lk[s] && !(ls[s] == ST_ACTIVE && lp[s].x == px && lp[s].y == py);
+    a &= ~__ballot(same);
+  }
+#pragma unroll
+  for (int s = LS - 1; s >= 0; --s) {
+    uint64_t b = __ballot(lk[s] && ls[s] == ST_ACTIVE);
+    while (b) {
+      const int v = 63 - __clzll(b);
+      const uint32_t px = (uint32_t)__builtin_amdgcn_readlane((int)lp[s].x, v),
+                     py = (uint32_t)__builtin_amdgcn_readlane((int)lp[s].y, v);
+      // older list entries with the same record (list position v + 64 s)
+#pragma unroll
+      for (int s2 = 0; s2 < LS; ++s2) {
+        const int k2 = (int)lane + 64 * s2, kv = v + 64 * s;
+        lk[s2] = lk[s2] && !(k2 < kv && ls[s2] == ST_ACTIVE && lp[s2].x == px && lp[s2].y == py);
+      }
+      b &= ~__ballot(lk[s] && ls[s] == ST_ACTIVE && lp[s].x == px && lp[s].y == py);
+      b &= (v > 0 ? (1ull << v) - 1ull : 0ull);  // (continue below v)
+    }
+  }
+  uint64_t lb[LS];
+  int nk = 0;
+#pragma unroll
+  for (int s = 0; s < LS; ++s) lb[s] = __ballot(lk[s]), nk += __popcll(lb[s]);
+  wave_sync_lds();  // every list read is done
+  int base = 0;
+#pragma unroll
+  for (int s = 0; s < LS; ++s) {
+    if (lk[s]) {
+      const int at = base + below_count(lb[s]);
+      L.lpk[at] = lp[s];
+      L.lpos[at] = lq[s];
+      L.lent[at] = le[s];
+      L.lst[at] = ls[s];
+    }
+    base += __popcll(lb[s]);
+  }
+  return nk;
+}
+
+#ifdef RK_SWEEP_PROF
+// measurement build only: the long-run walk's counters (first sweep) --
+// [0] runs, [1] entries, [2] chunks, [3] open lanes, [4] list length at the
+// chunks, [5] runs handed to the entry walk, [6] entries walked there, [7]
+// cycles in chunks, [8] cycles in the entry walk, [9] list entries dropped
+// as duplicates
+__device__ unsigned long long g_long_prof[16];
+#define LP_ADD(slot, v) do { if (lane == 0) atomicAdd(&g_long_prof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define LP_ADD(slot, v)
+#endif
 __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lflag,
                                                       uint32_t nwin, uint8_t *rpend,
                                                       uint32_t *counters, uint32_t *work) {
@@ -1284,6 +1366,39 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
       const uint32_t key = ax.key[beg];
       const uint32_t end = wave_find_end(ax, beg + LONG_RUN, key, lane);
       if (work && lane == 0) atomicAdd(work, end - beg);  // entries walked (kernel timer)
+      LP_ADD(0, 1);
+      LP_ADD(1, end - beg);
+#ifdef RK_SWEEP_PROF
+      const uint64_t lp_t0 = __builtin_amdgcn_s_memtime();
+#endif
+      // the run's open entries (UNKNOWN / HIT_PENDING): first fo, last lo.
+      // Entries after lo are decided and no later query reads them, entries
+      // before fo only join the list; a run without one is done (repeat-rich
+      // sets: most Y runs -- their X hits sit ACTIVE in the Y lists -- and
+      // many X runs).  Four states per lane and load round
+      uint32_t fo = NONE, lo = 0;
+      for (uint32_t c = beg; c < end; c += 256) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t p = c + 4 * lane + j;
+          const uint8_t sp = p < end ? load_state(&ax.state[p]) : (uint8_t)ST_HIT;
+          bits |= (uint32_t)(sp == ST_UNKNOWN || sp == ST_HIT_PENDING) << j;
+        }
+        const uint64_t any = __ballot(bits != 0);
+        if (any) {
+          const int lf = __builtin_ctzll(any), ll = 63 - __clzll(any);
+          const uint32_t bf = (uint32_t)__builtin_amdgcn_readlane((int)bits, lf),
+                         bl = (uint32_t)__builtin_amdgcn_readlane((int)bits, ll);
+          if (fo == NONE) fo = c + 4 * lf + __builtin_ctz(bf);
+          lo = c + 4 * ll + 31 - __clz(bl);
+        }
+      }
+      if (fo == NONE) {
+        LP_ADD(10, 1);
+        if (lane == 0) rpend[beg] = 0;
+        continue;
+      }
       uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
       const bool has_lo = beg > 0 && ax.key[beg - 1] == key - 1;
       if (has_lo) lo_e = beg, lo_b = wave_find_begin(ax, beg, key - 1, lane);
@@ -1307,15 +1422,57 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
         if ((int)lane < nn0) ns0 = load_state(&ax.state[L.npos[0][lane]]);
         if ((int)lane < nn1) ns1 = load_state(&ax.state[L.npos[1][lane]]);
       };
+      // this chunk's ACTIVE / UNKNOWN entries join the list: false when it
+      // would overflow even without its redundant entries
+      auto join_list = [&](bool keep, bool act, uint2 me, uint32_t t, uint32_t i, uint8_t st) {
+        uint64_t kb = __ballot(keep);
+        if (nl + __popcll(kb) > LCAP) {
+          // First drop the redundant entries.  An ACTIVE entry stays ACTIVE,
+          // so every OLDER ACTIVE entry with the same packed record {centre,
+          // length} -- the same match and the same deviation for every later
+          // query, later in scan order (newest first) -- can neither win (the
+          // first strict maximum) nor decide anything the newer one does not.
+          // Repeat-family runs hold a few dozen distinct records over hundreds
+          // of entries.  RK_LDEDUP=0: off
+          int nk = nl;
+#ifndef RK_LDEDUP
+#define RK_LDEDUP 1
+#endif
+          if (RK_LDEDUP) nk = list_dedup(L, nl, lane, act, me, keep);
+          kb = __ballot(keep);
+          LP_ADD(9, nl - nk);
+          nl = nk;
+          if (nl + __popcll(kb) > LCAP) return false;
+        }
+        wave_sync_lds();  // the list reads of this chunk are done
+        if (keep) {
+          const int at = nl + below_count(kb);
+          L.lpk[at] = me;
+          L.lpos[at] = t;
+          L.lent[at] = i;
+          L.lst[at] = st;
+        }
+        nl += __popcll(kb);
+        return true;
+      };
       fetch(beg);
-      for (; cb < end; cb += 64) {
+      for (; cb <= lo; cb += 64) {
         const uint32_t t = cb + lane;
         const bool in = t < end;
         const uint2 me = nme;
         const uint32_t i = ni;
         uint8_t st = nst;
         const uint8_t nd = nnd, s0 = ns0, s1 = ns1;
-        if (cb + 64 < end) fetch(cb + 64);
+        if (cb + 64 <= lo) fetch(cb + 64);
+        if (cb + 64 <= fo) {  // no open entry here: the ACTIVE ones only join the list
+          LP_ADD(11, 1);
+          const bool act = in && st == ST_ACTIVE;
+          if (!join_list(act, act, me, t, i, st)) {
+            cb += 64;
+            break;
+          }
+          continue;
+        }
         wave_sync_lds();  // the previous chunk's LDS reads are done
         L.cpk[lane] = me;
         L.cent[lane] = i;
@@ -1324,6 +1481,12 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
         wave_sync_lds();
         const uint8_t st0 = st;
         const bool open = in && (st == ST_UNKNOWN || st == ST_HIT_PENDING);
+        LP_ADD(2, 1);
+#ifdef RK_SWEEP_PROF
+        const uint32_t nopen = (uint32_t)__popcll(__ballot(open));  // (outside the lane-0 branch)
+        LP_ADD(3, nopen);
+#endif
+        LP_ADD(4, nl);
         uint64_t rown = 0;
         Scan fl{0.0, NONE, 0, false, false}, fn{0.0, NONE, 0, false, false};
         Q32 q{};
@@ -1409,25 +1572,25 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
           store_state(&ax.state[t], st);
         }
         // this chunk's ACTIVE / UNKNOWN entries join the list
-        const bool keep = in && (st == ST_ACTIVE || st == ST_UNKNOWN);
-        const uint64_t kb = __ballot(keep);
-        if (nl + __popcll(kb) > LCAP) {
+        if (!join_list(in && (st == ST_ACTIVE || st == ST_UNKNOWN), in && st == ST_ACTIVE, me, t, i,
+                       st)) {
           cb += 64;
           break;
         }
-        wave_sync_lds();  // the list reads of this chunk are done
-        if (keep) {
-          const int at = nl + below_count(kb);
-          L.lpk[at] = me;
-          L.lpos[at] = t;
-          L.lent[at] = i;
-          L.lst[at] = st;
-        }
-        nl += __popcll(kb);
       }
-      if (cb < end) {  // own list overflow: the rest entry by entry
+#ifdef RK_SWEEP_PROF
+      const uint64_t lp_t1 = __builtin_amdgcn_s_memtime();
+      LP_ADD(7, lp_t1 - lp_t0);
+#endif
+      if (cb <= lo) {  // own list overflow: the rest (up to the last open entry) one by one
+        LP_ADD(5, 1);
+        LP_ADD(6, lo + 1 - cb);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        pending |= walk_entries32(ax, beg, cb, end, has_lo, lo_b, lo_e, has_hi, hi_b, hi_e, lane);
+        pending |= walk_entries32(ax, beg, cb, lo + 1, has_lo, lo_b, lo_e, has_hi, hi_b, hi_e,
+                                  lane);
+#ifdef RK_SWEEP_PROF
+        LP_ADD(8, __builtin_amdgcn_s_memtime() - lp_t1);
+#endif
       }
       const bool pend = __ballot(pending) != 0;
       if (lane == 0) {
@@ -1584,6 +1747,21 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<const uint8_t *>(rl.big), rl.nwin,
                                          rpend, counters, work);
     kt_end_units(st, KID_SWEEP_LONG, 18.0);
+#ifdef RK_SWEEP_PROF
+    {  // every sweep (first=1: the first of the axis)
+      unsigned long long h[16];
+      (void)hipStreamSynchronize(st);
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_long_prof), sizeof h);
+      fprintf(stderr, "first=%d ", (int)first);
+      const double c = h[2] ? (double)h[2] : 1.0;
+      fprintf(stderr, "LONGPROF m=%u runs=%llu entries=%llu chunks=%llu open/chunk %.2f list/chunk %.1f overflow runs=%llu walked=%llu | Mcyc chunks %.1f walk %.1f | dedup drops=%llu | runs without open entries %llu, list-only chunks %llu\n",
+              ax.m, h[0], h[1], h[2], h[3] / c, h[4] / c, h[5], h[6], h[7] / 1e6, h[8] / 1e6, h[9],
+              h[10], h[11]);
+      void *p = nullptr;
+      (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_long_prof));
+      (void)hipMemsetAsync(p, 0, sizeof h, st);
+    }
+#endif
   } else if (rl.nbig) {
     kt_begin(st, KID_SWEEP_WAVE);
     k_sweep_wave<<<grid_for(rl.nbig, 4, 2048), 256, 0, st>>>(ax, rl.big, rl.nbig, rpend,

@@ -651,7 +651,7 @@ struct PartPlan {
 
 // The driver's all-gather message (see Shard::allgather): a 16-B header whose
 // first word is the sender's status, then up to GMAX payload bytes.
-constexpr size_t GMAX = NBINS * 4, GHDR = 16;
+constexpr size_t GMAX = NBINS * 4 + 64, GHDR = 16;  // a histogram + a few words
 constexpr int STATUS_COMM_FAILED = 0x7fffffff;
 int status_message(rk_comm *comm, hipStream_t st, int32_t status, const void *mine, void *all,
                    size_t bytes, uint32_t *who, std::string *err, std::vector<char> &snd,
@@ -690,6 +690,11 @@ struct Shard {
                             // [4] long-run count, [6] wide keys, [64..128) sweep
                             // counters, [128..161) partition totals
   uint64_t bytes_sent = 0;
+  // elements every rank received in the last exchange (known to every rank
+  // from that exchange's count all-gather: no further collective needed)
+  uint64_t last_recv[MAXP] = {};
+  uint32_t n_gathers = 0, n_a2a = 0, n_syncs = 0, n_agree_skipped = 0;  // (shard stats)
+  uint64_t readbacks0 = 0;  // ctx->readbacks at the call's start
 
   template <class T>
   T *take(int slot, size_t count) {
@@ -737,6 +742,7 @@ struct Shard {
   int status_gather(int32_t status, const void *mine, void *all, size_t bytes) {
     uint32_t who = 0;
     std::string cerr;
+    ++n_gathers;
     const int first = status_message(comm, st, status, mine, all, bytes, &who, &cerr, gsend,
                                      grecv);
     if (first == STATUS_COMM_FAILED) {
@@ -779,6 +785,7 @@ struct Shard {
   std::vector<uint32_t> d2h(const uint32_t *dev, size_t count) {
     std::vector<uint32_t> h(count);
     if (count) {
+      ++n_syncs;
       hip(hipMemcpyAsync(h.data(), dev, count * 4, hipMemcpyDeviceToHost, st), "d2h");
       hip(hipStreamSynchronize(st), "d2h sync");
     }
@@ -856,6 +863,7 @@ struct Shard {
     size_t i = 0;
     for (const uint32_t *d : src)
       hip(hipMemcpyAsync(&h[i++], d, 4, hipMemcpyDeviceToHost, st), "d2h");
+    ++n_syncs;
     hip(hipStreamSynchronize(st), "d2h sync");
     return h;
   }
@@ -880,26 +888,48 @@ struct Shard {
   T *exchange(const void *send, const PartPlan &pp, int recv_slot, uint32_t *nrecv,
               uint64_t *from = nullptr) {
     const size_t esz = sizeof(T);
-    uint64_t sb[MAXP], rb[MAXP];
-    for (uint32_t q = 0; q < P; ++q) sb[q] = pp.cnt[q] * esz;
-    std::vector<uint64_t> all((size_t)P * P);
-    allgather(sb, all.data(), P * sizeof(uint64_t));
+    // per destination the bytes sent, then this rank's receive-slot capacity
+    const uint32_t W = P + 1;
+    uint64_t msg[MAXP + 1], sb[MAXP], rb[MAXP];
+    for (uint32_t q = 0; q < P; ++q) sb[q] = msg[q] = pp.cnt[q] * esz;
+    {
+      const rk_pool &pl = ctx->pool;
+      msg[P] = (size_t)recv_slot < pl.cap.size() ? (uint64_t)pl.cap[recv_slot] : 0ull;
+    }
+    std::vector<uint64_t> all((size_t)P * W);
+    allgather(msg, all.data(), W * sizeof(uint64_t));
     uint64_t tot = 0;
-    for (uint32_t q = 0; q < P; ++q) rb[q] = all[(size_t)q * P + me], tot += rb[q];
-    if (tot / esz >= 0xFFFFFFFFull) {
+    for (uint32_t q = 0; q < P; ++q) rb[q] = all[(size_t)q * W + me], tot += rb[q];
+    // every rank's receive total against its capacity -- the same data, so
+    // the same decisions, on every rank
+    bool too_many = false, grows = false;
+    for (uint32_t r = 0; r < P; ++r) {
+      uint64_t need = 0;
+      for (uint32_t q = 0; q < P; ++q) need += all[(size_t)q * W + r];
+      last_recv[r] = need / esz;
+      too_many |= need / esz >= 0xFFFFFFFFull;
+      grows |= align_up((size_t)(need / esz + 1) * esz + 16) > all[(size_t)r * W + P];
+    }
+    if (too_many) {
       ctx->err = "a rank would receive more than 2^32-1 records";
       throw RK_E_TOO_MANY;
     }
     // the receive buffer (its size depends on the other ranks' data: the
     // allocation most likely to fail under skew) is agreed before data moves
+    // -- unless no rank has to allocate (a repeated call), when none can fail
     T *recv = nullptr;
-    int rc = RK_OK;
-    try {
-      recv = take<T>(recv_slot, tot / esz + 1);
-    } catch (int code) {
-      rc = code;
+    if (grows) {
+      int rc = RK_OK;
+      try {
+        recv = take<T>(recv_slot, tot / esz + 1);
+      } catch (int code) {
+        rc = code;
+      }
+      agree(rc);
+    } else {
+      recv = take<T>(recv_slot, tot / esz + 1);  // (no allocation)
+      ++n_agree_skipped;
     }
-    agree(rc);
     run_a2a(send, sb, recv, rb);
     *nrecv = (uint32_t)(tot / esz);
     if (from)
@@ -912,6 +942,7 @@ struct Shard {
     double moved = 0;
     for (uint32_t q = 0; q < P; ++q) moved += (double)sb[q] + (double)rb[q];
     kt_begin(st, KID_EXCHANGE);
+    ++n_a2a;
     const int rc = comm->alltoallv(send, sb, recv, rb, st);
     kt_end(st, KID_EXCHANGE, moved);  // bytes read + written (device time of the a2a)
     if (rc) {
@@ -921,6 +952,15 @@ struct Shard {
     }
   }
 
+  // a bound on every rank's last received count, checked by every rank on
+  // the same data (last_recv): all continue or all fail, no collective
+  void check_recv_below(uint64_t lim, int code, const char *what) {
+    for (uint32_t q = 0; q < P; ++q)
+      if (last_recv[q] >= lim) {
+        ctx->err = what;
+        throw code;
+      }
+  }
   // device error bits agreed by every rank
   void agree_errors() { agree_error_bits(read1(ctrl)); }
   void agree_error_bits(uint32_t bits) {
@@ -971,20 +1011,38 @@ Bounds split_bounds(const std::vector<uint64_t> &hist, uint32_t shift, uint64_t 
   return B;
 }
 
+// The global histogram of op's bins over every rank's n elements.  words: up
+// to 16 device words read back with this rank's histogram and gathered in the
+// same message (one readback, one all-gather); *gathered = every rank's words,
+// rank-major
 template <class Op>
-std::vector<uint64_t> global_hist(Shard &S, const Op &op, uint32_t n) {
+std::vector<uint64_t> global_hist(Shard &S, const Op &op, uint32_t n,
+                                  std::initializer_list<const uint32_t *> words = {},
+                                  std::vector<uint32_t> *gathered = nullptr) {
   uint32_t *h = S.take<uint32_t>(SL_HIST, NBINS);
   S.zero(h, NBINS * 4);
   if (n) {
     k_hist<<<grid_for(n, 256, 512), 256, 0, S.st>>>(op, n, h);
     S.launched("k_hist");
   }
-  std::vector<uint32_t> mine = S.d2h(h, NBINS);
-  std::vector<uint32_t> all((size_t)S.P * NBINS);
-  S.allgather(mine.data(), all.data(), NBINS * 4);
+  const size_t K = words.size(), W = NBINS + K;
+  std::vector<uint32_t> mine(W);
+  S.hip(hipMemcpyAsync(mine.data(), h, NBINS * 4, hipMemcpyDeviceToHost, S.st), "d2h");
+  size_t i = NBINS;
+  for (const uint32_t *d : words)
+    S.hip(hipMemcpyAsync(&mine[i++], d, 4, hipMemcpyDeviceToHost, S.st), "d2h");
+  ++S.n_syncs;
+  S.hip(hipStreamSynchronize(S.st), "d2h sync");
+  std::vector<uint32_t> all((size_t)S.P * W);
+  S.allgather(mine.data(), all.data(), W * 4);
   std::vector<uint64_t> g(NBINS, 0);
   for (uint32_t q = 0; q < S.P; ++q)
-    for (uint32_t b = 0; b < NBINS; ++b) g[b] += all[(size_t)q * NBINS + b];
+    for (uint32_t b = 0; b < NBINS; ++b) g[b] += all[(size_t)q * W + b];
+  if (gathered) {
+    gathered->resize((size_t)S.P * K);
+    for (uint32_t q = 0; q < S.P; ++q)
+      for (size_t k = 0; k < K; ++k) (*gathered)[q * K + k] = all[(size_t)q * W + NBINS + k];
+  }
   return g;
 }
 
@@ -1176,23 +1234,28 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
     exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), S.st);
   }
   // the error bits, the root count and the cross-slice link flag: one readback
-  uint32_t nroots = 0, xlink = 0;
+  uint32_t nroots = 0, xlink = 0, ebits = 0;
   if (m) {
     const std::vector<uint32_t> w = S.d2h_words({S.ctrl, lrank + m, S.ctrl + 23});
-    S.agree_error_bits(w[0]);
+    ebits = w[0];
     nroots = w[1];
     xlink = w[2];
   } else {
-    S.agree_errors();
+    ebits = S.read1(S.ctrl);
   }
-  // root count (low 32 bits) and whether this rank has a cross-slice link
-  std::vector<uint64_t> rall = S.gather1<uint64_t>(nroots | (uint64_t)xlink << 32);
+  // the error bits, the root count and whether this rank has a cross-slice
+  // link: one all-gather
   uint64_t goff = 0, Gtot = 0;
   bool links = false;
-  for (uint32_t q = 0; q < P; ++q) {
-    const uint64_t r = rall[q] & 0xFFFFFFFFull;
-    Gtot += r, goff += q < me ? r : 0;
-    links |= (rall[q] >> 32) != 0;
+  {
+    const std::vector<uint3> rall = S.gather1<uint3>(make_uint3(ebits, nroots, xlink));
+    uint32_t anyerr = 0;
+    for (uint32_t q = 0; q < P; ++q) {
+      anyerr |= rall[q].x;
+      links |= rall[q].z != 0;
+      Gtot += rall[q].y, goff += q < me ? rall[q].y : 0;
+    }
+    S.check(err_status(ctx, anyerr & ~(uint32_t)ERRB_WIDE_LENGTH));
   }
   if (!links) {  // every chain ends in its own slice: no label rounds
     if (m) {
@@ -1271,6 +1334,10 @@ void finish_stats(Shard &S, uint32_t nl, const rk_shard_result *out,
   rk_shard_stats &ss = ctx->shard_stats;
   if (ctx->profiling) collect_kernel_timing(ctx);
   ss.bytes_sent = S.bytes_sent;
+  ss.gathers = S.n_gathers;
+  ss.exchanges = S.n_a2a;
+  ss.host_syncs = S.n_syncs + (uint32_t)(ctx->readbacks - S.readbacks0);
+  ss.agree_skipped = S.n_agree_skipped;
   ss.ms_total = ms_since(t0);
   ctx->stats = rk_stats{};
   ctx->stats.n_in = nl;
@@ -1768,6 +1835,7 @@ int classify_sharded(rk_ctx *ctx, rk_comm *comm, const rk_frags_soa *in, const r
     if (!rc) rc = RK_E_HIP;
   }
   Shard S{ctx, comm, ctx->stream, ctx->stream2, (uint32_t)comm->size, (uint32_t)comm->rank};
+  S.readbacks0 = ctx->readbacks;
   try {
     return classify_sharded_impl(S, in, prm, lead_in, out, rc);
   } catch (int code) {

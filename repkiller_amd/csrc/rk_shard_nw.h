@@ -352,6 +352,7 @@ T *exchange_nw(Shard &S, const T *send, const PartPlan &pp, int recv_slot, uint3
   if (S.P == 1) {
     S.agree(RK_OK);  // the same collective sequence as with peers
     *nrecv = (uint32_t)pp.total;
+    S.last_recv[0] = pp.total;
     if (from) from[0] = pp.total;
     return const_cast<T *>(send);
   }
@@ -403,23 +404,33 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     kt_end(st, KID_SH_ROWKEYS, 25.0 * nl);
     S.launched("k_sh_rows");
   }
-  // the error bits (ctrl[0]), the pack flags (ctrl[20..21]) and the kept
-  // count (ctrl[25]) in one readback
-  const std::vector<uint32_t> flags = S.d2h(S.ctrl, 26);
-  S.agree_error_bits(flags[0]);
-  uint32_t nopack = 0, maxlen = 0;
-  for (uint32_t v : S.gather1<uint32_t>(flags[20] | (flags[21] << 1)))
-    nopack |= v & 1u, maxlen = (v >> 1) > maxlen ? (v >> 1) : maxlen;
-  if (nopack) return RK_SHARD_FALLBACK;
+  // the error bits (ctrl[0]), the pack flags (ctrl[20..21]), the kept count
+  // (ctrl[25]) and the slice histogram in one readback, and the first two with
+  // the histogram in one all-gather
+  std::vector<uint32_t> flags(26);
+  const uint32_t MW = 2 + (P > 1 ? NBINS : 0);  // message words
+  std::vector<uint32_t> msg(MW);
+  S.hip(hipMemcpyAsync(flags.data(), S.ctrl, 26 * 4, hipMemcpyDeviceToHost, st), "d2h");
+  if (P > 1) S.hip(hipMemcpyAsync(msg.data() + 2, hist, NBINS * 4, hipMemcpyDeviceToHost, st), "d2h");
+  ++S.n_syncs;
+  S.hip(hipStreamSynchronize(st), "d2h sync");
+  msg[0] = flags[0];
+  msg[1] = flags[20] | (flags[21] << 1);
+  std::vector<uint32_t> allm((size_t)P * MW);
+  S.allgather(msg.data(), allm.data(), MW * 4);
+  uint32_t anyerr = 0, nopack = 0, maxlen = 0;
   std::vector<uint64_t> gh(NBINS, 0);
-  std::vector<uint32_t> mine;
-  if (P > 1) {
-    std::vector<uint32_t> all((size_t)P * NBINS);
-    mine = S.d2h(hist, NBINS);
-    S.allgather(mine.data(), all.data(), NBINS * 4);
-    for (uint32_t q = 0; q < P; ++q)
-      for (uint32_t b = 0; b < NBINS; ++b) gh[b] += all[(size_t)q * NBINS + b];
+  for (uint32_t q = 0; q < P; ++q) {
+    const uint32_t *mq = allm.data() + (size_t)q * MW;
+    anyerr |= mq[0];
+    nopack |= mq[1] & 1u;
+    maxlen = (mq[1] >> 1) > maxlen ? (mq[1] >> 1) : maxlen;
+    if (P > 1)
+      for (uint32_t b = 0; b < NBINS; ++b) gh[b] += mq[2 + b];
   }
+  S.check(err_status(ctx, anyerr & ~(uint32_t)ERRB_WIDE_LENGTH));
+  if (nopack) return RK_SHARD_FALLBACK;
+  const uint32_t *mine = msg.data() + 2;  // this rank's own bins (P > 1)
   const Bounds slice_keys = split_bounds(gh, shift, drop, P);
   // the one-sweep passes' status words carry a 30-bit count (SW_VAL,
   // rk_onesweep.h), as the single-device record pipeline's bound n < 2^30
@@ -451,7 +462,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   S.emit(rop, pp);
   uint32_t m = 0;
   const uint4 *rin = exchange_nw<uint4>(S, rop.out, pp, SN_RIN, &m);
-  std::vector<uint64_t> mall = S.gather1<uint64_t>(m);
+  // every rank's slice size: known from the exchange's count all-gather
+  std::vector<uint64_t> mall(S.last_recv, S.last_recv + P);
   uint64_t poff64 = 0, M = 0;
   for (uint32_t q = 0; q < P; ++q) M += mall[q], poff64 += q < me ? mall[q] : 0;
   const uint32_t poff = (uint32_t)poff64;
@@ -536,8 +548,9 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   uint32_t ny = 0;
   const uint3 *yr = exchange_nw<uint3>(S, y_self ? yop.yrec : yop.out, ypp, SN_YR, &ny);
   ss.y_entries = ny;
-  // the Y ranges (+ halos) received: the same 30-bit bound on every rank's sort
-  S.agree(ny >= (1u << 30) ? (int)RK_E_TOO_MANY : (int)RK_OK);
+  // the Y ranges (+ halos) received: the same 30-bit bound on every rank's
+  // sort (every rank knows every rank's count from the exchange)
+  S.check_recv_below(1u << 30, RK_E_TOO_MANY, "a Y range of 2^30 or more records");
   const uint64_t ylo = yb.b[me], yhi = yb.b[me + 1];
   uint8_t *ycode = S.take<uint8_t>(SL_YCODE, ny + 1);
   uint8_t *ystate = S.take<uint8_t>(SL_YSTATE, ny + 1);
@@ -814,14 +827,19 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   // ---- 9: members -> gid-range owners; exact in-group order; emit
   const auto tm = std::chrono::steady_clock::now();
   bool narrow = true;  // every sort key fits 32 bits (the X-chunk kernel's flag)
-  for (uint32_t w : S.gather1<uint32_t>(S.read1(S.ctrl + 6))) narrow &= w == 0;
   const uint32_t mx = Gfin + m;
   const uint2 *erk = reinterpret_cast<const uint2 *>(S.take<uint4>(SN_EREC, (size_t)mx * 3 / 4 + 2));
   MemOpNw mop{gid_own, erk + Gfin, reinterpret_cast<const uint32_t *>(erk + mx) + Gfin,
-              {}, bin_shift(Gtot), narrow, nullptr};
+              {}, bin_shift(Gtot), true, nullptr};
   (void)hfin;
-  const Bounds gb = split_bounds(P > 1 ? global_hist(S, mop, m) : std::vector<uint64_t>(NBINS, 0),
-                                 mop.shift, Gtot, P);
+  // the gid histogram and the wide-key flags in one readback and one all-gather
+  std::vector<uint32_t> wide;
+  std::vector<uint64_t> ghist(NBINS, 0);
+  if (P > 1) ghist = global_hist(S, mop, m, {S.ctrl + 6}, &wide);
+  else wide = S.gather1<uint32_t>(S.read1(S.ctrl + 6));
+  for (uint32_t w : wide) narrow &= w == 0;
+  mop.narrow = narrow;
+  const Bounds gb = split_bounds(ghist, mop.shift, Gtot, P);
   mop.B = gb;
   const size_t esz = narrow ? 12 : 16;
   // one rank: every member stays here and the X chunk's member arrays are
@@ -843,7 +861,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
                  : (const void *)exchange_nw<uint4>(S, (const uint4 *)mop.out, pp, SL_MEM, &mr);
   }
   // the gid range's members: the same 30-bit bound on the member sort
-  S.agree(mr >= (1u << 30) ? (int)RK_E_TOO_MANY : (int)RK_OK);
+  if (m_self) S.last_recv[0] = mr;
+  S.check_recv_below(1u << 30, RK_E_TOO_MANY, "a gid range of 2^30 or more members");
   const uint32_t g0 = (uint32_t)gb.b[me], Gl = (uint32_t)(gb.b[me + 1] - gb.b[me]);
   uint32_t *ogid = S.take<uint32_t>(SL_OGID, mr + 1);
   uint8_t *orep = S.take<uint8_t>(SL_OREP, mr + 1);
@@ -878,7 +897,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     if (g0) k_add_u32<<<grid_for(mr, 256), 256, 0, st>>>(ogid, mr, g0);
     S.launched("member order");
   }
-  std::vector<uint64_t> oall = S.gather1<uint64_t>(mr);
+  // every rank's share of the output: its received members
+  std::vector<uint64_t> oall(S.last_recv, S.last_recv + P);
   uint64_t ooff = 0, otot = 0;
   for (uint32_t q = 0; q < P; ++q) otot += oall[q], ooff += q < me ? oall[q] : 0;
   S.hip(hipStreamSynchronize(st), "final sync");

@@ -7,6 +7,8 @@
 #   suite     smoke() and the whole GPU suite, as the driver runs them
 #   bench     the driver's bench command (cfg3, 20 steps, CPU baseline)
 #   parity    tests/test_gpu_parity.py (both pipelines against the oracle)
+#   check     parity + sharded tests, the cfg5q digests, the cfg5 bench, a
+#             2-rank rehearsal
 #   refresh   bench + rocprofv3 --kernel-trace --stats of it + the PMC passes
 #             (tools/pmc_run.sh) + cfg5 on one GPU + the ratio-pair batch
 #   cfg5      tools/cfg5_check.py (1B fragments: timing, determinism,
@@ -61,6 +63,18 @@ longprof)  # the long-run walk's counters (RK_SWEEP_PROF build under tools/mb/pr
   RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg5 --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 1
   RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg3 --no-cpu --steps 1 --warmup 0 || exit 2
   ;;
+lprof)  # parity + cfg3 bench of the working tree, then the long-run walk's counters at cfg5 with / without the list dedup
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  bench bench --no-cpu --steps 20 --warmup 5 || exit 2
+  RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg5 --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 3
+  RK_LIB=tools/mb/nodedup/librepkiller_amd.so bench long_cfg5_nodedup --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 4
+  ;;
+lcheck)  # the long-run walk: parity (long runs, cfg5q digests), the cfg5 bench, its counters (RK_SWEEP_PROF build)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  timeout -k 10 900 python3 -u -m pytest tests/test_large_configs.py -x -v -k cfg5q --timeout 600 --timeout-method thread > $O/cfg5q.log 2>&1 || exit 2
+  bench bench_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 3
+  RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg5 --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 4
+  ;;
 abcfg5)  # parity, then cfg5 / cfg3 against the HEAD build under tools/mb/base, then the counters
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
   RK_LIB=repkiller_amd/librepkiller_amd.so bench new_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
@@ -85,6 +99,12 @@ absplit)  # phase A / B boundary at cfg5 (RK_SPLIT_T builds under tools/mb/s*)
   ;;
 parity)  # the record / generic pipelines against the oracle and the fixtures
   timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  ;;
+check)  # parity + sharded tests + the cfg5q digests (one device, 8 ranks) + cfg5 bench + 2-rank rehearsal
+  timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_sharded.py -x -v --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  timeout -k 10 900 python3 -u -m pytest tests/test_large_configs.py -x -v -k cfg5q --timeout 600 --timeout-method thread > $O/cfg5q.log 2>&1 || exit 2
+  bench bench_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 3
+  RK_BENCH_SAME_GPU=1 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --comm host --steps 2 --warmup 1 --sharded-timeout 500 > $O/host2.json 2> $O/host2.err || exit 4
   ;;
 ablib)
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1

@@ -17,12 +17,26 @@ import os
 import re
 import sys
 
+# the segment kernel's instantiations by their emit type (bench.py's names)
+SEG_EMIT = {"OrderEmit": "k_seg_fine (order)", "CsrEmit": "k_seg_fine (Y)",
+            "MemberEmit": "k_seg_fine (members)"}
+
+
+def kernel_key(name: str) -> str:
+    m = re.search(r"(k_\w+)", name)
+    nm = m.group(1) if m else name
+    if nm == "k_seg_fine":
+        for emit, key in SEG_EMIT.items():
+            if emit in name:
+                return key
+    return nm
+
+
 def load(d):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for path in glob.glob(os.path.join(d, "p*", "*counter_collection.csv")):
         for r in csv.DictReader(open(path)):
-            m = re.search(r"(k_\w+)", r["Kernel_Name"])
-            nm = m.group(1) if m else r["Kernel_Name"]
+            nm = kernel_key(r["Kernel_Name"])
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
             agg[nm][r["Counter_Name"]].append((float(r["Counter_Value"]), dur))
     return agg
