@@ -406,6 +406,21 @@ __device__ void wave_sort_heap_equal(uint32_t *T, uint32_t n, uint32_t lane) {
   if (lane == 0) T[0] = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)head);
 }
 
+// __make_heap of [0, n) of K/T (global memory) by one block: the calls of
+// one heap level touch disjoint subtrees, deeper levels first
+__device__ void block_make_heap(uint64_t *K, uint32_t *T, uint32_t n) {
+  const uint32_t tid = threadIdx.x;
+  if (n < 2) return;
+  const uint32_t last_parent = (n - 2) / 2;
+  for (int lv = 31 - __clz((int)(last_parent + 1)); lv >= 0; --lv) {
+    const uint32_t a = (1u << lv) - 1;
+    const uint32_t e = min((1u << (lv + 1)) - 2, last_parent);
+    for (uint32_t x = a + tid; x <= e; x += blockDim.x)
+      adjust_heap(GView{K, T, nullptr, nullptr, nullptr}, 0, x, n, K[x], T[x]);
+    __syncthreads();
+  }
+}
+
 // The whole __partial_sort of segment [0, n) of K/T (global memory) by one
 // 256-thread block; its final tags go to out[0..n).
 __device__ void block_heap_sort(uint64_t *K, uint32_t *T, uint32_t n, uint32_t *out, uint64_t *lk,
@@ -420,14 +435,7 @@ __device__ void block_heap_sort(uint64_t *K, uint32_t *T, uint32_t n, uint32_t *
   for (uint32_t x = tid; x < n; x += blockDim.x) neq |= K[x] != K[0];
   const bool equal = __syncthreads_or(neq) == 0;
   {
-    const uint32_t last_parent = (n - 2) / 2;
-    for (int lv = 31 - __clz((int)(last_parent + 1)); lv >= 0; --lv) {
-      const uint32_t a = (1u << lv) - 1;
-      const uint32_t e = min((1u << (lv + 1)) - 2, last_parent);
-      for (uint32_t x = a + tid; x <= e; x += blockDim.x)
-        adjust_heap(GView{K, T, nullptr, nullptr, nullptr}, 0, x, n, K[x], T[x]);
-      __syncthreads();
-    }
+    block_make_heap(K, T, n);
     if (equal) {
       if (tid < 64) wave_sort_heap_equal(T, n, tid);
       __syncthreads();
@@ -1149,6 +1157,348 @@ __global__ void __launch_bounds__(256) k_heap_segments(const uint32_t *heapq_n,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Heap segments with a few distinct keys (2..RANK_MAX): a median-of-three
+// killer whose never-compared members carry a few values.  A pop's path
+// depends on the keys alone, and a pop moves the tags along that path: the
+// root's to `last`, the one at `last` to path slot j, path slots 1..j up one
+// level each.  So instead of replaying the pops with the tags (one pop after
+// another, ~2.7 us each: 285 ms for a 100K heap):
+//  1. k_heap_prep: __make_heap (level-parallel), the segment's distinct keys
+//     (one block-wide minimum per key) and every key's rank (one byte) --
+//     or, with one key, the spine-ring path; with more than RANK_MAX, the
+//     general pops;
+//  2. k_heap_rank_pops: the pops on the ranks alone, one wavefront, the heap
+//     in LDS as far as it fits (one byte per node: 160K nodes), the descent
+//     found HR levels per round as in wave_sort_heap; each pop logs its
+//     direction bits from the root (D levels) and the slot j where the
+//     displaced value lands;
+//  3. the (node, pop) pairs of every pop's written slots p_0..p_j, sorted by
+//     node (stable: by pop within a node);
+//  4. k_heap_trace: every output position independently, backwards through
+//     the pops: the element at node y just before pop t was put there by the
+//     last pop t' < t that wrote y -- from its slot i + 1 when y is its slot
+//     i < j, from its `last` when y is its slot j --, or has been there since
+//     __make_heap when no pop before t wrote y.
+constexpr uint32_t RANK_MAX = 16;  // distinct keys of the rank path (one pass each)
+enum : uint32_t { HM_EQUAL = 1, HM_RANK = 2, HM_GENERAL = 3 };
+
+__global__ void __launch_bounds__(256) k_heap_prep(uint64_t *K, uint32_t *T, uint32_t n,
+                                                  uint8_t *R, uint32_t *mode) {
+  __shared__ unsigned long long vals[RANK_MAX];
+  __shared__ unsigned long long s_min;
+  __shared__ uint32_t s_found;
+  const uint32_t tid = threadIdx.x;
+  block_make_heap(K, T, n);
+  // the distinct keys in ascending order, one block-wide minimum per round
+  uint32_t D = 0;
+  for (;;) {
+    if (tid == 0) s_min = ~0ull, s_found = 0;
+    __syncthreads();
+    const unsigned long long prev = D ? vals[D - 1] : 0ull;
+    unsigned long long mn = ~0ull;
+    bool found = false;
+    for (uint32_t x = tid; x < n; x += blockDim.x) {
+      const unsigned long long k = K[x];
+      if (D == 0 || k > prev) {
+        found = true;
+        mn = k < mn ? k : mn;
+      }
+    }
+    if (found) {
+      atomicMin(&s_min, mn);
+      atomicOr(&s_found, 1u);
+    }
+    __syncthreads();
+    if (!s_found) break;
+    if (D == RANK_MAX) {  // too many distinct keys for the rank path
+      ++D;
+      break;
+    }
+    if (tid == 0) vals[D] = s_min;
+    ++D;
+    __syncthreads();
+  }
+  const uint32_t md = D <= 1 ? HM_EQUAL : D <= RANK_MAX ? HM_RANK : HM_GENERAL;
+  if (md == HM_RANK)
+    for (uint32_t x = tid; x < n; x += blockDim.x) {
+      const unsigned long long k = K[x];
+      uint32_t r = 0;
+      while (vals[r] != k) ++r;
+      R[x] = (uint8_t)r;
+    }
+  if (tid == 0) *mode = md;
+}
+
+// the spine-ring path (one key) and the general pops (more than RANK_MAX keys)
+// of a heap segment after k_heap_prep; each returns at once on the other modes
+__global__ void __launch_bounds__(64) k_heap_equal(uint32_t *T, uint32_t n, uint32_t *out,
+                                                  const uint32_t *mode) {
+  if (*mode != HM_EQUAL) return;
+  const uint32_t lane = threadIdx.x;
+  wave_sort_heap_equal(T, n, lane);
+  wave_sync_global();  // (this wavefront's stores before its loads)
+  for (uint32_t x = lane; x < n; x += 64) out[x] = T[x];
+}
+__global__ void __launch_bounds__(256) k_heap_general(uint64_t *K, uint32_t *T, uint32_t n,
+                                                     uint32_t *out, const uint32_t *mode) {
+  __shared__ uint64_t lk[HTOP];
+  __shared__ uint32_t lt[HTOP];
+  if (*mode != HM_GENERAL) return;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t x = tid; x < n && x < HTOP; x += blockDim.x) lk[x] = K[x], lt[x] = T[x];
+  __syncthreads();
+  if (tid < 64) wave_sort_heap(HeapMem{K, T, lk, lt}, n, tid);
+  __syncthreads();
+  for (uint32_t x = tid; x < n; x += blockDim.x) out[x] = x < HTOP ? lt[x] : T[x];
+}
+
+struct RankMem {  // node x: LDS below RT, else the ranks in global memory
+  uint8_t *lr, *gr;
+  uint32_t RT;
+  __device__ __forceinline__ uint32_t key(uint32_t x) const { return x < RT ? lr[x] : gr[x]; }
+  __device__ __forceinline__ void put(uint32_t x, uint32_t k) const {
+    if (x < RT) lr[x] = (uint8_t)k;
+    else gr[x] = (uint8_t)k;
+  }
+};
+
+// __sort_heap of [0, n) on the ranks alone by one wavefront (wave_sort_heap's
+// descent, no tags): pop t = n - 1 - last logs its direction bits from the
+// root (logb, the first level the highest of D bits) and D | j << 8 (logq)
+__device__ void wave_rank_pops(const RankMem &h, uint32_t n, uint32_t lane, uint32_t *logb,
+                               uint16_t *logq) {
+  for (uint32_t last = n - 1; last > 0; --last) {
+    // (the root leaves for `last`, outside the heap from now on: not stored)
+    const uint32_t vk = h.key(last);
+    const uint32_t len = last;
+    const uint32_t two_lim = (len - 1) / 2;  // hole x has two children iff x < two_lim
+    uint64_t pm0[HRMAX], pm1[HRMAX];
+    uint32_t k0[HRMAX], k1[HRMAX], x0[HRMAX], x1[HRMAX];
+    uint32_t hole = 0, bits = 0, D = 0;
+    int rounds = 0;
+    bool more = true;
+#pragma unroll
+    for (int r = 0; r < HRMAX; ++r) {
+      pm0[r] = pm1[r] = 0;
+      k0[r] = k1[r] = x0[r] = x1[r] = 0;
+      if (!more) continue;
+      ++rounds;
+      uint32_t kk[2], xx[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t c = lane + 64 * s;
+        const int d = 31 - __clz((int)(c + 2));
+        const uint64_t pos = ((uint64_t)hole + 1) * (1ull << d) - 1 + (c + 2 - (1u << d));
+        const bool in = c < HR_NODES && pos < len;
+        xx[s] = in ? (uint32_t)pos : 0u;
+        kk[s] = in ? h.key((uint32_t)pos) : 0u;
+      }
+      uint64_t dir[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t sib = (uint32_t)__shfl_xor((int)kk[s], 1);
+        dir[s] = __ballot((lane & 1) && !(kk[s] < sib));  // ties go right
+      }
+      uint32_t J = 0, x = hole;
+      more = false;
+      for (;;) {
+        if (x >= two_lim) {  // no second child: a lone left child ends the descent
+          if ((len & 1) == 0 && x == (len - 2) / 2) {
+            const uint32_t c = 2 * J;
+            if (c < 64) pm0[r] |= 1ull << c;
+            else pm1[r] |= 1ull << (c - 64);
+            bits <<= 1;
+            ++D;
+          }
+          break;
+        }
+        const uint32_t cr = 2 * J + 1;
+        const bool right = ((cr < 64 ? dir[0] >> cr : dir[1] >> (cr - 64)) & 1ull) != 0;
+        const uint32_t c = right ? cr : cr - 1;
+        if (c < 64) pm0[r] |= 1ull << c;
+        else pm1[r] |= 1ull << (c - 64);
+        bits = bits << 1 | (right ? 1u : 0u);
+        ++D;
+        x = 2 * x + (right ? 2 : 1);
+        if (c >= HR_LAST) {
+          hole = x;
+          more = true;
+          break;
+        }
+        J = c + 1;
+      }
+      k0[r] = kk[0], k1[r] = kk[1];
+      x0[r] = xx[0], x1[r] = xx[1];
+    }
+    // __push_heap: the value rises past the path keys below it (a suffix)
+    uint32_t below = 0;
+#pragma unroll
+    for (int r = 0; r < HRMAX; ++r) {
+      if (r >= rounds) break;
+      below += __popcll(__ballot(((pm0[r] >> lane) & 1) && k0[r] < vk)) +
+               __popcll(__ballot(((pm1[r] >> lane) & 1) && k1[r] < vk));
+    }
+    const uint32_t j = D - below;  // the value's slot is path position j (0: the root)
+    uint32_t before = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < HRMAX; ++r) {
+      if (r >= rounds) break;
+      const bool on0 = (pm0[r] >> lane) & 1, on1 = (pm1[r] >> lane) & 1;
+      const uint32_t p0 = before + __popcll(pm0[r] & lt) + 1;
+      const uint32_t p1 = before + __popcll(pm0[r]) + __popcll(pm1[r] & lt) + 1;
+      if (on0 && p0 <= j) {
+        h.put((x0[r] - 1) / 2, k0[r]);
+        if (p0 == j) h.put(x0[r], vk);
+      }
+      if (on1 && p1 <= j) {
+        h.put((x1[r] - 1) / 2, k1[r]);
+        if (p1 == j) h.put(x1[r], vk);
+      }
+      before += __popcll(pm0[r]) + __popcll(pm1[r]);
+    }
+    if (lane == 0) {
+      if (j == 0) h.put(0, vk);
+      const uint32_t t = n - 1 - last;
+      logb[t] = bits;
+      logq[t] = (uint16_t)(D | j << 8);
+    }
+    wave_sync();  // the next pop reads what this one wrote (in order, one wavefront)
+  }
+}
+
+__global__ void __launch_bounds__(64) k_heap_rank_pops(uint8_t *R, uint32_t n, uint32_t RT,
+                                                      uint32_t *logb, uint16_t *logq,
+                                                      const uint32_t *mode) {
+  extern __shared__ uint8_t lr[];
+  if (*mode != HM_RANK) return;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t x = lane; x < RT; x += 64) lr[x] = R[x];
+  wave_sync();
+  wave_rank_pops(RankMem{lr, R, RT}, n, lane, logb, logq);
+}
+
+__global__ void k_heap_pair_counts(const uint16_t *logq, uint32_t npop, uint32_t *cnt) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < npop + 1; t += gridDim.x * blockDim.x)
+    cnt[t] = t < npop ? (uint32_t)(logq[t] >> 8) + 1u : 0u;
+}
+// the slots p_0..p_j pop t wrote: (node, pop) pairs at off[t]
+__global__ void k_heap_pairs(const uint32_t *logb, const uint16_t *logq, const uint32_t *off,
+                             uint32_t npop, uint32_t *key, uint32_t *val) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < npop; t += gridDim.x * blockDim.x) {
+    const uint32_t b = logb[t], q = logq[t], D = q & 255u, j = q >> 8;
+    uint32_t y = 0;
+    const uint32_t o = off[t];
+    for (uint32_t i = 0;; ++i) {
+      key[o + i] = y;
+      val[o + i] = t;
+      if (i == j) break;
+      y = 2 * y + 1 + ((b >> (D - 1 - i)) & 1u);
+    }
+  }
+}
+// first pair of every node y in [0, n] (the pairs sorted by node)
+__global__ void k_heap_node_starts(const uint32_t *skey, uint32_t P, uint32_t n, uint32_t *noff) {
+  for (uint32_t y = blockIdx.x * blockDim.x + threadIdx.x; y <= n; y += gridDim.x * blockDim.x) {
+    uint32_t a = 0, b = P;
+    while (a < b) {
+      const uint32_t mid = a + (b - a) / 2;
+      if (skey[mid] < y) a = mid + 1;
+      else b = mid;
+    }
+    noff[y] = a;
+  }
+}
+__global__ void k_heap_trace(const uint32_t *sval, const uint32_t *noff, const uint32_t *logb,
+                             const uint16_t *logq, const uint32_t *T, uint32_t n, uint32_t *out) {
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+    uint32_t y = 0, t = n - 1 - x;  // position x is the root just before pop n - 1 - x
+    for (;;) {
+      const uint32_t lo = noff[y], hi = noff[y + 1];
+      uint32_t a = lo, b = hi;  // the first of y's writers at or after t
+      while (a < b) {
+        const uint32_t mid = a + (b - a) / 2;
+        if (sval[mid] < t) a = mid + 1;
+        else b = mid;
+      }
+      if (a == lo) break;  // no pop before t wrote y
+      const uint32_t tp = sval[a - 1];
+      const uint32_t q = logq[tp], D = q & 255u, j = q >> 8;
+      const uint32_t i = 31 - __clz(y + 1);  // y's depth: it is slot i of pop tp
+      y = i < j ? 2 * y + 1 + ((logb[tp] >> (D - 1 - i)) & 1u) : n - 1 - tp;
+      t = tp;
+    }
+    out[x] = T[y];
+  }
+}
+
+// The queued heap segments (their number already read back), one after
+// another: prep, then the path its keys take.  A rare path (only crafted
+// inputs reach libstdc++'s depth limit on 2048+ members): its buffers are
+// stream-ordered allocations of its own, and it waits for the device twice
+// per rank-path segment to size them.
+static void heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint32_t *tag,
+                          uint32_t *otag, uint32_t *host_words, hipStream_t st) {
+  std::vector<HeapSeg> q(nheap);
+  (void)hipMemcpyAsync(q.data(), dq, nheap * sizeof(HeapSeg), hipMemcpyDeviceToHost, st);
+  (void)hipStreamSynchronize(st);
+  uint32_t nmax = 0;
+  for (const HeapSeg &g : q) nmax = g.n > nmax ? g.n : nmax;
+  constexpr uint32_t LDS_MAX = 160 * 1024 - 1024;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void *)k_heap_rank_pops,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+    return true;
+  }();
+  (void)attr;
+  uint8_t *R = nullptr;
+  uint32_t *logb = nullptr, *mode = nullptr, *cnt = nullptr, *off = nullptr, *ssb = nullptr;
+  uint16_t *logq = nullptr;
+  const size_t sscap = scan_blocks((size_t)nmax + 1) + 64;
+  (void)hipMallocAsync((void **)&R, nmax + 16, st);
+  (void)hipMallocAsync((void **)&logb, (size_t)nmax * 4 + 16, st);
+  (void)hipMallocAsync((void **)&logq, (size_t)nmax * 2 + 16, st);
+  (void)hipMallocAsync((void **)&mode, 16, st);
+  (void)hipMallocAsync((void **)&cnt, ((size_t)nmax + 1) * 4 + 16, st);
+  (void)hipMallocAsync((void **)&off, ((size_t)nmax + 1) * 4 + 16, st);
+  (void)hipMallocAsync((void **)&ssb, sscap * 4, st);
+  for (const HeapSeg &g : q) {
+    const size_t o = (size_t)g.b + g.f;
+    uint64_t *K = key + o;
+    uint32_t *T = tag + o, *out = otag + o;
+    const uint32_t n = g.n, RT = n < LDS_MAX ? n : LDS_MAX;
+    k_heap_prep<<<1, 256, 0, st>>>(K, T, n, R, mode);
+    k_heap_equal<<<1, 64, 0, st>>>(T, n, out, mode);
+    k_heap_general<<<1, 256, 0, st>>>(K, T, n, out, mode);
+    k_heap_rank_pops<<<1, 64, RT, st>>>(R, n, RT, logb, logq, mode);
+    (void)hipMemcpyAsync(host_words, mode, 4, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    if (host_words[0] != HM_RANK) continue;
+    const uint32_t npop = n - 1;
+    k_heap_pair_counts<<<grid_for(npop + 1, 256), 256, 0, st>>>(logq, npop, cnt);
+    exclusive_scan_u32(cnt, off, (size_t)npop + 1, ScanScratch{ssb, sscap}, st);
+    (void)hipMemcpyAsync(host_words, off + npop, 4, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    const uint32_t P = host_words[0];
+    const size_t rw = radix_scratch_words(P);
+    uint32_t *pk = nullptr, *pv = nullptr, *sk = nullptr, *sv = nullptr, *tk = nullptr,
+             *tv = nullptr, *rs = nullptr, *noff = nullptr;
+    for (uint32_t **b : {&pk, &pv, &sk, &sv, &tk, &tv})
+      (void)hipMallocAsync((void **)b, (size_t)P * 4 + 16, st);
+    (void)hipMallocAsync((void **)&rs, rw * 4, st);
+    (void)hipMallocAsync((void **)&noff, ((size_t)n + 2) * 4, st);
+    k_heap_pairs<<<grid_for(npop, 256), 256, 0, st>>>(logb, logq, off, npop, pk, pv);
+    radix_sort_pairs(pk, pv, sk, sv, tk, tv, P, bit_length(n), rs, rw, st);
+    k_heap_node_starts<<<grid_for(n + 1, 256), 256, 0, st>>>(sk, P, n, noff);
+    k_heap_trace<<<grid_for(n, 256), 256, 0, st>>>(sv, noff, logb, logq, T, n, out);
+    for (uint32_t *b : {pk, pv, sk, sv, tk, tv, rs, noff}) (void)hipFreeAsync(b, st);
+  }
+  for (void *b : {(void *)R, (void *)logb, (void *)logq, (void *)mode, (void *)cnt, (void *)off,
+                  (void *)ssb})
+    (void)hipFreeAsync(b, st);
+}
+
 // phase B: LDS layout of k_sort_groups_lds with a stack for any depth budget
 __host__ __device__ constexpr size_t seg_lds_bytes(uint32_t cap, size_t key_bytes) {
   return (size_t)cap * (key_bytes + 4 + 2 + 2 + 1) +
@@ -1389,7 +1739,6 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   auto tier_slot = [&](int u) {
     if (timing && g_ktimer->only < 0 && g_ktimer->n > 0) g_ktimer->tier_slot[u] = g_ktimer->n - 1;
   };
-  (void)host_words;
   // fixed grids: every kernel reads its list range on the device
   if (side) {
     (void)hipEventRecord(ev_fork, st);  // the tier lists are ready
@@ -1534,8 +1883,23 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
                                             heapq_n, heapq);
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
+  // the heap segments (libstdc++'s depth-limit fallback on 2048+ members: a
+  // median-of-three killer, never ordinary data): their number back to the
+  // host, which sizes their buffers (RK_HEAP_RANK=0: every segment through
+  // k_heap_segments, the one-block general / spine-ring pops)
+  static const bool heap_rank = [] {
+    const char *e = getenv("RK_HEAP_RANK");
+    return !(e && e[0] == '0');
+  }();
   kt_begin(st, KID_SORT_HEAP);
-  k_heap_segments<<<64, 256, 0, st>>>(heapq_n, heapq, key, tag, otag);
+  if (heap_rank) {
+    (void)hipMemcpyAsync(host_words, heapq_n, 4, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    const uint32_t nheap = host_words[0] < HEAPQ_CAP ? host_words[0] : HEAPQ_CAP;
+    if (nheap) heap_segments(heapq, nheap, key, tag, otag, host_words, st);
+  } else {
+    k_heap_segments<<<64, 256, 0, st>>>(heapq_n, heapq, key, tag, otag);
+  }
   kt_end(st, KID_SORT_HEAP, 0.0);
   kt_begin(st, KID_SORT_SEGS);
   {

@@ -1338,8 +1338,9 @@ __device__ int list_dedup(LongLds &L, int nl, uint32_t lane, bool act, uint2 rec
 // chunks, [5] runs handed to the entry walk, [6] entries walked there, [7]
 // cycles in chunks, [8] cycles in the entry walk, [9] list entries dropped
 // as duplicates
-__device__ unsigned long long g_long_prof[16];
-#define LP_ADD(slot, v) do { if (lane == 0) atomicAdd(&g_long_prof[slot], (unsigned long long)(v)); } while (0)
+__device__ unsigned long long g_long_prof[24];
+// (accumulated per wave in lpacc, flushed once at the end of the kernel)
+#define LP_ADD(slot, v) do { lpacc[slot] += (unsigned long long)(v); } while (0)
 #else
 #define LP_ADD(slot, v)
 #endif
@@ -1350,10 +1351,18 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
   const uint32_t lane = threadIdx.x & 63;
   LongLds &L = s_l[threadIdx.x >> 6];
   const uint32_t ngrp = (nwin + 63) / 64;
+  uint32_t walked = 0;  // (one atomic per wave at the end: 4.6 M same-word atomics per
+                        // launch at cfg5 cost the timed launch ~20 ms)
+#ifdef RK_SWEEP_PROF
+  unsigned long long lpacc[24] = {};
+#endif
   for (uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; gi < ngrp;
        gi += (gridDim.x * blockDim.x) >> 6) {
     uint64_t todo = __ballot(gi * 64 + lane < nwin && lflag[gi * 64 + lane]);
     while (todo) {
+#ifdef RK_SWEEP_PROF
+      const uint64_t lp_tr = __builtin_amdgcn_s_memtime();
+#endif
       const uint32_t w = gi * 64 + (uint32_t)__builtin_ctzll(todo);
       todo &= todo - 1;
       const uint32_t pw = w * 64 + lane;
@@ -1365,11 +1374,12 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
       if (!rpend[beg]) continue;
       const uint32_t key = ax.key[beg];
       const uint32_t end = wave_find_end(ax, beg + LONG_RUN, key, lane);
-      if (work && lane == 0) atomicAdd(work, end - beg);  // entries walked (kernel timer)
+      walked += end - beg;  // entries walked (the kernel timer's units)
       LP_ADD(0, 1);
       LP_ADD(1, end - beg);
 #ifdef RK_SWEEP_PROF
-      const uint64_t lp_t0 = __builtin_amdgcn_s_memtime();
+      const uint64_t lp_ta = __builtin_amdgcn_s_memtime();
+      LP_ADD(16, lp_ta - lp_tr);
 #endif
       // the run's open entries (UNKNOWN / HIT_PENDING): first fo, last lo.
       // Entries after lo are decided and no later query reads them, entries
@@ -1394,6 +1404,10 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
           lo = c + 4 * ll + 31 - __clz(bl);
         }
       }
+#ifdef RK_SWEEP_PROF
+      const uint64_t lp_tb = __builtin_amdgcn_s_memtime();
+      LP_ADD(12, lp_tb - lp_ta);
+#endif
       if (fo == NONE) {
         LP_ADD(10, 1);
         if (lane == 0) rpend[beg] = 0;
@@ -1405,8 +1419,17 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
       const bool has_hi = end < ax.m && ax.key[end] == key + 1;
       if (has_hi) hi_b = end, hi_e = wave_find_end(ax, end + 1, key + 1, lane);
       wave_sync_lds();  // the previous run's LDS reads are done
+#ifdef RK_SWEEP_PROF
+      const uint64_t lp_tc = __builtin_amdgcn_s_memtime();
+      LP_ADD(13, lp_tc - lp_tb);
+#endif
       const int nn0 = has_lo ? neighbour_list(ax, lo_b, lo_e, L, 0, lane) : 0;
       const int nn1 = has_hi ? neighbour_list(ax, hi_b, hi_e, L, 1, lane) : 0;
+      LP_ADD(15, (nn0 < 0 ? 1 : 0) + (nn1 < 0 ? 1 : 0));
+#ifdef RK_SWEEP_PROF
+      const uint64_t lp_t0 = __builtin_amdgcn_s_memtime();
+      LP_ADD(14, lp_t0 - lp_tc);
+#endif
       int nl = 0;
       bool pending = false;
       uint32_t cb = beg;
@@ -1490,6 +1513,7 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
         uint64_t rown = 0;
         Scan fl{0.0, NONE, 0, false, false}, fn{0.0, NONE, 0, false, false};
         Q32 q{};
+        bool coop = false;  // a neighbour query for the wavefront-wide scan
         if (open) {
           q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
           for (int j = 0; j < (int)lane; j += OWN_U) {
@@ -1530,10 +1554,53 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
                 if (d > fn.best) fn.best = d, fn.win = L.nent[sd][k];
                 fn.any_active = true;
               }
-            } else {  // list overflow: the global scan of the short-run kernel
-              foreign_scan32(ax, dir < 0 ? beg - 1 : end, dir, key + dir, i, q, fn);
+            } else {  // list overflow: the wavefront scans the neighbour run (below)
+              coop = true;
             }
           }
+        }
+        // Queries whose neighbour run overflowed its list: the whole wavefront
+        // scans that run for each of them, 64 entries per load, newest first.
+        // (A lane walking it alone -- foreign_scan32 -- waits for one load per
+        // entry: on cfg5's Y axis, where a family copy's runs straddle bucket
+        // bounds and hold hundreds of ACTIVE X hits, that walk took most of
+        // the kernel's time.)
+        for (uint64_t cm = __ballot(coop); cm; cm &= cm - 1) {
+          const int v = __builtin_ctzll(cm);
+          const int dv = __shfl(nd == 1 ? -1 : 1, v);
+          const uint32_t iv = __shfl(i, v);
+          const Q32 qv{(uint32_t)__shfl((int)q.c, v), (uint32_t)__shfl((int)q.L, v),
+                       (uint32_t)__shfl((int)q.tl, v), (uint32_t)__shfl((int)q.tc, v),
+                       __shfl(q.ok ? 1 : 0, v) != 0, __shfl(q.eq ? 1 : 0, v) != 0};
+          const uint32_t nb = dv < 0 ? lo_b : hi_b, ne = dv < 0 ? lo_e : hi_e;
+          Scan cs{0.0, NONE, 0, false, false};
+          uint32_t bestg = 0;
+          for (uint32_t top = ne; top > nb;) {  // positions [top - 64, top), newest first
+            const uint32_t g = top - 1 - lane;
+            const bool ing = g + 1 > nb && top >= 1 + lane;  // g >= nb, no wrap
+            const uint32_t eg = ing ? ax.ent[g] : 0xFFFFFFFFu;
+            const uint8_t sg = ing ? load_state(&ax.state[g]) : (uint8_t)ST_HIT;
+            const uint2 og = ing ? ax.pk[g] : make_uint2(0, 0);
+            const bool cand = ing && eg < iv && sg < ST_HIT_PENDING && m32(qv, og);
+            if (__ballot(cand && sg != ST_ACTIVE)) {  // an undecided candidate: not final now
+              cs.any_unknown = true;
+              break;
+            }
+            const bool act = cand && sg == ST_ACTIVE;
+            double d = act ? dev32(qv, og, ax.len_ratio, ax.pos_ratio) : -1.0;
+            uint32_t gg = act ? g : 0u;
+            // the first strict maximum, newest first: the larger d, then the larger g
+            for (int o = 32; o > 0; o >>= 1) {
+              const double od = __shfl_xor(d, o);
+              const uint32_t og2 = (uint32_t)__shfl_xor((int)gg, o);
+              if (od > d || (od == d && og2 > gg)) d = od, gg = og2;
+            }
+            if (__ballot(act) && (!cs.any_active || d > cs.best))
+              cs.best = d, bestg = gg, cs.any_active = true;
+            top = top > 64 ? top - 64 : 0;
+          }
+          if (cs.any_active) cs.win = ax.ent[bestg];
+          if ((int)lane == v) fn = cs;
         }
         const bool out_act = fl.any_active || fn.any_active;
         const bool out_unk = fl.any_unknown || fn.any_unknown;
@@ -1599,6 +1666,12 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
       }
     }
   }
+  if (work && lane == 0 && walked) atomicAdd(work, walked);
+#ifdef RK_SWEEP_PROF
+  if (lane == 0)
+    for (int k = 0; k < 24; ++k)
+      if (lpacc[k]) atomicAdd(&g_long_prof[k], lpacc[k]);
+#endif
 }
 
 // Run bounds of every bucket run, one wavefront per 64 positions: rlen_at at
@@ -1749,14 +1822,14 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     kt_end_units(st, KID_SWEEP_LONG, 18.0);
 #ifdef RK_SWEEP_PROF
     {  // every sweep (first=1: the first of the axis)
-      unsigned long long h[16];
+      unsigned long long h[24];
       (void)hipStreamSynchronize(st);
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_long_prof), sizeof h);
       fprintf(stderr, "first=%d ", (int)first);
       const double c = h[2] ? (double)h[2] : 1.0;
-      fprintf(stderr, "LONGPROF m=%u runs=%llu entries=%llu chunks=%llu open/chunk %.2f list/chunk %.1f overflow runs=%llu walked=%llu | Mcyc chunks %.1f walk %.1f | dedup drops=%llu | runs without open entries %llu, list-only chunks %llu\n",
-              ax.m, h[0], h[1], h[2], h[3] / c, h[4] / c, h[5], h[6], h[7] / 1e6, h[8] / 1e6, h[9],
-              h[10], h[11]);
+      fprintf(stderr, "LONGPROF m=%u runs=%llu entries=%llu chunks=%llu open/chunk %.2f list/chunk %.1f overflow runs=%llu walked=%llu | Mcyc run-find %.1f prescan %.1f nbounds %.1f nlists %.1f chunks %.1f walk %.1f | dedup drops=%llu | runs without open entries %llu, list-only chunks %llu, overflowed neighbour lists %llu\n",
+              ax.m, h[0], h[1], h[2], h[3] / c, h[4] / c, h[5], h[6], h[16] / 1e6, h[12] / 1e6,
+              h[13] / 1e6, h[14] / 1e6, h[7] / 1e6, h[8] / 1e6, h[9], h[10], h[11], h[15]);
       void *p = nullptr;
       (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_long_prof));
       (void)hipMemsetAsync(p, 0, sizeof h, st);

@@ -337,6 +337,24 @@ def test_std_sort_block_heapsort_vs_restatement(gpu_ctx):
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
 
 
+def test_std_sort_rank_heap_vs_restatement(gpu_ctx):
+    """Heap segments with a few distinct keys take the rank path (ranks-only
+    pops, then every output position traced back through the pops that wrote
+    its nodes): 2, 3 and 16 distinct keys (RANK_MAX), a heap beyond the
+    160K-node LDS part (the deeper ranks in global memory), and 17 keys (the
+    general pops again) -- against the restated std::sort."""
+    from sort_cases import killer_with_keys
+    segs = [killer_with_keys(30000, 2, 21), killer_with_keys(30001, 3, 22),
+            killer_with_keys(12000, 16, 23, base=1 << 40), killer_with_keys(12000, 17, 24),
+            killer_with_keys(400_000, 3, 25)]
+    keys = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
+    perm = gpu_ctx.std_sort_segments(keys, off)
+    for a, b, s in zip(off[:-1], off[1:], segs):
+        want = ro.std_sort(s) + a
+        assert np.array_equal(perm[a:b], want), (int(a), s.size)
+
+
 def test_pipeline_choice(gpu_ctx, generic_ctx):
     """The record pipeline runs on the BASELINE-shaped sets; inputs it cannot
     represent (a length >= 2^24) take the generic one with the same result."""

@@ -1,26 +1,27 @@
 #!/usr/bin/env python3
-"""Regenerate DESIGN.md's kernel table from profiles/r4_bench.json (HIP-event
+"""Regenerate DESIGN.md's kernel table from profiles/r5_bench.json (HIP-event
 timing inside bench.py's timed steps, cfg3), profiles/traffic.json
-(PMC HBM bytes, cfg3) and profiles/r4_bench_cfg5.json (the same timing at cfg5,
+(PMC HBM bytes, cfg3) and profiles/r5_bench_cfg5.json (the same timing at cfg5,
 one GPU) when present."""
 import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
-BENCH, CFG5 = "r4_bench.json", "r4_bench_cfg5.json"
-# bench kernel name -> the PMC summary's name (tools/pmc_summary.py keys by k_\w+)
-PMC_NAME = {"k_seg_fine (order)": "k_seg_fine"}
+BENCH, CFG5 = "r5_bench.json", "r5_bench_cfg5.json"
+# bench kernel name -> the PMC summary's name (tools/pmc_summary.py uses the bench's names)
+PMC_NAME = {}
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
-    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (2 coarse processing-order passes: the key's top 15 bits as 8 + 7 at cfg3, the second also counting each coarse key), 12-B records 7168 per tile (3 Y passes, 9 + 9 + 8 bits, after X: the first carries the X-hit bits, the last writes CSR + states; 3 member passes): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; last Y pass: 30)"),
+    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (2 coarse processing-order passes: the key's top 15 bits as 8 + 7 at cfg3, the second also counting each coarse key), 12-B records 7168 per tile (2 coarse Y passes after X, 8 + 7 bits, the first carrying the X-hit bits, the second counting each coarse key; 3 member passes, 9 + 9 + 8): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; first Y pass: 24.1)"),
     ("k_seg_fine (order)", "one block per coarse-key segment (<= 4096 records in LDS): the 14 fine bits by ballot-ranked LSD rounds, then the final records, the Y records and the X-chunk counts (an LDS window of chunk counters)", "44"),
+    ("k_seg_fine (Y)", "one block per coarse Y-key segment (<= 4096 records in LDS): the 11 fine bits by ballot-ranked LSD rounds, then the Y axis' CSR arrays (key, entry, packed record, neighbour code, state from the carried X-hit bit) written as whole lines", "30"),
     ("k_seg_big", "segments above 4096 records: the same passes through global memory, one block each", "-"),
     ("k_nw_xcount", "(RK_NW_SPLIT=0 only) entries per (strand, X chunk) and owned rows per chunk, over the processing order", "16"),
     ("k_nw_xchunk", "X axis: a wavefront per chunk places its entries (bin counts, scan, ballot ranks) and writes the owned rows' member records (in-group sort keys)", "50"),
     ("k_sweep_fast", "occupancy decisions, first sweep: a wavefront per 64-position window, ballot rounds, 32-bit candidate tests", "26"),
     ("k_sweep_fast_more", "later sweeps: one wavefront per 64 windows handles the still-pending ones", "-"),
-    ("k_sweep_long32", "runs of more than 64 entries, 64 entries at a time against LDS lists", "-"),
+    ("k_sweep_long32", "runs of more than 64 entries: a pre-scan for the run's open entries (none: the run is done), then 64 entries at a time against LDS lists (redundant ACTIVE records dropped when a list would overflow)", "-"),
     ("k_nw_x_bits", "X hits as a bitmask by processing index (ballots over the X states at each fragment's X position), read in order by the first Y pass", "5"),
     ("k_nw_fill_y", "Y states from the bitmask for later ratio pairs (X hits sit in the Y lists)", "5"),
     ("k_jump", "chase parent chains to the root", "16"),

@@ -75,6 +75,14 @@ lcheck)  # the long-run walk: parity (long runs, cfg5q digests), the cfg5 bench,
   bench bench_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 3
   RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg5 --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 4
   ;;
+lwhere)  # where k_sweep_long32's time goes at cfg5: a kernel trace of one step, and the counters of every sweep
+  timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $O/ktrace -o p -- python3 bench.py --config cfg5 --no-cpu --steps 1 --warmup 1 > $O/ktrace.log 2>&1 || exit 1
+  RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg5 --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 2
+  ;;
+heap)  # the depth-limit heapsort: parity of the std::sort emulation, then the killers' times
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v -k "std_sort" --timeout 300 --timeout-method thread > $O/heap_tests.log 2>&1 || exit 1
+  timeout -k 10 600 python3 -u tools/heap_killer_check.py --tied ${@:-10000 100000 1000000} > $O/heap_killer.log 2>&1 || exit 2
+  ;;
 abcfg5)  # parity, then cfg5 / cfg3 against the HEAD build under tools/mb/base, then the counters
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
   RK_LIB=repkiller_amd/librepkiller_amd.so bench new_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
