@@ -694,8 +694,12 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
       rk::group_offsets(w.sgid, m, G, w.goff, st);
     }
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
+    // one pair: the depth-limit heap segments' count (crafted inputs only)
+    // comes back with the final status word (ctrl[33]) instead of a wait of
+    // its own (several pairs share the scratch: each waits)
     rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
-                          ctx->host + 128, narrow_keys, st, st2, ctx->fork, ctx->join);
+                          ctx->host + 128, narrow_keys, st, st2, ctx->fork, ctx->join,
+                          npairs == 1 ? w.ctrl + 33 : nullptr);
     if (prof) mark(ctx, RK_PH_EMIT);
     rk::emit_result(w.otag, w.sgid, w.goff, w.mrow, m, out->gid, out->repval, out->out_order,
                     st);
@@ -703,7 +707,17 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (prof) mark(ctx, RK_N_PHASES);
   }
   HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
-  if ((rc = readback(ctx, w.ctrl, 1))) return rc;
+  if ((rc = readback(ctx, w.ctrl, npairs == 1 ? 34 : 1))) return rc;
+  if (npairs == 1 && m && ctx->host[33]) {  // heap segments: sorted now, then the result again
+    const uint32_t G = outs[0].n_groups;
+    rk::sort_groups_heap_deferred(G, m, w.reckey, w.tag, w.otag, w.gsort, ctx->host[33],
+                                  ctx->host + 128, st);
+    rk::emit_result(w.otag, w.sgid, w.goff, w.mrow, m, outs[0].gid, outs[0].repval,
+                    outs[0].out_order, st);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
+    if ((rc = readback(ctx, w.ctrl, 1))) return rc;
+  }
   collect_phases(ctx);
   if ((rc = err_status(ctx, ctx->host[0]))) return rc;
   float ms = 0;

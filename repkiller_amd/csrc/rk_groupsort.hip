@@ -169,7 +169,7 @@ __device__ void heap_sort_segment(const V &v, uint32_t f, uint32_t l) {
 //    above its slot are written.
 constexpr uint32_t HEAP_BLOCK_MIN = 2048;  // smaller exhausted segments: one thread
 constexpr int HLV = 13;                    // heap levels in LDS
-// k_heap_segments keeps the heap's top HLV levels in LDS: (2^13 - 1) x (8 + 4)
+// k_heap_segments keeps the heap's top HLV levels in LDS: 2^13 x (8 + 4)
 // B = 96 KB of static LDS, which needs gfx950's 160 KB per workgroup (64 KB
 // on gfx942 / gfx90a)
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
@@ -181,16 +181,29 @@ constexpr uint32_t HR_LAST = (1u << HR) - 2, HR_NODES = (2u << HR) - 2;  // 62, 
 static_assert(HR_NODES <= 128, "two logical nodes per lane");
 constexpr int HRMAX = 6;                   // rounds per pop (heaps below 2^36 nodes)
 
-struct HeapMem {  // node x: LDS below HTOP, else the segment in global memory
+// node x: LDS below HTOP, else the segment in global memory.  The LDS access
+// is unconditional (slot HTOP of the LDS arrays is a dummy) and the global one
+// conditional: `x < HTOP ? lk[x] : K[x]` compiled to a select of the two
+// pointers and one FLAT access, which costs every LDS access a flat round trip
+struct HeapMem {
   uint64_t *K;
   uint32_t *T;
-  uint64_t *lk;
+  uint64_t *lk;  // HTOP + 1 entries
   uint32_t *lt;
-  __device__ __forceinline__ uint64_t key(uint32_t x) const { return x < HTOP ? lk[x] : K[x]; }
-  __device__ __forceinline__ uint32_t tag(uint32_t x) const { return x < HTOP ? lt[x] : T[x]; }
+  __device__ __forceinline__ uint64_t key(uint32_t x) const {
+    uint64_t v = lk[x < HTOP ? x : HTOP];
+    if (x >= HTOP) v = K[x];
+    return v;
+  }
+  __device__ __forceinline__ uint32_t tag(uint32_t x) const {
+    uint32_t v = lt[x < HTOP ? x : HTOP];
+    if (x >= HTOP) v = T[x];
+    return v;
+  }
   __device__ __forceinline__ void put(uint32_t x, uint64_t k, uint32_t t) const {
-    if (x < HTOP) lk[x] = k, lt[x] = t;
-    else K[x] = k, T[x] = t;
+    const uint32_t y = x < HTOP ? x : HTOP;
+    lk[y] = k, lt[y] = t;
+    if (x >= HTOP) K[x] = k, T[x] = t;
   }
 };
 
@@ -1147,8 +1160,8 @@ __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tie
 __global__ void __launch_bounds__(256) k_heap_segments(const uint32_t *heapq_n,
                                                        const HeapSeg *heapq, uint64_t *key,
                                                        uint32_t *tag, uint32_t *otag) {
-  __shared__ uint64_t lk[HTOP];
-  __shared__ uint32_t lt[HTOP];
+  __shared__ uint64_t lk[HTOP + 1];
+  __shared__ uint32_t lt[HTOP + 1];
   const uint32_t cnt = min(*heapq_n, HEAPQ_CAP);
   for (uint32_t s = blockIdx.x; s < cnt; s += gridDim.x) {
     const HeapSeg g = heapq[s];
@@ -1219,13 +1232,14 @@ __global__ void __launch_bounds__(256) k_heap_prep(uint64_t *K, uint32_t *T, uin
     ++D;
     __syncthreads();
   }
-  const uint32_t md = D <= 1 ? HM_EQUAL : D <= RANK_MAX ? HM_RANK : HM_GENERAL;
+  // (the rank pops' 32-bit positions: heaps below 2^23 nodes)
+  const uint32_t md = D <= 1 ? HM_EQUAL : D <= RANK_MAX && n < (1u << 23) ? HM_RANK : HM_GENERAL;
   if (md == HM_RANK)
     for (uint32_t x = tid; x < n; x += blockDim.x) {
       const unsigned long long k = K[x];
       uint32_t r = 0;
       while (vals[r] != k) ++r;
-      R[x] = (uint8_t)r;
+      R[x + 1] = (uint8_t)r;  // (shifted: a node pair is one aligned 16-bit word)
     }
   if (tid == 0) *mode = md;
 }
@@ -1242,8 +1256,8 @@ __global__ void __launch_bounds__(64) k_heap_equal(uint32_t *T, uint32_t n, uint
 }
 __global__ void __launch_bounds__(256) k_heap_general(uint64_t *K, uint32_t *T, uint32_t n,
                                                      uint32_t *out, const uint32_t *mode) {
-  __shared__ uint64_t lk[HTOP];
-  __shared__ uint32_t lt[HTOP];
+  __shared__ uint64_t lk[HTOP + 1];
+  __shared__ uint32_t lt[HTOP + 1];
   if (*mode != HM_GENERAL) return;
   const uint32_t tid = threadIdx.x;
   for (uint32_t x = tid; x < n && x < HTOP; x += blockDim.x) lk[x] = K[x], lt[x] = T[x];
@@ -1253,130 +1267,207 @@ __global__ void __launch_bounds__(256) k_heap_general(uint64_t *K, uint32_t *T, 
   for (uint32_t x = tid; x < n; x += blockDim.x) out[x] = x < HTOP ? lt[x] : T[x];
 }
 
-struct RankMem {  // node x: LDS below RT, else the ranks in global memory
-  uint8_t *lr, *gr;
-  uint32_t RT;
-  __device__ __forceinline__ uint32_t key(uint32_t x) const { return x < RT ? lr[x] : gr[x]; }
-  __device__ __forceinline__ void put(uint32_t x, uint32_t k) const {
-    if (x < RT) lr[x] = (uint8_t)k;
-    else gr[x] = (uint8_t)k;
-  }
-};
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
-// __sort_heap of [0, n) on the ranks alone by one wavefront (wave_sort_heap's
-// descent, no tags): pop t = n - 1 - last logs its direction bits from the
-// root (logb, the first level the highest of D bits) and D | j << 8 (logq)
-__device__ void wave_rank_pops(const RankMem &h, uint32_t n, uint32_t lane, uint32_t *logb,
-                               uint16_t *logq) {
-  for (uint32_t last = n - 1; last > 0; --last) {
-    // (the root leaves for `last`, outside the heap from now on: not stored)
-    const uint32_t vk = h.key(last);
-    const uint32_t len = last;
-    const uint32_t two_lim = (len - 1) / 2;  // hole x has two children iff x < two_lim
-    uint64_t pm0[HRMAX], pm1[HRMAX];
-    uint32_t k0[HRMAX], k1[HRMAX], x0[HRMAX], x1[HRMAX];
-    uint32_t hole = 0, bits = 0, D = 0;
-    int rounds = 0;
-    bool more = true;
-#pragma unroll
-    for (int r = 0; r < HRMAX; ++r) {
-      pm0[r] = pm1[r] = 0;
-      k0[r] = k1[r] = x0[r] = x1[r] = 0;
-      if (!more) continue;
-      ++rounds;
-      uint32_t kk[2], xx[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const uint32_t c = lane + 64 * s;
-        const int d = 31 - __clz((int)(c + 2));
-        const uint64_t pos = ((uint64_t)hole + 1) * (1ull << d) - 1 + (c + 2 - (1u << d));
-        const bool in = c < HR_NODES && pos < len;
-        xx[s] = in ? (uint32_t)pos : 0u;
-        kk[s] = in ? h.key((uint32_t)pos) : 0u;
-      }
-      uint64_t dir[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const uint32_t sib = (uint32_t)__shfl_xor((int)kk[s], 1);
-        dir[s] = __ballot((lane & 1) && !(kk[s] < sib));  // ties go right
-      }
-      uint32_t J = 0, x = hole;
-      more = false;
-      for (;;) {
-        if (x >= two_lim) {  // no second child: a lone left child ends the descent
-          if ((len & 1) == 0 && x == (len - 2) / 2) {
-            const uint32_t c = 2 * J;
-            if (c < 64) pm0[r] |= 1ull << c;
-            else pm1[r] |= 1ull << (c - 64);
-            bits <<= 1;
-            ++D;
-          }
-          break;
-        }
-        const uint32_t cr = 2 * J + 1;
-        const bool right = ((cr < 64 ? dir[0] >> cr : dir[1] >> (cr - 64)) & 1ull) != 0;
-        const uint32_t c = right ? cr : cr - 1;
-        if (c < 64) pm0[r] |= 1ull << c;
-        else pm1[r] |= 1ull << (c - 64);
-        bits = bits << 1 | (right ? 1u : 0u);
-        ++D;
-        x = 2 * x + (right ? 2 : 1);
-        if (c >= HR_LAST) {
-          hole = x;
-          more = true;
-          break;
-        }
-        J = c + 1;
-      }
-      k0[r] = kk[0], k1[r] = kk[1];
-      x0[r] = xx[0], x1[r] = xx[1];
-    }
-    // __push_heap: the value rises past the path keys below it (a suffix)
-    uint32_t below = 0;
-#pragma unroll
-    for (int r = 0; r < HRMAX; ++r) {
-      if (r >= rounds) break;
-      below += __popcll(__ballot(((pm0[r] >> lane) & 1) && k0[r] < vk)) +
-               __popcll(__ballot(((pm1[r] >> lane) & 1) && k1[r] < vk));
-    }
-    const uint32_t j = D - below;  // the value's slot is path position j (0: the root)
-    uint32_t before = 0;
-    const uint64_t lt = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int r = 0; r < HRMAX; ++r) {
-      if (r >= rounds) break;
-      const bool on0 = (pm0[r] >> lane) & 1, on1 = (pm1[r] >> lane) & 1;
-      const uint32_t p0 = before + __popcll(pm0[r] & lt) + 1;
-      const uint32_t p1 = before + __popcll(pm0[r]) + __popcll(pm1[r] & lt) + 1;
-      if (on0 && p0 <= j) {
-        h.put((x0[r] - 1) / 2, k0[r]);
-        if (p0 == j) h.put(x0[r], vk);
-      }
-      if (on1 && p1 <= j) {
-        h.put((x1[r] - 1) / 2, k1[r]);
-        if (p1 == j) h.put(x1[r], vk);
-      }
-      before += __popcll(pm0[r]) + __popcll(pm1[r]);
-    }
-    if (lane == 0) {
-      if (j == 0) h.put(0, vk);
-      const uint32_t t = n - 1 - last;
-      logb[t] = bits;
-      logq[t] = (uint16_t)(D | j << 8);
-    }
-    wave_sync();  // the next pop reads what this one wrote (in order, one wavefront)
-  }
+// k_heap_rank_pops: __sort_heap of [0, n) on the ranks alone by one
+// wavefront; pop t = n - 1 - last logs its direction bits from the root
+// (logb, the first level the highest of D bits) and D | j << 8 (logq).  The
+// ranks come from k_heap_prep at R[x + 1]; nodes x < RT live in LDS at
+// L[x + 1] (the whole heap when it fits, BIG = false; else the top ~159K
+// nodes, RT odd, and the rest stays in R) -- shifted by one so that a node's
+// two children 2y + 1, 2y + 2 are one aligned 16-bit word, read by one 16-bit
+// load per pair (RT odd: no pair straddles the two arrays).  L[SENT],
+// L[SENT + 1] hold a sentinel pair (1, 0) -- right < left, no "right"
+// direction -- read in place of every pair whose right child is outside the
+// heap, so a direction is one compare.  No static LDS: the array starts at
+// LDS address 0 and constant offsets fold into the ds instructions.  32-bit
+// positions (a round's (hole + 1) << 8 stays below 2^32 for heaps below 2^23
+// nodes; the host routes larger ones to the general pops).  A lone wavefront
+// pays every instruction in latency (~5-8 cycles each,
+// `tools/mb/clockprobe.hip`), so the pop is cut to what it needs:
+//  * a pop's descent is found 8 levels per round: lane l holds the child pairs
+//    of the round's internal nodes J = l + 64 s, s < 4, numbered from 1 (J's
+//    children are 2J, 2J + 1), one ballot per s holds every direction (ties go
+//    right), and the round's direction bits are J - 2^Dr at its end;
+//  * the first round's pairs (the heap's top 8 levels, fixed positions 2J - 1,
+//    2J) stay in registers, re-read after each pop's stores;
+//  * the walk takes all 8 steps as s_bitcmp1 (SCC = the direction bit) +
+//    s_addc (J = 2J + SCC) and is cut afterwards to the levels that exist
+//    without a test (descents onto the complete levels; the first k steps of
+//    a walk are J >> (8 - k)); at most one step more, onto the incomplete last
+//    level, is tested;
+//  * __push_heap: lane i reads path node i (x_0 the root) at the position the
+//    bits give, one ballot counts the path keys below the displaced value
+//    (they form a suffix: the path's keys descend), and lane i moves its key to
+//    x_{i-1} when 1 <= i <= j, the value landing at x_j; the log collects in
+//    two registers, lane t % 64 holding pop t, 64 pops per store.
+// The round-4 general pops (64-bit keys, tags moved along) took ~2.9 us per
+// pop; the first rank version (64-bit positions, per-node LDS / global
+// selection, path keys through a scratch) ~3 us, bound by instruction
+// latency; this one ~0.5 us with the heap in LDS.
+constexpr int RHR = 8;                          // levels per round
+constexpr uint32_t RPAIRS = (1u << RHR) - 1;    // internal nodes of a round (255)
+constexpr int RS = (int)((RPAIRS + 64) / 64);   // pairs per lane (4: J = 0 .. 255)
+__device__ __forceinline__ uint32_t dir_bit(uint64_t d0, uint64_t d1, uint64_t d2, uint64_t d3,
+                                            uint32_t J) {
+  const uint64_t lo = J < 64 ? d0 : d1, hi = J < 192 ? d2 : d3;
+  return (uint32_t)((J < 128 ? lo : hi) >> (J & 63)) & 1u;
 }
-
+template <bool BIG>
 __global__ void __launch_bounds__(64) k_heap_rank_pops(uint8_t *R, uint32_t n, uint32_t RT,
                                                       uint32_t *logb, uint16_t *logq,
                                                       const uint32_t *mode) {
   extern __shared__ uint8_t lr[];
   if (*mode != HM_RANK) return;
+  lds_u8 *L = (lds_u8 *)lr;
   const uint32_t lane = threadIdx.x;
-  for (uint32_t x = lane; x < RT; x += 64) lr[x] = R[x];
+  const uint32_t SENT = (RT + 2) & ~1u, DUMMY = SENT + 4;  // (a discarded store's slot)
+  for (uint32_t x = lane; x < RT; x += 64) L[x + 1] = R[x + 1];
+  if (lane == 0) L[0] = 0, L[RT + 1] = 0, L[SENT] = 1, L[SENT + 1] = 0;
   wave_sync();
-  wave_rank_pops(RankMem{lr, R, RT}, n, lane, logb, logq);
+  const auto key = [&](uint32_t x) {  // (wave-uniform x)
+    return BIG && x >= RT ? (uint32_t)R[x + 1] : (uint32_t)L[x + 1];
+  };
+  // (lane 0's J = 0 is no node: its words and direction bit are never used)
+  uint32_t Jv[RS], sh[RS], ad[RS], w1[RS];
+#pragma unroll
+  for (int s = 0; s < RS; ++s) {
+    const uint32_t J = lane + 64 * s, d = 31 - __clz((int)(J | 1u));
+    Jv[s] = J;
+    sh[s] = d + 1;                         // left child of J below hole h:
+    ad[s] = 2 * (J - (1u << d)) - 1u;      // ((h + 1) << (d + 1)) - 1 + 2 (J - 2^d)
+  }
+  const auto load_w1 = [&] {  // (positions <= 510 < RT)
+#pragma unroll
+    for (int s = 0; s < RS; ++s) w1[s] = *(const lds_u16 *)(L + 2 * Jv[s]);
+  };
+  load_w1();
+  uint32_t lb = 0, lq = 0;
+#ifdef RK_HEAP_PROF
+  unsigned long long c_load = 0, c_walk = 0, c_push = 0, c_rounds = 0;
+#define HP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define HP_T(v)
+#endif
+  for (uint32_t last = n - 1; last > 0; --last) {
+    const uint32_t vk = key(last);
+    const uint32_t len = last;
+    const uint32_t fl = 31 - __clz((int)(len + 1));  // levels 0 .. fl - 1 are complete
+    uint32_t hole = 0, bits = 0, D = 0;
+    for (bool first = true;; first = false) {
+      HP_T(h0);
+      uint32_t w[RS];
+      if (first) {
+#pragma unroll
+        for (int s = 0; s < RS; ++s) w[s] = 2 * Jv[s] < len ? w1[s] : 1u;  // (1, 0): no direction
+      } else {
+        uint32_t lp[RS];
+        bool glob[RS], anyg = false;
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+          const uint32_t l = ((hole + 1) << sh[s]) + ad[s];
+          const bool pres = l + 1 < len;
+          lp[s] = l + 1;
+          glob[s] = BIG && pres && l >= RT;
+          anyg |= glob[s];
+          w[s] = *(const lds_u16 *)(L + (pres && !glob[s] ? l + 1 : SENT));
+        }
+        if (BIG && __builtin_amdgcn_ballot_w64(anyg)) {  // a round below the LDS levels
+#pragma unroll
+          for (int s = 0; s < RS; ++s)
+            if (glob[s]) w[s] = *(const uint16_t *)(R + lp[s]);
+        }
+      }
+      uint64_t dm[RS];
+#pragma unroll
+      for (int s = 0; s < RS; ++s) dm[s] = __builtin_amdgcn_ballot_w64((w[s] >> 8) >= (w[s] & 0xffu));  // ties go right
+      HP_T(h1);
+      D = __builtin_amdgcn_readfirstlane(D);
+      hole = __builtin_amdgcn_readfirstlane(hole);
+      bits = __builtin_amdgcn_readfirstlane(bits);
+      const uint64_t d0 = dm[0], d1 = dm[1 % RS], d2 = dm[2 % RS], d3 = dm[3 % RS];
+      uint32_t J8 = 1;
+      uint64_t tmp;
+      static_assert(RHR == 8 && RS == 4, "the walk below is written for 8 levels");
+      asm volatile(
+          "s_bitcmp1_b64 %[d0], %[J]\n\ts_addc_u32 %[J], %[J], %[J]\n\t"
+          "s_bitcmp1_b64 %[d0], %[J]\n\ts_addc_u32 %[J], %[J], %[J]\n\t"
+          "s_bitcmp1_b64 %[d0], %[J]\n\ts_addc_u32 %[J], %[J], %[J]\n\t"
+          "s_bitcmp1_b64 %[d0], %[J]\n\ts_addc_u32 %[J], %[J], %[J]\n\t"
+          "s_bitcmp1_b64 %[d0], %[J]\n\ts_addc_u32 %[J], %[J], %[J]\n\t"
+          "s_bitcmp1_b64 %[d0], %[J]\n\ts_addc_u32 %[J], %[J], %[J]\n\t"
+          "s_bitcmp1_b64 %[d1], %[J]\n\ts_addc_u32 %[J], %[J], %[J]\n\t"
+          "s_cmpk_lt_u32 %[J], 0xc0\n\ts_cselect_b64 %[t], %[d2], %[d3]\n\t"
+          "s_bitcmp1_b64 %[t], %[J]\n\ts_addc_u32 %[J], %[J], %[J]"
+          : [J] "+s"(J8), [t] "=&s"(tmp)
+          : [d0] "s"(d0), [d1] "s"(d1), [d2] "s"(d2), [d3] "s"(d3)
+          : "scc");
+      const uint32_t lim = fl >= D + 2 ? min((uint32_t)RHR, fl - 1 - D) : 0u;
+      uint32_t J = J8 >> (RHR - lim), Dr = lim;
+      uint32_t x = ((hole + 1) << Dr) - 1 + (J - (1u << Dr));
+      bool more;
+      if (Dr == RHR) {
+        more = 2 * x + 1 < len;
+      } else {
+        const uint32_t two = 2 * x + 2;
+        more = false;
+        if (two <= len) {
+          const uint32_t bt = two < len ? dir_bit(d0, d1, d2, d3, J) : 0u;  // (==: a lone left child)
+          J = 2 * J + bt;
+          x = two - 1 + bt;
+          if (++Dr == RHR) more = 2 * x + 1 < len;
+        }
+      }
+      bits = (Dr ? bits << Dr : bits) | (J - (1u << Dr));
+      D += Dr;
+      hole = x;
+#ifdef RK_HEAP_PROF
+      HP_T(h2);
+      c_load += h1 - h0, c_walk += h2 - h1, ++c_rounds;
+#endif
+      if (!more) break;
+    }
+    HP_T(h4);
+    // __push_heap
+    const uint32_t i = lane;
+    const bool on = i <= D;
+    const uint32_t xi = (1u << i) - 1u + (on ? bits >> (D - i) : 0u);
+    const bool gi = BIG && on && xi >= RT;
+    uint32_t ki = on && !gi ? (uint32_t)L[xi + 1] : 0u;
+    if (BIG && gi) ki = R[xi + 1];
+    const uint32_t j = D - (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(on && i >= 1 && ki < vk));
+    wave_sync();  // (every lane's read before any write; one wavefront's memory ops are in order)
+    if (i >= 1 && i <= j) {
+      const uint32_t y = (xi - 1) / 2;  // x_{i-1}
+      if (!BIG || y < RT) L[y + 1] = (uint8_t)ki;
+      else R[y + 1] = (uint8_t)ki;
+    }
+    if (i == j) {
+      if (!BIG || xi < RT) L[xi + 1] = (uint8_t)vk;
+      else R[xi + 1] = (uint8_t)vk;
+    }
+    const uint32_t t = n - 1 - last;
+    if (lane == (t & 63)) lb = bits, lq = D | j << 8;
+    if ((t & 63) == 63 || last == 1) {
+      const uint32_t t0 = t & ~63u;
+      if (t0 + lane <= t) logb[t0 + lane] = lb, logq[t0 + lane] = (uint16_t)lq;
+    }
+    wave_sync();
+    load_w1();
+#ifdef RK_HEAP_PROF
+    HP_T(h5);
+    c_push += h5 - h4;
+#endif
+  }
+  (void)DUMMY;
+#ifdef RK_HEAP_PROF
+  if (lane == 0)
+    printf("HEAPPROF n=%u cycles/pop: load %.0f walk %.0f push %.0f | rounds/pop %.2f\n", n,
+           (double)c_load / (n - 1), (double)c_walk / (n - 1), (double)c_push / (n - 1),
+           (double)c_rounds / (n - 1));
+#endif
+#undef HP_T
 }
 
 __global__ void k_heap_pair_counts(const uint16_t *logq, uint32_t npop, uint32_t *cnt) {
@@ -1447,7 +1538,9 @@ static void heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint
   for (const HeapSeg &g : q) nmax = g.n > nmax ? g.n : nmax;
   constexpr uint32_t LDS_MAX = 160 * 1024 - 1024;
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void *)k_heap_rank_pops,
+    (void)hipFuncSetAttribute((const void *)k_heap_rank_pops<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+    (void)hipFuncSetAttribute((const void *)k_heap_rank_pops<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
     return true;
   }();
@@ -1467,11 +1560,14 @@ static void heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint
     const size_t o = (size_t)g.b + g.f;
     uint64_t *K = key + o;
     uint32_t *T = tag + o, *out = otag + o;
-    const uint32_t n = g.n, RT = n < LDS_MAX ? n : LDS_MAX;
+    const uint32_t n = g.n, RT = (LDS_MAX - 32) | 1u;  // (odd: no pair straddles)
     k_heap_prep<<<1, 256, 0, st>>>(K, T, n, R, mode);
     k_heap_equal<<<1, 64, 0, st>>>(T, n, out, mode);
     k_heap_general<<<1, 256, 0, st>>>(K, T, n, out, mode);
-    k_heap_rank_pops<<<1, 64, RT, st>>>(R, n, RT, logb, logq, mode);
+    if (n + 16 <= LDS_MAX)  // the whole heap in LDS
+      k_heap_rank_pops<false><<<1, 64, n + 16, st>>>(R, n, n, logb, logq, mode);
+    else  // the top RT (odd) nodes in LDS
+      k_heap_rank_pops<true><<<1, 64, RT + 16, st>>>(R, n, RT, logb, logq, mode);
     (void)hipMemcpyAsync(host_words, mode, 4, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     if (host_words[0] != HM_RANK) continue;
@@ -1699,11 +1795,39 @@ size_t groupsort_scratch_bytes(uint32_t n) {
          (HEAPQ_CAP + 1) * sizeof(HeapSeg) + 64;
 }
 
+// the heap-segment queue inside sort_groups_exact's scratch (the layout below)
+static HeapSeg *heap_queue(void *scratch, uint32_t m, uint32_t ngroups) {
+  const uint32_t nblk = (ngroups + TCH - 1) / TCH;
+  uint32_t *pl = reinterpret_cast<uint32_t *>(scratch);
+  uint32_t *list = pl + 2 * (size_t)m;
+  uint8_t *bnd = reinterpret_cast<uint8_t *>(
+      (reinterpret_cast<uintptr_t>(list + ngroups + 1) + 15) & ~(uintptr_t)15);
+  uint32_t *bc = reinterpret_cast<uint32_t *>(
+      (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
+  uint32_t *bm = bc + 2 * ((size_t)NTIER * nblk + 1);
+  return reinterpret_cast<HeapSeg *>(
+      (reinterpret_cast<uintptr_t>(bm + (size_t)NTIER * nblk) + 63) & ~(uintptr_t)63);
+}
+
+// The heap segments of a sort_groups_exact call made with `heap_count`: their
+// number was copied to heap_count, which the caller read back together with
+// its own words; this sorts them (their tags into otag) afterwards.
+void sort_groups_heap_deferred(uint32_t ngroups, uint32_t m, uint64_t *key, uint32_t *tag,
+                               uint32_t *otag, void *scratch, uint32_t nheap,
+                               uint32_t *host_words, hipStream_t st) {
+  nheap = nheap < HEAPQ_CAP ? nheap : HEAPQ_CAP;
+  if (nheap) heap_segments(heap_queue(scratch, m, ngroups), nheap, key, tag, otag, host_words, st);
+}
+
 void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
                        ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
-                       hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
-  if (!m) return;
+                       hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join,
+                       uint32_t *heap_count) {
+  if (!m) {
+    if (heap_count) (void)hipMemsetAsync(heap_count, 0, 4, st);
+    return;
+  }
   constexpr int NL = NTIER;  // every tier is listed
   // groups of <= 64 members (k_sort_small, registers) run on `side`,
   // concurrently with the LDS tiers
@@ -1719,8 +1843,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
       (reinterpret_cast<uintptr_t>(bnd + m) + 63) & ~(uintptr_t)63);
   uint32_t *boff = bc + (size_t)NL * nblk + 1;
   uint32_t *bm = boff + (size_t)NL * nblk + 1;
-  HeapSeg *heapq = reinterpret_cast<HeapSeg *>(
-      (reinterpret_cast<uintptr_t>(bm + (size_t)NL * nblk) + 63) & ~(uintptr_t)63);
+  HeapSeg *heapq = heap_queue(scratch, m, ngroups);  // (after bm's NL * nblk words)
   uint32_t *heapq_n = reinterpret_cast<uint32_t *>(heapq + HEAPQ_CAP);
   const bool timing = g_ktimer != nullptr;
   if (timing) {
@@ -1892,7 +2015,9 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     return !(e && e[0] == '0');
   }();
   kt_begin(st, KID_SORT_HEAP);
-  if (heap_rank) {
+  if (heap_rank && heap_count) {  // the caller reads the count back with its own words
+    (void)hipMemcpyAsync(heap_count, heapq_n, 4, hipMemcpyDeviceToDevice, st);
+  } else if (heap_rank) {
     (void)hipMemcpyAsync(host_words, heapq_n, 4, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     const uint32_t nheap = host_words[0] < HEAPQ_CAP ? host_words[0] : HEAPQ_CAP;

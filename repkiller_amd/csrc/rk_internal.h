@@ -203,6 +203,18 @@ struct Csr {  // one axis in CSR order (see Axis)
   uint8_t *nbd;  // neighbour bucket probed: 0 none, 1 = B-1, 2 = B+1
 };
 
+// inclusive prefix sum over the 64 lanes of a wavefront by DPP row shifts and
+// row broadcasts (no LDS round trip; lanes outside the shifted row read 0)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
 // The neighbour bucket get_associated_group effectively probes
 // (SequenceOcupationList.cpp:47-89): rescanning a bucket under the strict `>`
 // is a no-op, so only B-1 (c % 100 in {0, 1}, c >= 100) or B+1 (c % 100 == 99
@@ -253,7 +265,13 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
                        ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
                        hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
-                       hipEvent_t ev_join = nullptr);
+                       hipEvent_t ev_join = nullptr, uint32_t *heap_count = nullptr);
+// heap_count != nullptr: the depth-limit heap segments are not sorted, their
+// number goes to heap_count (device), and the caller, having read it back,
+// sorts them by this before using otag
+void sort_groups_heap_deferred(uint32_t ngroups, uint32_t m, uint64_t *key, uint32_t *tag,
+                               uint32_t *otag, void *scratch, uint32_t nheap,
+                               uint32_t *host_words, hipStream_t st);
 // sorted member slots (otag), group of every slot (sgid), group bounds, the
 // members' file rows -> the output columns
 void emit_result(const uint32_t *otag, const uint32_t *sgid, const uint32_t *goff,

@@ -487,10 +487,12 @@ __device__ __forceinline__ void foreign_scan32(const Axis &ax, uint32_t g0, int 
 #endif
 constexpr int OWN_U = RK_OWN_U;
 #ifdef RK_SWEEP_PROF
-// measurement build only: per-phase shader cycles of the first window sweep
+// measurement build only: per-phase shader cycles of the first window sweep,
+// sampled over every 64th window (the atomics of every window slowed the
+// memory phases they were timing)
 __device__ unsigned long long g_sweep_prof[16];
 #define SP_T(k) const uint64_t _t##k = __builtin_amdgcn_s_memtime()
-#define SP_ADD(slot, v) do { if (lflag && lane == 0) atomicAdd(&g_sweep_prof[slot], (unsigned long long)(v)); } while (0)
+#define SP_ADD(slot, v) do { if (lflag && lane == 0 && (w & 63) == 0) atomicAdd(&g_sweep_prof[slot], (unsigned long long)(v)); } while (0)
 #else
 #define SP_T(k)
 #define SP_ADD(slot, v)
@@ -595,6 +597,7 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
     SP_T(2);
 #ifdef RK_SWEEP_PROF
     uint32_t nbl = 0, nfor = 0;  // neighbour-run entries in LDS / foreign scans of this lane
+    uint64_t fcyc = 0;           // cycles the wavefront spent in foreign scans
 #endif
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
@@ -638,7 +641,13 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
 #ifdef RK_SWEEP_PROF
         ++nfor;
 #endif
+#ifdef RK_SWEEP_PROF
+        const uint64_t _f0 = __builtin_amdgcn_s_memtime();
+#endif
         foreign_scan32(ax, g0, dir, k + dir, i, q, fs[s]);
+#ifdef RK_SWEEP_PROF
+        fcyc += __builtin_amdgcn_s_memtime() - _f0;
+#endif
       }
     }
     // all candidates of a slot as one mask in window positions, so a round
@@ -738,12 +747,8 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
 #define RK_DEV_PAR_MIN 3
 #endif
     if (PAR && cmax >= RK_DEV_PAR_MIN) {
-      uint32_t incl = ct;  // inclusive prefix of the pair counts
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-      }
-      const uint32_t start = incl - ct, T = __shfl(incl, 63);
+      const uint32_t incl = wave_incl_scan(ct);  // inclusive prefix of the pair counts
+      const uint32_t start = incl - ct, T = __builtin_amdgcn_readlane(incl, 63);
       uint32_t *owner_at = key;  // the keys are done with (64 words used)
       for (uint32_t cb = 0; cb < T; cb += 64) {
         // owners mark their pairs inside this chunk
@@ -793,19 +798,31 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
           const Q32 q = make_q32(qp.x, qp.y, ax.len_ratio, ax.pos_ratio);
           d = dev32(q, pk[cpos], ax.len_ratio, ax.pos_ratio);
           dev[lane] = d;
-          owner_at[64 + lane] = (uint32_t)cpos;
+          owner_at[64 + lane] = ent[cpos];  // the candidate's id
         }
         wave_sync_lds();
-        // every owner takes its pairs of this chunk in scan order
+        // every owner takes its pairs of this chunk in scan order, four per
+        // step (independent LDS reads; the longest list sets the pace)
         {
           const uint32_t j0 = start > cb ? start : cb, j1e = start + ct, j1 = j1e < cb + 64 ? j1e : cb + 64;
-          for (uint32_t j = j0; j < j1; ++j) {
-            const uint32_t x = j - cb, kj = j - start;
-            const double dj = dev[x];
-            if (NSLOT == 2 && kj >= c0) {
-              if (dj > bestv[1 % NSLOT]) bestv[1 % NSLOT] = dj, winv[1 % NSLOT] = ent[owner_at[64 + x]];
-            } else {
-              if (dj > bestv[0]) bestv[0] = dj, winv[0] = ent[owner_at[64 + x]];
+          for (uint32_t j = j0; j < j1; j += 4) {
+            double dj[4];
+            uint32_t ej[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const uint32_t x = (j + u < j1 ? j + u : j0) - cb;
+              dj[u] = dev[x];
+              ej[u] = owner_at[64 + x];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (j + u >= j1) break;
+              const uint32_t kj = j + u - start;
+              if (NSLOT == 2 && kj >= c0) {
+                if (dj[u] > bestv[1 % NSLOT]) bestv[1 % NSLOT] = dj[u], winv[1 % NSLOT] = ej[u];
+              } else {
+                if (dj[u] > bestv[0]) bestv[0] = dj[u], winv[0] = ej[u];
+              }
             }
           }
         }
@@ -832,6 +849,7 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
         }
       }
     }
+    SP_T(45);
 #pragma unroll
     for (int s = 0; s < NSLOT; ++s) {
       if (!own[s] || st[s] == st0[s]) continue;
@@ -853,7 +871,9 @@ __device__ __forceinline__ bool sweep_core32(const Axis &ax, uint32_t w, uint8_t
     SP_ADD(1, _t2 - _t1);
     SP_ADD(2, _t3 - _t2);
     SP_ADD(3, _t4 - _t3);
-    SP_ADD(4, _t5 - _t4);
+    SP_ADD(4, _t45 - _t4);
+    SP_ADD(14, _t5 - _t45);
+    SP_ADD(15, __builtin_amdgcn_readfirstlane((uint32_t)fcyc));
     SP_ADD(5, nrounds);
     SP_ADD(6, 1);
     SP_ADD(7, o1 != 0);
@@ -1806,8 +1826,8 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
       (void)hipStreamSynchronize(st);
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sweep_prof), sizeof h);
       const double w = h[6] ? (double)h[6] : 1.0;
-      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f rounds %.0f win %.0f | rounds/win %.2f slot1 %.3f one-slot windows %.3f | longest deviation list/win %.2f deviations/win %.2f | longest LDS neighbour run/win %.2f LDS neighbour entries/win %.2f foreign scans/win %.3f\n",
-              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[7] / w, h[8] / w, h[9] / w, h[10] / w, h[11] / w, h[12] / w, h[13] / w);
+      fprintf(stderr, "SWEEPPROF m=%u windows=%llu cyc/win: setup %.0f own %.0f nb %.0f (foreign scans %.0f) rounds %.0f winners %.0f record %.0f | rounds/win %.2f slot1 %.3f one-slot windows %.3f | longest deviation list/win %.2f deviations/win %.2f | longest LDS neighbour run/win %.2f LDS neighbour entries/win %.2f foreign scans/win %.3f\n",
+              ax.m, h[6], h[0] / w, h[1] / w, h[2] / w, h[15] / w, h[3] / w, h[4] / w, h[14] / w, h[5] / w, h[7] / w, h[8] / w, h[9] / w, h[10] / w, h[11] / w, h[12] / w, h[13] / w);
       (void)hipMemsetAsync(g_sweep_prof_ptr(), 0, sizeof h, st);
     }
 #endif

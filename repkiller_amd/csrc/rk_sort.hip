@@ -17,16 +17,6 @@ constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ROW = SCAN_THREADS * 4;  // 1024
 constexpr int SCAN_TILE = SCAN_ROW * 4;     // 4096
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return v;
-}
-
 __device__ __forceinline__ uint4 load4(const uint32_t *in, size_t base, size_t n) {
   if (base + 3 < n) return *reinterpret_cast<const uint4 *>(in + base);
   uint4 v = {0, 0, 0, 0};

@@ -355,6 +355,32 @@ def test_std_sort_rank_heap_vs_restatement(gpu_ctx):
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
 
 
+def test_killer_group_heap_segment_vs_oracle(gpu_ctx):
+    """A group whose in-group sort keys (|yStart - diag|, commonFunctions.cpp:
+    148-159) are a median-of-3 killer with 3 keys on its never-compared items:
+    copies of one X fragment (each hits the first on X) at yStart = Y0 + key,
+    then one more fragment of the same xStart bucket (another length: a group
+    of its own) at Y0, last in the file, which sets the bucket's diagonal to
+    Y0 (commonFunctions.cpp:161-177).  The record pipeline's group sort reaches
+    libstdc++'s depth-limit heapsort on the group (the rank path), its count
+    coming back with the call's final status word; the result against the
+    oracle."""
+    from sort_cases import heap_fallbacks, killer_with_keys
+    k = killer_with_keys(20000, 3, 31)
+    assert heap_fallbacks(k) > 0
+    n, y0 = k.size, 1_000_000
+    f = rk.Frags(np.full(n + 1, 5000, np.uint64), np.r_[y0 + k, y0].astype(np.uint64),
+                 np.r_[np.full(n, 200), 5000].astype(np.uint64),
+                 np.full(n + 1, ord('f'), np.uint8))
+    got = gpu_vs_oracle(gpu_ctx, f, 2_000_000, 2_000_000)
+    assert got.n_groups == 2
+    # the same set twice in one call (two ratio pairs share the scratch: each
+    # pair reads its heap count back on its own)
+    pairs = gpu_ctx.classify_pairs(f, 2_000_000, 2_000_000, [(0.3, 0.3), (0.3, 0.3)])
+    for r in pairs:
+        assert np.array_equal(r.out_order, got.out_order) and np.array_equal(r.gid, got.gid)
+
+
 def test_pipeline_choice(gpu_ctx, generic_ctx):
     """The record pipeline runs on the BASELINE-shaped sets; inputs it cannot
     represent (a length >= 2^24) take the generic one with the same result."""

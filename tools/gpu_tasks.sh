@@ -83,6 +83,12 @@ heap)  # the depth-limit heapsort: parity of the std::sort emulation, then the k
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v -k "std_sort" --timeout 300 --timeout-method thread > $O/heap_tests.log 2>&1 || exit 1
   timeout -k 10 600 python3 -u tools/heap_killer_check.py --tied ${@:-10000 100000 1000000} > $O/heap_killer.log 2>&1 || exit 2
   ;;
+sprof3)  # the window sweep's sampled phase cycles at cfg3 (RK_SWEEP_PROF build under tools/mb/prof)
+  RK_LIB=tools/mb/prof/librepkiller_amd.so bench sprof3 --no-cpu --steps 1 --warmup 0 || exit 1
+  ;;
+heapprof)  # kernel times of the tied killer (ARGS: sizes)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/hprof -o p -- python3 tools/heap_killer_check.py --tied ${@:-100000} > $O/hprof.log 2>&1 || exit 1
+  ;;
 abcfg5)  # parity, then cfg5 / cfg3 against the HEAD build under tools/mb/base, then the counters
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
   RK_LIB=repkiller_amd/librepkiller_amd.so bench new_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
