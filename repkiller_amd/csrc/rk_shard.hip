@@ -185,6 +185,13 @@ __global__ void __launch_bounds__(256) k_part_scatter(Op op, uint32_t n, uint32_
   }
 }
 
+// a plan that keeps every element for rank 0 in element order (world size 1,
+// nothing dropped): the emit at position i, no counts, scan or ballots
+template <class Op>
+__global__ void __launch_bounds__(256) k_part_identity(Op op, uint32_t n) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) op.emit(i, 0, i);
+}
+
 __global__ void k_totals(const uint32_t *off, uint32_t nblk, uint32_t P, uint32_t *tot) {
   const uint32_t d = threadIdx.x;
   if (d <= P) tot[d] = off[(size_t)d * nblk];
@@ -866,6 +873,23 @@ struct Shard {
     ++n_syncs;
     hip(hipStreamSynchronize(st), "d2h sync");
     return h;
+  }
+  // world size 1 with every element selected (known on the host): the
+  // identity plan, emitted by k_part_identity
+  template <class Op>
+  void emit_identity(const Op &op, uint32_t n, PartPlan &pp) {
+    identity_plan(n, pp);
+    kt_begin(st, KID_PART);
+    k_part_identity<<<grid_for(n, 256, 4096), 256, 0, st>>>(op, n);
+    kt_end(st, KID_PART, 0.0);
+    launched("k_part_identity");
+  }
+  void identity_plan(uint32_t n, PartPlan &pp) {
+    pp.n = n;
+    pp.nblk = 1;
+    for (uint32_t q = 0; q < MAXP; ++q) pp.cnt[q] = 0;
+    pp.cnt[0] = n;
+    pp.total = n;
   }
   // a plan that sends nothing (the op cannot select any element)
   void zero_plan(uint32_t n, PartPlan &pp) {

@@ -444,7 +444,10 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   // owner is a sum of its own bins -- the plan needs no readback
   RowOp16 rop{f, slice_keys, drop, (uint32_t)row_base, nullptr};
   PartPlan pp;
-  {
+  rop.out = S.take<uint4>(SN_SROWS, (size_t)nl + 1);  // room for every row (see plan_counts)
+  if (P == 1 && flags[25] == nl) {  // one rank, no row dropped: the records in row order
+    S.emit_identity(rop, nl, pp);
+  } else {
     uint64_t cnt[MAXP] = {};
     if (P == 1) {
       cnt[0] = flags[25];
@@ -457,9 +460,8 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
       }
     }
     S.plan_counts(rop, nl, pp, cnt);
+    S.emit(rop, pp);
   }
-  rop.out = S.take<uint4>(SN_SROWS, (size_t)nl + 1);  // room for every row (see plan_counts)
-  S.emit(rop, pp);
   uint32_t m = 0;
   const uint4 *rin = exchange_nw<uint4>(S, rop.out, pp, SN_RIN, &m);
   // every rank's slice size: known from the exchange's count all-gather
@@ -532,11 +534,10 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     yop.hi[q] = q < P ? (int64_t)yb.b[q + 1] + 1 + (int64_t)H : 0;
   }
   PartPlan ypp;
-  ypp.mcache = S.take<uint32_t>(SL_YMASK, m + 1);  // the X-hit bytes follow the same masks
-  if (P == 1) {  // one Y range, halos included: every record stays, count known
-    const uint64_t cnt1[1] = {m};
-    S.plan_counts(yop, m, ypp, cnt1);
+  if (P == 1) {  // one Y range, halos included: every record stays, in order
+    S.identity_plan(m, ypp);
   } else {
+    ypp.mcache = S.take<uint32_t>(SL_YMASK, m + 1);  // the X-hit bytes follow the same masks
     S.plan(yop, m, ypp);
   }
   // every own record stays here, once: the send layout is the records themselves
@@ -640,7 +641,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   if (nsuf) S.plan(gop, nsuf, pp);
   else S.zero_plan(0, pp);  // no row can reach a later slice: nothing to send
   gop.out = S.take<uint4>(SN_SHALO, pp.total + 1);
-  S.emit(gop, pp);
+  if (nsuf) S.emit(gop, pp);
   uint32_t G = 0;
   const uint4 *hx = exchange_nw<uint4>(S, gop.out, pp, SN_HX, &G);
   ss.x_ghosts = G;
@@ -747,11 +748,15 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     YOp12 xop = yop;
     xop.xg = xg;
     PartPlan xpp;
-    xpp.mcache = ypp.mcache;
-    xpp.mread = true;
-    S.plan_same(xop, m, xpp, ypp);  // the Y records' own selection: counts known
-    xop.xout = S.take<uint8_t>(SN_SXH, xpp.total + 1);
-    S.emit(xop, xpp);
+    xop.xout = S.take<uint8_t>(SN_SXH, (size_t)ypp.total + 1);
+    if (P == 1) {
+      S.emit_identity(xop, m, xpp);
+    } else {
+      xpp.mcache = ypp.mcache;
+      xpp.mread = true;
+      S.plan_same(xop, m, xpp, ypp);  // the Y records' own selection: counts known
+      S.emit(xop, xpp);
+    }
     uint32_t n2 = 0;
     const uint8_t *xh = exchange_nw<uint8_t>(S, xop.xout, xpp, SL_YXH, &n2);
     if (n2 != ny) {
