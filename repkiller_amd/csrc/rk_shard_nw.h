@@ -396,7 +396,31 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   uint32_t *hist = S.take<uint32_t>(SN_HIST, 3 * 4096);  // later the sorts' digit histograms
   S.zero(hist, NBINS * 4);
   S.zero(S.ctrl + 25, 4);
-  if (nl) {
+  // World size 1 (rows numbered from 0): the rows are read once, as on one
+  // device -- k_nw_order_hist takes the checks, the kept count and the order
+  // and Y digit histograms (into step 3's ahist / yhist) in the place of
+  // k_sh_rows, and when no row is dropped the order sort's first pass reads
+  // the rows themselves (no row records, no record histogram, no Y-record
+  // histogram).  RK_SH_ONE=0: the record route at world size 1 too.
+  static const bool one_on = [] {
+    const char *e = getenv("RK_SH_ONE");
+    return !(e && e[0] == '0');
+  }();
+  static const bool y_early_env = [] {
+    const char *e = getenv("RK_SH_YEARLY");
+    return e && e[0] == '1';
+  }();
+  const bool one = one_on && P == 1 && row_base == 0;
+  const NwDigits ad = nw_plan(bit_length(vsize - 1));
+  const NwDigits yd = nw_plan(bit_length(2ull * nby - 1), 9);
+  const NwOrderPlan op1 = one ? nw_order_split_range(nl, 0, drop) : NwOrderPlan{};
+  if (one) {
+    S.zero(hist, 3 * 4096 * 4);
+    S.zero(S.ctrl + 32, 16 * 4);
+    if (nl)
+      nw_order_hist(*in, vsize, max_x, max_y, nby, op1.nseg ? op1.coarse : ad, yd, hist,
+                    hist + 4096, S.ctrl + 32, st);
+  } else if (nl) {
     // more blocks when there is no slice histogram to flush (one rank)
     kt_begin(st, KID_SH_ROWKEYS);
     k_sh_rows<<<grid_for(nl, 256, P > 1 ? 1024 : 4096), 256, 0, st>>>(
@@ -407,13 +431,20 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   // the error bits (ctrl[0]), the pack flags (ctrl[20..21]), the kept count
   // (ctrl[25]) and the slice histogram in one readback, and the first two with
   // the histogram in one all-gather
-  std::vector<uint32_t> flags(26);
+  std::vector<uint32_t> flags(41);
   const uint32_t MW = 2 + (P > 1 ? NBINS : 0);  // message words
   std::vector<uint32_t> msg(MW);
-  S.hip(hipMemcpyAsync(flags.data(), S.ctrl, 26 * 4, hipMemcpyDeviceToHost, st), "d2h");
+  S.hip(hipMemcpyAsync(flags.data(), S.ctrl, (one ? 41 : 26) * 4, hipMemcpyDeviceToHost, st),
+        "d2h");
   if (P > 1) S.hip(hipMemcpyAsync(msg.data() + 2, hist, NBINS * 4, hipMemcpyDeviceToHost, st), "d2h");
   ++S.n_syncs;
   S.hip(hipStreamSynchronize(st), "d2h sync");
+  if (one) {  // k_nw_order_hist's words: [0] error bits, [1] kept, [3] no pack, [4] longest
+    flags[0] = flags[32];
+    flags[25] = flags[33];
+    flags[20] = flags[35];
+    flags[21] = flags[36];
+  }
   msg[0] = flags[0];
   msg[1] = flags[20] | (flags[21] << 1);
   std::vector<uint32_t> allm((size_t)P * MW);
@@ -445,7 +476,11 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   RowOp16 rop{f, slice_keys, drop, (uint32_t)row_base, nullptr};
   PartPlan pp;
   rop.out = S.take<uint4>(SN_SROWS, (size_t)nl + 1);  // room for every row (see plan_counts)
-  if (P == 1 && flags[25] == nl) {  // one rank, no row dropped: the records in row order
+  // (fast: step 3 reads the rows, rop.out is the fine kernel's scratch)
+  const bool fast = one && flags[25] == nl;
+  if (fast) {
+    S.identity_plan(nl, pp);
+  } else if (P == 1 && flags[25] == nl) {  // one rank, no row dropped: the records in row order
     S.emit_identity(rop, nl, pp);
   } else {
     uint64_t cnt[MAXP] = {};
@@ -478,10 +513,10 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   ss.n_slice = m;
 
   // ---- 3: the slice's processing order (one-sweep passes), its Y records
-  const NwDigits ad = nw_plan(bit_length(vsize - 1));
   uint32_t *ahist = S.take<uint32_t>(SN_HIST, 3 * 4096);  // order / Y / member digit histograms
   uint32_t *yhist = ahist + 4096, *ehist = ahist + 2 * 4096;
-  S.zero(ahist, 3 * 4096 * 4);
+  if (!fast) S.zero(ahist, 3 * 4096 * 4);  // (fast: the order and Y ones are in, ehist zero)
+  else if (y_early_env) S.zero(yhist, 4096 * 4);  // (that schedule counts the Y keys itself)
   const size_t sw = nw_status_words(m + 1);
   uint32_t *astat = S.take<uint32_t>(SN_STAT, sw);
   uint4 *Ra = S.take<uint4>(SN_RA, m + 1), *Rb = S.take<uint4>(SN_RB, m + 1);
@@ -490,7 +525,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   // slice's key density suits it: the slice holds m rows over its own key
   // span, and the coarse digits are slice-relative, (key - kbase) >> F, so the
   // segment table covers that span only
-  const NwOrderPlan op = nw_order_split_range(m, slice_keys.b[me], slice_keys.b[me + 1]);
+  const NwOrderPlan op = fast ? op1 : nw_order_split_range(m, slice_keys.b[me], slice_keys.b[me + 1]);
   ss.order_split = op.nseg ? 1u : 0u;
   // the X axis' chunk width (step 6) from the slice's own rows: the fine
   // kernel then counts the slice's X-chunk entries as it writes the order, and
@@ -505,16 +540,28 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     uint32_t *chist = S.take<uint32_t>(SN_CHIST, nw_seg_words(m));
     uint32_t *coff = S.take<uint32_t>(SN_COFF, nw_seg_words(m));
     own_cc.cnts = S.take<uint32_t>(SN_XCNT0, (size_t)3 * own_cc.nch + 2);
-    nw_rec_hist(rin, 16, m, op.kbase, op.coarse, ahist, st);
-    // rin is read by the first coarse pass only: the fine kernel's scratch
-    nw_order_sort_recs_split(rin, m, nby, poff, op, ahist, astat, Ra, Rb, yown,
-                             const_cast<uint4 *>(rin), chist, coff,
-                             S.scan_scratch(SL_PSCAN, (size_t)op.nseg + 1), &own_cc, st);
+    if (fast) {  // the rows themselves (op == op1, whose histogram is in)
+      nw_order_sort_split_coarse(*in, op, ahist, astat, Ra, Rb, chist,
+                                 ZeroRegion{own_cc.cnts, ((size_t)3 * own_cc.nch + 1) * 4}, vsize,
+                                 st, nullptr);
+      nw_order_sort_split_fine(nl, m, nby, op, Ra, Rb, yown, rop.out, chist, coff,
+                               S.scan_scratch(SL_PSCAN, (size_t)op.nseg + 1), &own_cc, st);
+    } else {
+      nw_rec_hist(rin, 16, m, op.kbase, op.coarse, ahist, st);
+      // rin is read by the first coarse pass only: the fine kernel's scratch
+      nw_order_sort_recs_split(rin, m, nby, poff, op, ahist, astat, Ra, Rb, yown,
+                               const_cast<uint4 *>(rin), chist, coff,
+                               S.scan_scratch(SL_PSCAN, (size_t)op.nseg + 1), &own_cc, st);
+    }
     own_counts = true;
     S.launched("order sort");
   } else if (m) {
-    nw_rec_hist(rin, 16, m, 0, ad, ahist, st);
-    nw_order_sort_recs(rin, m, nby, poff, ad, ahist, astat, Ra, Rb, yown, st);
+    if (fast) {
+      nw_order_sort(*in, vsize, nby, ad, ahist, astat, Ra, Rb, yown, st);
+    } else {
+      nw_rec_hist(rin, 16, m, 0, ad, ahist, st);
+      nw_order_sort_recs(rin, m, nby, poff, ad, ahist, astat, Ra, Rb, yown, st);
+    }
     S.launched("order sort");
   }
   ss.ms_ingress = ms_since(t0);
@@ -567,7 +614,6 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   cy.nbd = S.take<uint8_t>(SN_YNBD, ny + 1);
   cy.state = S.take<uint8_t>(SN_YST, ny + 1);
   uint32_t *ybits = S.take<uint32_t>(SN_XBITS, ny / 32 + 2);
-  const NwDigits yd = nw_plan(bit_length(2ull * nby - 1), 9);
   // the Y sort's passes read the received records (first pass: arrival
   // numbering) and ping-pong through yA / yB; the received array stays whole
   // for the winners' global ids
@@ -601,7 +647,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
   if (y_early) {
     y_sort(yr, ny, nullptr, sy, true, false);
     S.launched("Y sort head");
-  } else if (ny) {
+  } else if (ny && !fast) {  // (fast: counted by k_nw_order_hist over the same rows)
     nw_rec_hist(yr, 12, ny, 0, yd, yhist, sy);
   }
   S.hip(hipEventRecord(ctx->join, st2), "join");

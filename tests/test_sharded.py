@@ -229,6 +229,38 @@ def test_sharded_edge_fixtures(gpu_ctx, tmp_path):
             assert out.read_bytes() == f.read(), name
 
 
+@pytest.mark.parametrize("env", [None, {"RK_SH_ONE": "0"}, {"RK_SH_YEARLY": "1"}],
+                         ids=["one", "records", "y-early"])
+def test_sharded_world_one(gpu_ctx, tmp_path, env):
+    """World size 1: the rows read once as on one device (k_nw_order_hist in
+    place of the row checks, the order sort's first pass on the rows; a set
+    with a dropped last-bucket row or out-of-bounds rows takes the record
+    route), against the single device and the reference's edge fixtures;
+    RK_SH_ONE=0 forces the record route, RK_SH_YEARLY=1 the head-first Y
+    schedule."""
+    named = _edge_cases()
+    cases = SYNTH + [c for _, c in named]
+    got = run_ranks(1, cases, env=env)
+    for ci, case in enumerate(SYNTH):
+        order, gid, rep, ng, _ = assemble(got, ci, 1)
+        want, *_ = reference(gpu_ctx, case)
+        assert ng == want.n_groups, case
+        assert np.array_equal(order, want.out_order) and np.array_equal(gid, want.gid), case
+        assert np.array_equal(rep, want.repval), case
+    for cj, (name, case) in enumerate(named):
+        ci = len(SYNTH) + cj
+        if case["expect"] != "ref":
+            kind, code = got[(ci, 0)]
+            assert kind == "error" and code == ERR[case["expect"]], (name, kind, code)
+            continue
+        order, gid, rep, ng, _ = assemble(got, ci, 1)
+        db = rk.FragmentsDatabase(case["path"])
+        out = tmp_path / f"{name}.csv"
+        db.save_all_frag_pairs(str(out), rk.ClassifyResult(gid, rep, order, ng))
+        with open(os.path.join(EDGE, name + ".out.csv"), "rb") as f:
+            assert out.read_bytes() == f.read(), name
+
+
 def test_sharded_one_rank_fails(gpu_ctx):
     """A rank that fails locally takes its peers down with it (status word in
     the driver's all-gather message): the failing rank returns its own error,
