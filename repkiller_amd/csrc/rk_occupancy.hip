@@ -1177,6 +1177,7 @@ struct LongLds {
   uint2 npk[2][NCAP];
   uint32_t npos[2][NCAP], nent[2][NCAP];
   uint8_t nst[2][NCAP];
+  uint32_t ht[2][256];  // list_dedup's two hash tables (zero between calls)
 };
 
 // the entry-by-entry walk (k_sweep_wave's, on the 32-bit records) over
@@ -1301,6 +1302,56 @@ __device__ int list_dedup(LongLds &L, int nl, uint32_t lane, bool act, uint2 rec
     le[s] = lk[s] ? L.lent[k] : 0u;
     ls[s] = lk[s] ? L.lst[k] : (uint8_t)ST_HIT;
   }
+#ifndef RK_LDEDUP_HASH
+#define RK_LDEDUP_HASH 1
+#endif
+#if RK_LDEDUP_HASH
+  // Every ACTIVE entry by age (list position k: k; chunk lane: nl + lane; the
+  // larger the newer) into two 256-slot tables under two hashes of its
+  // record, the newest age per slot winning (atomicMax); an entry whose winner
+  // in either table is a newer entry with the same record is an older twin.
+  // A slot shared by two records can hide a twin -- it then stays, which is
+  // always allowed (only the list's room depends on the drops).  ~40
+  // instructions per entry where the rounds below took one round trip per
+  // distinct record (~2/3 of the cfg5 Y walk's cycles)
+  {
+    const auto h1 = [](uint2 r) { return (r.x * 0x9E3779B1u ^ r.y * 0x85EBCA77u) >> 24; };
+    const auto h2 = [](uint2 r) { return ((r.x ^ (r.y * 0xC2B2AE3Du)) * 0x27D4EB2Fu) >> 24; };
+    L.cpk[lane] = rec;  // (the chunk's records, for the winners' lookups)
+    wave_sync_lds();
+    const uint32_t ca = (uint32_t)nl + lane + 1;  // ages + 1 (0: an empty slot)
+    if (act) atomicMax(&L.ht[0][h1(rec)], ca), atomicMax(&L.ht[1][h2(rec)], ca);
+#pragma unroll
+    for (int s = 0; s < LS; ++s)
+      if (lk[s] && ls[s] == ST_ACTIVE) {
+        const uint32_t a = (uint32_t)((int)lane + 64 * s) + 1;
+        atomicMax(&L.ht[0][h1(lp[s])], a);
+        atomicMax(&L.ht[1][h2(lp[s])], a);
+      }
+    wave_sync_lds();
+    const auto twin = [&](uint2 r, uint32_t age1) {  // a newer ACTIVE entry with record r
+      bool t = false;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint32_t w = L.ht[k][k ? h2(r) : h1(r)];
+        if (w > age1) {
+          const uint2 o = w - 1 < (uint32_t)nl ? L.lpk[w - 1] : L.cpk[w - 1 - (uint32_t)nl];
+          t |= o.x == r.x && o.y == r.y;
+        }
+      }
+      return t;
+    };
+    if (act && twin(rec, ca)) keep = false;
+#pragma unroll
+    for (int s = 0; s < LS; ++s)
+      if (lk[s] && ls[s] == ST_ACTIVE && twin(lp[s], (uint32_t)((int)lane + 64 * s) + 1)) lk[s] = false;
+    wave_sync_lds();  // every table read is done: clear the slots written
+    if (act) L.ht[0][h1(rec)] = 0, L.ht[1][h2(rec)] = 0;
+#pragma unroll
+    for (int s = 0; s < LS; ++s)
+      if (ls[s] == ST_ACTIVE && (int)lane + 64 * s < nl) L.ht[0][h1(lp[s])] = 0, L.ht[1][h2(lp[s])] = 0;
+  }
+#else
   // one round per distinct record among the newest entries: the chunk's ACTIVE
   // lanes, newest first, then the list's ACTIVE entries newest first
   uint64_t a = __ballot(act);
@@ -1332,6 +1383,7 @@ __device__ int list_dedup(LongLds &L, int nl, uint32_t lane, bool act, uint2 rec
       b &= (v > 0 ? (1ull << v) - 1ull : 0ull);  // (continue below v)
     }
   }
+#endif
   uint64_t lb[LS];
   int nk = 0;
 #pragma unroll
@@ -1370,6 +1422,7 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
   __shared__ LongLds s_l[4];
   const uint32_t lane = threadIdx.x & 63;
   LongLds &L = s_l[threadIdx.x >> 6];
+  for (uint32_t j = lane; j < 2 * 256; j += 64) (&L.ht[0][0])[j] = 0;
   const uint32_t ngrp = (nwin + 63) / 64;
   uint32_t walked = 0;  // (one atomic per wave at the end: 4.6 M same-word atomics per
                         // launch at cfg5 cost the timed launch ~20 ms)
@@ -1534,8 +1587,81 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
         Scan fl{0.0, NONE, 0, false, false}, fn{0.0, NONE, 0, false, false};
         Q32 q{};
         bool coop = false;  // a neighbour query for the wavefront-wide scan
-        if (open) {
-          q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
+        // few open entries (cfg5's Y runs: ~1 per chunk, the list holding ~54
+        // ACTIVE X hits): the wavefront scans the chunk, the list and the
+        // neighbour list for each of them together, as below for an
+        // overflowed neighbour run; many (X: ~55 per chunk): a lane each
+        const uint64_t openm = __ballot(open);
+        const bool wide = __popcll(openm) <= 8;
+        if (open) q = make_q32(me.x, me.y, ax.len_ratio, ax.pos_ratio);
+        if (wide) {
+          for (uint64_t om = openm; om; om &= om - 1) {
+            const int v = __builtin_ctzll(om);
+            const uint32_t iv = __shfl(i, v);
+            const int ndv = __shfl((int)nd, v);
+            const Q32 qv{(uint32_t)__shfl((int)q.c, v), (uint32_t)__shfl((int)q.L, v),
+                         (uint32_t)__shfl((int)q.tl, v), (uint32_t)__shfl((int)q.tc, v),
+                         __shfl(q.ok ? 1 : 0, v) != 0, __shfl(q.eq ? 1 : 0, v) != 0};
+            // the chunk's earlier entries: one ballot
+            const uint64_t ro = __ballot((int)lane < v && m32(qv, L.cpk[lane]));
+            // the list (older chunks), newest first: the first strict maximum
+            // is the largest d, then the largest position
+            const auto best_of = [&](bool act, double d, int k, Scan &out, const uint32_t *ids) {
+              d = act ? d : -1.0;
+              k = act ? k : -1;
+              for (int o = 32; o > 0; o >>= 1) {
+                const double od = __shfl_xor(d, o);
+                const int ok = __shfl_xor(k, o);
+                if (od > d || (od == d && ok > k)) d = od, k = ok;
+              }
+              if (k >= 0) out.best = d, out.win = ids[k], out.any_active = true;
+            };
+            Scan sl{0.0, NONE, 0, false, false}, sn{0.0, NONE, 0, false, false};
+            {
+              bool unk = false, act = false;
+              double d = -1.0;
+              int kb = -1;
+#pragma unroll
+              for (int s2 = 0; s2 < LCAP / 64; ++s2) {
+                const int k = (int)lane + 64 * s2;
+                if (k >= nl) continue;
+                const uint2 o = L.lpk[k];
+                if (!m32(qv, o)) continue;
+                if (L.lst[k] != ST_ACTIVE) {
+                  unk = true;
+                  continue;
+                }
+                const double dk = dev32(qv, o, ax.len_ratio, ax.pos_ratio);
+                if (!act || dk > d || (dk == d && k > kb)) d = dk, kb = k;
+                act = true;
+              }
+              sl.any_unknown = __ballot(unk) != 0;
+              best_of(act, d, kb, sl, L.lent);
+            }
+            const int dir = ndv == 1 ? -1 : ndv == 2 ? 1 : 0;
+            const int sd = dir < 0 ? 0 : 1;
+            const int nn = dir < 0 ? nn0 : nn1;
+            if (dir != 0 && (dir < 0 ? has_lo : has_hi) && nn >= 0) {
+              bool unk = false, act = false;
+              double d = -1.0;
+              int kb = -1;
+              static_assert(NCAP == 64, "one neighbour-list entry per lane");
+              const int k = (int)lane;
+              if (k < nn && L.nent[sd][k] < iv && L.nst[sd][k] < ST_HIT_PENDING) {
+                const uint2 o = L.npk[sd][k];
+                if (m32(qv, o)) {
+                  if (L.nst[sd][k] != ST_ACTIVE) unk = true;
+                  else act = true, d = dev32(qv, o, ax.len_ratio, ax.pos_ratio), kb = k;
+                }
+              }
+              sn.any_unknown = __ballot(unk) != 0;
+              best_of(act, d, kb, sn, L.nent[sd]);
+            } else if (dir != 0 && (dir < 0 ? has_lo : has_hi)) {
+              if ((int)lane == v) coop = true;  // (overflowed: the scan below)
+            }
+            if ((int)lane == v) rown = ro, fl = sl, fn = sn;
+          }
+        } else if (open) {
           for (int j = 0; j < (int)lane; j += OWN_U) {
             uint64_t b4 = 0;
   #pragma unroll
