@@ -1416,7 +1416,12 @@ __device__ unsigned long long g_long_prof[24];
 #else
 #define LP_ADD(slot, v)
 #endif
-__global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lflag,
+#ifdef RK_LONG_WPE  // (measurement builds: wavefronts per SIMD the register budget allows)
+#define RK_LONG_ATTR __attribute__((amdgpu_waves_per_eu(RK_LONG_WPE)))
+#else
+#define RK_LONG_ATTR
+#endif
+__global__ void __launch_bounds__(256) RK_LONG_ATTR k_sweep_long32(Axis ax, uint8_t *lflag,
                                                       uint32_t nwin, uint8_t *rpend,
                                                       uint32_t *counters, uint32_t *work) {
   __shared__ LongLds s_l[4];
@@ -1483,7 +1488,7 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
 #endif
       if (fo == NONE) {
         LP_ADD(10, 1);
-        if (lane == 0) rpend[beg] = 0;
+        if (lane == 0) rpend[beg] = 0, lflag[w] = 0;  // (later sweeps skip the window)
         continue;
       }
       uint32_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0;
@@ -1686,19 +1691,27 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
           const int nn = dir < 0 ? nn0 : nn1;
           if (dir != 0 && (dir < 0 ? has_lo : has_hi)) {
             if (nn >= 0) {
-              for (int k = nn - 1; k >= 0; --k) {  // newest first
-                if (L.nent[sd][k] >= i) continue;
-                const uint8_t sk = L.nst[sd][k];
-                if (sk >= ST_HIT_PENDING) continue;
-                const uint2 o = L.npk[sd][k];
-                if (!m32(q, o)) continue;
-                if (sk != ST_ACTIVE) {
-                  fn.any_unknown = true;
-                  continue;
+              // newest first, four entries per step (their LDS reads together)
+              for (int k0 = nn - 1; k0 >= 0; k0 -= 4) {
+                uint32_t ek[4];
+                uint8_t sk[4];
+                uint2 ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  const int k = k0 - u >= 0 ? k0 - u : 0;
+                  ek[u] = L.nent[sd][k], sk[u] = L.nst[sd][k], ok[u] = L.npk[sd][k];
                 }
-                const double d = dev32(q, o, ax.len_ratio, ax.pos_ratio);
-                if (d > fn.best) fn.best = d, fn.win = L.nent[sd][k];
-                fn.any_active = true;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  if (k0 - u < 0 || ek[u] >= i || sk[u] >= ST_HIT_PENDING || !m32(q, ok[u])) continue;
+                  if (sk[u] != ST_ACTIVE) {
+                    fn.any_unknown = true;
+                    continue;
+                  }
+                  const double d = dev32(q, ok[u], ax.len_ratio, ax.pos_ratio);
+                  if (d > fn.best) fn.best = d, fn.win = ek[u];
+                  fn.any_active = true;
+                }
               }
             } else {  // list overflow: the wavefront scans the neighbour run (below)
               coop = true;
@@ -1809,6 +1822,7 @@ __global__ void __launch_bounds__(256) k_sweep_long32(Axis ax, const uint8_t *lf
       if (lane == 0) {
         rpend[beg] = pend;
         if (pend) atomicAdd(&counters[w % PEND_SLOTS], 1u);
+        else lflag[w] = 0;  // a decided run: later sweeps skip its window at the flag load
       }
     }
   }
@@ -1963,7 +1977,7 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     // id (4 B), state read and write (2 B) and winner (4 B)
     uint32_t *work = kt_units(st, KID_SWEEP_LONG);  // (its clear ahead of the start event)
     kt_begin(st, KID_SWEEP_LONG);
-    k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<const uint8_t *>(rl.big), rl.nwin,
+    k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<uint8_t *>(rl.big), rl.nwin,
                                          rpend, counters, work);
     kt_end_units(st, KID_SWEEP_LONG, 18.0);
 #ifdef RK_SWEEP_PROF

@@ -83,6 +83,13 @@ heap)  # the depth-limit heapsort: parity of the std::sort emulation, then the k
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v -k "std_sort" --timeout 300 --timeout-method thread > $O/heap_tests.log 2>&1 || exit 1
   timeout -k 10 600 python3 -u tools/heap_killer_check.py --tied ${@:-10000 100000 1000000} > $O/heap_killer.log 2>&1 || exit 2
   ;;
+abw5)  # k_sweep_long32 at 5 wavefronts per SIMD (tools/mb/w5) against the working tree at cfg5
+  RK_LIB=tools/mb/w5/librepkiller_amd.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q -k "long or synthetic" --timeout 300 --timeout-method thread > $O/parity_w5.log 2>&1 || exit 1
+  for rep in 1 2; do
+    RK_LIB=tools/mb/w5/librepkiller_amd.so bench w5_cfg5_$rep --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 2
+    RK_LIB=repkiller_amd/librepkiller_amd.so bench main_cfg5_$rep --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 3
+  done
+  ;;
 sprof3)  # the window sweep's sampled phase cycles at cfg3 (RK_SWEEP_PROF build under tools/mb/prof)
   RK_LIB=tools/mb/prof/librepkiller_amd.so bench sprof3 --no-cpu --steps 1 --warmup 0 || exit 1
   ;;
