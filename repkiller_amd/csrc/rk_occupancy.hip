@@ -1724,6 +1724,10 @@ __global__ void __launch_bounds__(256) RK_LONG_ATTR k_sweep_long32(Axis ax, uint
         // entry: on cfg5's Y axis, where a family copy's runs straddle bucket
         // bounds and hold hundreds of ACTIVE X hits, that walk took most of
         // the kernel's time.)
+#ifdef RK_SWEEP_PROF
+        const uint64_t lp_c0 = __builtin_amdgcn_s_memtime();
+        LP_ADD(18, __popcll(__ballot(coop)));
+#endif
         for (uint64_t cm = __ballot(coop); cm; cm &= cm - 1) {
           const int v = __builtin_ctzll(cm);
           const int dv = __shfl(nd == 1 ? -1 : 1, v);
@@ -1761,6 +1765,9 @@ __global__ void __launch_bounds__(256) RK_LONG_ATTR k_sweep_long32(Axis ax, uint
           if (cs.any_active) cs.win = ax.ent[bestg];
           if ((int)lane == v) fn = cs;
         }
+#ifdef RK_SWEEP_PROF
+        LP_ADD(17, __builtin_amdgcn_s_memtime() - lp_c0);
+#endif
         const bool out_act = fl.any_active || fn.any_active;
         const bool out_unk = fl.any_unknown || fn.any_unknown;
         for (;;) {
@@ -1987,9 +1994,10 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_long_prof), sizeof h);
       fprintf(stderr, "first=%d ", (int)first);
       const double c = h[2] ? (double)h[2] : 1.0;
-      fprintf(stderr, "LONGPROF m=%u runs=%llu entries=%llu chunks=%llu open/chunk %.2f list/chunk %.1f overflow runs=%llu walked=%llu | Mcyc run-find %.1f prescan %.1f nbounds %.1f nlists %.1f chunks %.1f walk %.1f | dedup drops=%llu | runs without open entries %llu, list-only chunks %llu, overflowed neighbour lists %llu\n",
+      fprintf(stderr, "LONGPROF m=%u runs=%llu entries=%llu chunks=%llu open/chunk %.2f list/chunk %.1f overflow runs=%llu walked=%llu | Mcyc run-find %.1f prescan %.1f nbounds %.1f nlists %.1f chunks %.1f walk %.1f | dedup drops=%llu | runs without open entries %llu, list-only chunks %llu, overflowed neighbour lists %llu | wavefront neighbour scans %llu, %.1f Mcyc\n",
               ax.m, h[0], h[1], h[2], h[3] / c, h[4] / c, h[5], h[6], h[16] / 1e6, h[12] / 1e6,
-              h[13] / 1e6, h[14] / 1e6, h[7] / 1e6, h[8] / 1e6, h[9], h[10], h[11], h[15]);
+              h[13] / 1e6, h[14] / 1e6, h[7] / 1e6, h[8] / 1e6, h[9], h[10], h[11], h[15], h[18],
+              h[17] / 1e6);
       void *p = nullptr;
       (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_long_prof));
       (void)hipMemsetAsync(p, 0, sizeof h, st);
