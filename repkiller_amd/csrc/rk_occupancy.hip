@@ -1416,7 +1416,14 @@ __device__ unsigned long long g_long_prof[24];
 #else
 #define LP_ADD(slot, v)
 #endif
-#ifdef RK_LONG_WPE  // (measurement builds: wavefronts per SIMD the register budget allows)
+// 5 wavefronts per SIMD (96 VGPRs, a few spilled; 119 without the bound, 4
+// per SIMD): the walk is latency-bound, and its LDS (28.8 KB per block)
+// allows 5 blocks per CU.  cfg5: 66.1 -> 63.7 ms per step (two A/B pairs,
+// `tools/gpu_tasks.sh abw5`).  RK_LONG_WPE=0 at build time: unbounded
+#ifndef RK_LONG_WPE
+#define RK_LONG_WPE 5
+#endif
+#if RK_LONG_WPE > 0
 #define RK_LONG_ATTR __attribute__((amdgpu_waves_per_eu(RK_LONG_WPE)))
 #else
 #define RK_LONG_ATTR

@@ -90,21 +90,6 @@ abw5)  # k_sweep_long32 at 5 wavefronts per SIMD (tools/mb/w5) against the worki
     RK_LIB=repkiller_amd/librepkiller_amd.so bench main_cfg5_$rep --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 3
   done
   ;;
-abmid)  # phase A' (LDS partitioning of 513..MID_T-member segments): parity, cfg5q digests, cfg5 against tools/mb/base (RK_MID_T=0)
-  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
-  timeout -k 10 900 python3 -u -m pytest tests/test_large_configs.py -x -v -k cfg5q --timeout 600 --timeout-method thread > $O/cfg5q.log 2>&1 || exit 2
-  for rep in 1 2; do
-    RK_LIB=repkiller_amd/librepkiller_amd.so bench new_cfg5_$rep --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 3
-    RK_LIB=tools/mb/base/librepkiller_amd.so bench base_cfg5_$rep --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 4
-  done
-  ;;
-abyb)  # the Y sort beside the X sweeps (RK_Y_BESIDE, tools/mb/yb): parity with it on, then cfg3 off / on interleaved
-  RK_Y_BESIDE=1 RK_LIB=tools/mb/yb/librepkiller_amd.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
-  for rep in 1 2 3; do
-    RK_Y_BESIDE=0 RK_LIB=tools/mb/yb/librepkiller_amd.so bench off_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 2
-    RK_Y_BESIDE=1 RK_LIB=tools/mb/yb/librepkiller_amd.so bench on_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 3
-  done
-  ;;
 sprof3)  # the window sweep's sampled phase cycles at cfg3 (RK_SWEEP_PROF build under tools/mb/prof)
   RK_LIB=tools/mb/prof/librepkiller_amd.so bench sprof3 --no-cpu --steps 1 --warmup 0 || exit 1
   ;;
