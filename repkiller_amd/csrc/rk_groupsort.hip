@@ -1093,20 +1093,38 @@ struct HeapSeg {
 };
 constexpr uint32_t HEAPQ_CAP = 512;
 
+// The groups are claimed one at a time (claim[0..1], zeroed): first every
+// group of at least `big` members, then the rest -- the largest jobs first, so
+// no block is left with a large group at the end (a static round-robin
+// share of ~18 groups per block left the launch waiting on its heaviest
+// blocks).  big = 0: one dynamic pass in list order; claim null: the static
+// round-robin.
 __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tier,
                                                            const uint32_t *goff, uint64_t *key,
                                                            uint32_t *tag, uint32_t *otag,
                                                            uint32_t *pl, uint32_t *pr,
                                                            uint8_t *bnd, uint32_t *heapq_n,
-                                                           HeapSeg *heapq) {
+                                                           HeapSeg *heapq, uint32_t *claim,
+                                                           uint32_t big) {
   __shared__ Frame stack[SPLIT_STACK];
   __shared__ uint32_t s_w[16];
   const uint32_t tid = threadIdx.x;
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
-  for (uint32_t w = lo + blockIdx.x; w < hi; w += gridDim.x) {
+  if (lo == hi) return;
+  const int npass = claim ? (big ? 2 : 1) : 1;
+  for (int pass = 0; pass < npass; ++pass)
+  for (uint32_t w = lo + blockIdx.x;; w += gridDim.x) {
+    if (claim) {
+      if (tid == 0) s_w[11] = lo + atomicAdd(&claim[pass], 1u);
+      __syncthreads();
+      w = s_w[11];
+      __syncthreads();  // (read by every thread before the next claim)
+    }
+    if (w >= hi) break;
     const uint32_t g = tl.list[w];
     const uint32_t b = goff[g], n = goff[g + 1] - b;
+    if (claim && big && (n >= big) != (pass == 0)) continue;
     uint64_t *K = key + b;
     uint32_t *T = tag + b;
     // the tags (positions) written here: phase A moves them in memory, phase
@@ -2000,10 +2018,20 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   // phase A marks the final segments' starts in bnd (cleared first); both
   // kernels return at once when no group is that large
   k_clear_if_tier<<<1024, 256, 0, st>>>(tl, NTIER - 1, bnd, m);
-  (void)hipMemsetAsync(heapq_n, 0, 4, st);
+  (void)hipMemsetAsync(heapq_n, 0, 12, st);  // the heap count and the two claim counters
+  // RK_SPLIT_DYN=0: the static round-robin; RK_SPLIT_BIG: the first pass' size
+  static const bool split_dyn = [] {
+    const char *e = getenv("RK_SPLIT_DYN");
+    return !(e && e[0] == '0');
+  }();
+  static const uint32_t split_big = [] {
+    const char *e = getenv("RK_SPLIT_BIG");
+    return e ? (uint32_t)atoi(e) : 65536u;
+  }();
   kt_begin(st, KID_SORT_GLOBAL);
   k_sort_groups_split<<<2048, 256, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
-                                            heapq_n, heapq);
+                                            heapq_n, heapq, split_dyn ? heapq_n + 1 : nullptr,
+                                            split_big);
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
   // the heap segments (libstdc++'s depth-limit fallback on 2048+ members: a

@@ -17,6 +17,7 @@
 #             library interleaved with tools/mb/base (a build of an earlier
 #             HEAD) through RK_LIB
 #   abenv     the same with environment variants: ARGS = "VAR=a" "VAR=b" ...
+#   abenv5    parity + cfg5q digests, then cfg5 with environment variants
 #   trace     per-tile phase times of every record pass (RK_NW_TRACE)
 #   shard     sharded parity tests (+ the large sharded digests with ARGS=large)
 #             and the world-1 sharded bench
@@ -141,6 +142,17 @@ abenv)
     for E in "$@"; do
       i=$((i+1))
       env $E timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $O/v${i}_$rep.json 2> $O/v${i}_$rep.err || exit 2
+    done
+  done
+  ;;
+abenv5)  # parity + the cfg5q digests, then cfg5 with environment variants (ARGS: "VAR=a" "VAR=b" ...) interleaved, two rounds
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  timeout -k 10 900 python3 -u -m pytest tests/test_large_configs.py -x -v -k cfg5q --timeout 600 --timeout-method thread > $O/cfg5q.log 2>&1 || exit 2
+  for rep in 1 2; do
+    i=0
+    for E in "$@"; do
+      i=$((i+1))
+      env $E timeout -k 10 600 python3 bench.py --config cfg5 --no-cpu --steps 3 --warmup 1 > $O/v${i}_$rep.json 2> $O/v${i}_$rep.err || exit 3
     done
   done
   ;;
