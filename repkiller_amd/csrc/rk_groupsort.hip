@@ -33,6 +33,7 @@
 // In every tier the result goes to `otag` (member order, group-major).
 #include "rk_internal.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -1926,7 +1927,12 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     const uint32_t cap = caps.c[j];
     // (more blocks than stay resident: a grid capped at the resident blocks, or
     // half of them, was slower -- group-sort phase 1.275 / 1.37 against 1.20 ms)
-    const uint32_t waves = cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048;
+    static const uint32_t gs_mul = [] {  // RK_GS_WAVES_MUL: the grids below x this
+      const char *e = getenv("RK_GS_WAVES_MUL");
+      const int v = e ? atoi(e) : 1;
+      return v > 0 ? (uint32_t)v : 1u;
+    }();
+    const uint32_t waves = (cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048) * gs_mul;
     const int wp = cap <= 512 ? wpb : 1;
     const size_t slab = (lds_bytes(cap, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
     kt_begin(sj, KID_SORT_LDS);
@@ -2065,12 +2071,23 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
         k_sort_segments<uint64_t, 4><<<2048, 256, 4 * slab, st>>>(
             tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
     } else {
+      // Each wavefront scans a fixed 1/grid of the positions: a grid many
+      // times the resident wavefronts (~19 per CU) lets the hardware balance
+      // the segments' uneven work as wavefronts finish -- one wavefront per
+      // 8192 members, 8192 .. 131072 (cfg5: 8192 -> 131072 wavefronts, phase
+      // B 47.6 -> 38.5 ms; cfg3 has no phase B).  RK_SEG_WAVES: a fixed grid
+      static const int seg_env = [] {
+        const char *e = getenv("RK_SEG_WAVES");
+        return e ? atoi(e) : 0;
+      }();
+      const int seg_waves =
+          seg_env > 0 ? seg_env : (int)std::min(131072u, std::max(8192u, m / 8192));
       if (narrow_keys)
-        k_sort_segments<uint32_t, 1><<<8192, 64, slab, st>>>(tl, NTIER - 1, m, bnd, pl, key, tag,
-                                                             otag, reg_max, (uint32_t)slab);
+        k_sort_segments<uint32_t, 1><<<seg_waves, 64, slab, st>>>(
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
       else
-        k_sort_segments<uint64_t, 1><<<8192, 64, slab, st>>>(tl, NTIER - 1, m, bnd, pl, key, tag,
-                                                             otag, reg_max, (uint32_t)slab);
+        k_sort_segments<uint64_t, 1><<<seg_waves, 64, slab, st>>>(
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
     }
   }
   kt_end(st, KID_SORT_SEGS, 0.0);

@@ -42,6 +42,7 @@
 // the reference's expression shape; this TU is built with -ffp-contract=off so
 // 0.4*sl + 0.6*sp is never fused (the reference binary is baseline x86-64).
 #include "rk_internal.h"
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -1990,9 +1991,21 @@ void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t
     // algorithmic bytes per entry of a walked run: its packed record (8 B),
     // id (4 B), state read and write (2 B) and winner (4 B)
     uint32_t *work = kt_units(st, KID_SWEEP_LONG);  // (its clear ahead of the start event)
+    // blocks: the 64-window groups go round-robin over them, so a grid many
+    // times the resident blocks (5 per CU) lets the hardware balance the
+    // uneven groups -- one block per 8 groups, 2048 .. 32768 (cfg5: 2048 ->
+    // 32768 blocks, 63.7 -> 55.6 ms per step; cfg3 keeps 2048).
+    // RK_LONG_GRID: a fixed grid
+    static const int long_env = [] {
+      const char *e = getenv("RK_LONG_GRID");
+      return e ? atoi(e) : 0;
+    }();
+    const int long_grid =
+        long_env > 0 ? long_env
+                     : (int)std::min(32768u, std::max(2048u, (rl.nwin + 63) / 64 / 8));
     kt_begin(st, KID_SWEEP_LONG);
-    k_sweep_long32<<<2048, 256, 0, st>>>(ax, reinterpret_cast<uint8_t *>(rl.big), rl.nwin,
-                                         rpend, counters, work);
+    k_sweep_long32<<<long_grid, 256, 0, st>>>(ax, reinterpret_cast<uint8_t *>(rl.big), rl.nwin,
+                                              rpend, counters, work);
     kt_end_units(st, KID_SWEEP_LONG, 18.0);
 #ifdef RK_SWEEP_PROF
     {  // every sweep (first=1: the first of the axis)
