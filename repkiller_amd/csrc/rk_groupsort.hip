@@ -1926,10 +1926,14 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   auto launch_lds = [&](int j, hipStream_t sj) {
     const uint32_t cap = caps.c[j];
     // (more blocks than stay resident: a grid capped at the resident blocks, or
-    // half of them, was slower -- group-sort phase 1.275 / 1.37 against 1.20 ms)
-    static const uint32_t gs_mul = [] {  // RK_GS_WAVES_MUL: the grids below x this
+    // half of them, was slower -- group-sort phase 1.275 / 1.37 against 1.20 ms;
+    // a larger one is faster, below)
+    // x4 (RK_GS_WAVES_MUL): cfg3's group-sort phase 1.070 / 1.073 -> 1.027 /
+    // 1.032 ms (x2: 1.032 / 1.037), the hardware balancing the static group
+    // shares as wavefronts finish (`gpurun_out` r5gs)
+    static const uint32_t gs_mul = [] {
       const char *e = getenv("RK_GS_WAVES_MUL");
-      const int v = e ? atoi(e) : 1;
+      const int v = e ? atoi(e) : 4;
       return v > 0 ? (uint32_t)v : 1u;
     }();
     const uint32_t waves = (cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048) * gs_mul;
