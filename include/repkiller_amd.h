@@ -223,6 +223,13 @@ typedef struct {
   uint32_t host_syncs;       /* host waits for the device stream (readbacks) this call */
   uint32_t agree_skipped;    /* receive-buffer agreements skipped: every rank's buffer
                                 was already large enough */
+  uint32_t fast_path;        /* 1: the call started on the fast path (sizes agreed up front
+                                through device-assembled messages, rk_shard_fast.h) */
+  uint32_t fast_retry;       /* 1: the fast attempt found a halo disagreement or an axis
+                                left open and the careful driver repeated the call */
+  uint32_t fast_stages;      /* fast-path stages run without agreement points (bits:
+                                1 axes, 2 parents + first roots round, 4 later rounds
+                                + members) */
 } rk_shard_stats;
 
 /* in_dev: this rank's block of input rows (device SoA, FILE order); blocks are

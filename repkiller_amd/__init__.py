@@ -125,7 +125,8 @@ class ShardStats(ctypes.Structure):
                 ("ms_members", ctypes.c_double), ("generic_driver", ctypes.c_uint32),
                 ("order_split", ctypes.c_uint32), ("gathers", ctypes.c_uint32),
                 ("exchanges", ctypes.c_uint32), ("host_syncs", ctypes.c_uint32),
-                ("agree_skipped", ctypes.c_uint32)]
+                ("agree_skipped", ctypes.c_uint32), ("fast_path", ctypes.c_uint32),
+                ("fast_retry", ctypes.c_uint32), ("fast_stages", ctypes.c_uint32)]
 
 
 class SynthParams(ctypes.Structure):

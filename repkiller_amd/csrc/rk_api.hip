@@ -150,6 +150,28 @@ int resolve_axis(rk_ctx *ctx, const Axis &ax, SweepScratch sc, bool fast32, uint
   return RK_OK;
 }
 
+__global__ void k_pend_flag(const uint32_t *counters, uint32_t *pend) {
+  uint32_t s = 0;
+  for (uint32_t k = threadIdx.x; k < PEND_WORDS; k += 64) s |= counters[k];
+  if (__ballot(s != 0) && threadIdx.x == 0) *pend = 1u;
+}
+
+// `sweeps` sweeps of a 32-bit axis queued without a host round trip, then the
+// pending count folded into *pend (left alone when the axis is final): the
+// sharded driver's fast path reads it with its next all-gather and repeats the
+// call the careful way if any axis was left open
+int resolve_axis_queued(rk_ctx *ctx, const Axis &ax, SweepScratch sc, uint32_t sweeps,
+                        uint32_t *pend) {
+  if (!ax.m) return RK_OK;
+  RunList rl{sc.runs, sc.wpend, 0, 0, true};
+  build_runs(ax, rl, sc.dev_count, ctx->host + 128, ctx->stream);  // (32-bit: no readback)
+  for (uint32_t s = 0; s < sweeps; ++s)
+    occupancy_sweep(ax, rl, sc.rpend, sc.counters, s == 0, ctx->stream);
+  k_pend_flag<<<1, 64, 0, ctx->stream>>>(sc.counters, pend);
+  HIPCHK(ctx, hipGetLastError());
+  return RK_OK;
+}
+
 }  // namespace rk
 
 static const char *kPhaseNames[RK_N_PHASES] = {
@@ -697,9 +719,12 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     // one pair: the depth-limit heap segments' count (crafted inputs only)
     // comes back with the final status word (ctrl[33]) instead of a wait of
     // its own (several pairs share the scratch: each waits)
-    rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
-                          ctx->host + 128, narrow_keys, st, st2, ctx->fork, ctx->join,
-                          npairs == 1 ? w.ctrl + 33 : nullptr);
+    if ((rc = rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
+                                    ctx->host + 128, narrow_keys, st, st2, ctx->fork, ctx->join,
+                                    npairs == 1 ? w.ctrl + 33 : nullptr))) {
+      ctx->err = "depth-limit heap segments: buffer allocation failed";
+      return rc;
+    }
     if (prof) mark(ctx, RK_PH_EMIT);
     rk::emit_result(w.otag, w.sgid, w.goff, w.mrow, m, out->gid, out->repval, out->out_order,
                     st);
@@ -710,8 +735,11 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   if ((rc = readback(ctx, w.ctrl, npairs == 1 ? 34 : 1))) return rc;
   if (npairs == 1 && m && ctx->host[33]) {  // heap segments: sorted now, then the result again
     const uint32_t G = outs[0].n_groups;
-    rk::sort_groups_heap_deferred(G, m, w.reckey, w.tag, w.otag, w.gsort, ctx->host[33],
-                                  ctx->host + 128, st);
+    if ((rc = rk::sort_groups_heap_deferred(G, m, w.reckey, w.tag, w.otag, w.gsort, ctx->host[33],
+                                            ctx->host + 128, st))) {
+      ctx->err = "depth-limit heap segments: buffer allocation failed";
+      return rc;
+    }
     rk::emit_result(w.otag, w.sgid, w.goff, w.mrow, m, outs[0].gid, outs[0].repval,
                     outs[0].out_order, st);
     HIPCHK(ctx, hipGetLastError());
@@ -765,6 +793,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   }
   HIPCHK(ctx, hipSetDevice(ctx->device));
   std::memset(&ctx->stats, 0, sizeof ctx->stats);
+  rk::stats_numa_unknown(&ctx->stats);
   hipStream_t st = ctx->stream;
   const rk_params *prm = &prms[0];
 
@@ -798,6 +827,7 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (ctx->profiling) ctx->kt.n = 0;  // the timings of the abandoned attempt
     const uint32_t why = ctx->stats.record_fallback;
     std::memset(&ctx->stats, 0, sizeof ctx->stats);
+    rk::stats_numa_unknown(&ctx->stats);
     ctx->stats.record_fallback = why;
   }
   Work w{};  // value-initialised: optional Proc columns (grow, ...) stay null
@@ -910,8 +940,12 @@ int classify_device(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     rk::group_offsets(w.sgid, m, G, w.goff, st);
     rk::build_records(w.gmem, w.p.hrec, m, w.reckey, w.tag, st);
     if (prof) mark(ctx, RK_PH_GROUP_SORT);
-    rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
-                          ctx->host + 128, narrow_keys, st, ctx->stream2, ctx->fork, ctx->join);
+    if ((rc = rk::sort_groups_exact(w.sgid, w.goff, G, m, w.reckey, w.tag, w.otag, w.gsort, ss,
+                                    ctx->host + 128, narrow_keys, st, ctx->stream2, ctx->fork,
+                                    ctx->join))) {
+      ctx->err = "depth-limit heap segments: buffer allocation failed";
+      return rc;
+    }
     if (prof) mark(ctx, RK_PH_EMIT);
     rk::emit_result(w.otag, w.sgid, w.goff, w.gmem, m, out->gid, out->repval,
                     out->out_order, st);
@@ -1008,6 +1042,7 @@ extern "C" void rk_destroy(rk_ctx *ctx) {
   for (void *p : ctx->pool.ptr)
     if (p) (void)hipFree(p);
   if (ctx->host) (void)hipHostFree(ctx->host);
+  if (ctx->sh_msg) (void)hipHostFree(ctx->sh_msg);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   for (auto &e : ctx->pev)
@@ -1141,15 +1176,17 @@ extern "C" int rk_std_sort_segments(rk_ctx *ctx, const uint64_t *keys, uint64_t 
     for (uint32_t x = 0; x < m; ++x) narrow &= (keys[x] >> 32) == 0;
     // one-element segments are not written by the group sort: their slot stays
     (void)hipMemcpyAsync(dot, dt, M * 4, hipMemcpyDeviceToDevice, st);
-    rk::sort_groups_exact(dg, doff, nseg, m, dk, dt, dot, dgs, rk::ScanScratch{dsc, sc},
-                          ctx->host + 128, narrow, st);
-    if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(perm, dot, M * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+    rc = rk::sort_groups_exact(dg, doff, nseg, m, dk, dt, dot, dgs, rk::ScanScratch{dsc, sc},
+                               ctx->host + 128, narrow, st);
+    if (!rc && (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(perm, dot, M * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
       rc = RK_E_HIP;
   }
+  (void)hipStreamSynchronize(st);
   (void)hipFree(buf);
-  if (rc) ctx->err = "rk_std_sort_segments: HIP failure";
+  if (rc == RK_E_NOMEM) ctx->err = "rk_std_sort_segments: heap-segment buffer allocation failed";
+  else if (rc) ctx->err = "rk_std_sort_segments: HIP failure";
   return rc;
 }
 

@@ -116,6 +116,32 @@ struct RcclComm final : rk_comm {
     return RK_OK;
   }
 
+  // the message is gathered on the device (no host-to-device leg) and comes
+  // down in one copy: a single wait for the stream
+  int allgather_dev(const void *dsend, void *recv, size_t bytes, hipStream_t st) override {
+    if (!bytes) return RK_OK;
+    hipError_t e;
+    if (size == 1) {
+      e = hipMemcpyAsync(recv, dsend, bytes, hipMemcpyDeviceToHost, st);
+    } else {
+      const size_t need = bytes * (size_t)size;
+      if (need > stage_cap) {
+        if (stage) (void)hipFree(stage);
+        stage = nullptr;
+        stage_cap = 0;
+        e = hipMalloc(&stage, need);
+        if (e != hipSuccess) return fail_hip("hipMalloc", e);
+        stage_cap = need;
+      }
+      ncclResult_t r = rccl().AllGather(dsend, stage, bytes, ncclUint8, comm, st);
+      if (r != ncclSuccess) return fail("ncclAllGather", r);
+      e = hipMemcpyAsync(recv, stage, need, hipMemcpyDeviceToHost, st);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail_hip("hipMemcpyAsync", e);
+    return RK_OK;
+  }
+
   int alltoallv(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb,
                 hipStream_t st) override {
     const RcclApi &api = rccl();

@@ -47,6 +47,16 @@ struct rk_ctx {
   size_t io_cap = 0;
   rk::IoEngine *ioe = nullptr;
   rk_pool pool;  // rk_classify_sharded buffers
+  // the sharded driver's fast path (rk_shard_fast.h): its all-gather messages
+  // (pinned, every rank's), the stage fingerprints of the last call that
+  // completed on it (a stage whose gathered counts match needs no agreement
+  // before its exchanges: every buffer it takes already has its size), and the
+  // sweeps it queues per axis before one deferred pending check
+  char *sh_msg = nullptr;
+  size_t sh_msg_cap = 0;
+  uint64_t sh_fp[8] = {};
+  uint32_t sh_blind[2] = {3, 3};
+  uint32_t sh_jumps = 1;  // pointer-jumping rounds it queues
   rk_stats stats{};
   rk_shard_stats shard_stats{};
   std::string err;
@@ -119,6 +129,10 @@ void gids_from_flags_async(const uint8_t *flag, size_t n, uint32_t *gid, int thr
 void io_destroy(rk_ctx *ctx);
 // the NUMA nodes of the last upload (rk_stats numa_*)
 void io_numa_stats(const rk_ctx *ctx, rk_stats *st);
+// a call without an upload of its own: every NUMA field unknown (-1)
+inline void stats_numa_unknown(rk_stats *st) {
+  st->numa_input = st->numa_threads = st->numa_staging = st->numa_gpu = -1;
+}
 bool host_pinned(const void *p);
 double wall_ms();
 
@@ -139,5 +153,9 @@ struct SweepScratch {
 };
 // run sweeps on one axis until no bucket has undecided entries
 int resolve_axis(rk_ctx *ctx, const Axis &ax, SweepScratch sc, bool fast32, uint32_t *sweeps);
+// `sweeps` sweeps of a 32-bit axis with no host round trip; *pend = 1 (device)
+// when entries are still undecided after them
+int resolve_axis_queued(rk_ctx *ctx, const Axis &ax, SweepScratch sc, uint32_t sweeps,
+                        uint32_t *pend);
 
 }  // namespace rk

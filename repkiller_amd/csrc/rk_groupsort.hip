@@ -1543,16 +1543,34 @@ __global__ void k_heap_trace(const uint32_t *sval, const uint32_t *noff, const u
   }
 }
 
+// One stream-ordered allocation of the heap path; RK_HEAP_ALLOC_CAP (a test
+// hook) fails every allocation above that many bytes, as HBM exhaustion would.
+static hipError_t heap_alloc(void **p, size_t bytes, hipStream_t st) {
+  static const size_t cap = [] {
+    const char *e = getenv("RK_HEAP_ALLOC_CAP");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+  }();
+  *p = nullptr;
+  if (cap && bytes > cap) return hipErrorOutOfMemory;
+  return hipMallocAsync(p, bytes, st);
+}
+static int heap_status(hipError_t e) {
+  return e == hipSuccess ? RK_OK : e == hipErrorOutOfMemory ? RK_E_NOMEM : RK_E_HIP;
+}
+
 // The queued heap segments (their number already read back), one after
 // another: prep, then the path its keys take.  A rare path (only crafted
 // inputs reach libstdc++'s depth limit on 2048+ members): its buffers are
 // stream-ordered allocations of its own, and it waits for the device twice
-// per rank-path segment to size them.
-static void heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint32_t *tag,
-                          uint32_t *otag, uint32_t *host_words, hipStream_t st) {
+// per rank-path segment to size them.  Returns RK_E_NOMEM when a buffer
+// cannot be had (nothing is launched on a missing buffer; what was allocated
+// is freed), RK_E_HIP on any other runtime failure.
+static int heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint32_t *tag,
+                         uint32_t *otag, uint32_t *host_words, hipStream_t st) {
   std::vector<HeapSeg> q(nheap);
-  (void)hipMemcpyAsync(q.data(), dq, nheap * sizeof(HeapSeg), hipMemcpyDeviceToHost, st);
-  (void)hipStreamSynchronize(st);
+  hipError_t e = hipMemcpyAsync(q.data(), dq, nheap * sizeof(HeapSeg), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return RK_E_HIP;
   uint32_t nmax = 0;
   for (const HeapSeg &g : q) nmax = g.n > nmax ? g.n : nmax;
   constexpr uint32_t LDS_MAX = 160 * 1024 - 1024;
@@ -1568,14 +1586,16 @@ static void heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint
   uint32_t *logb = nullptr, *mode = nullptr, *cnt = nullptr, *off = nullptr, *ssb = nullptr;
   uint16_t *logq = nullptr;
   const size_t sscap = scan_blocks((size_t)nmax + 1) + 64;
-  (void)hipMallocAsync((void **)&R, nmax + 16, st);
-  (void)hipMallocAsync((void **)&logb, (size_t)nmax * 4 + 16, st);
-  (void)hipMallocAsync((void **)&logq, (size_t)nmax * 2 + 16, st);
-  (void)hipMallocAsync((void **)&mode, 16, st);
-  (void)hipMallocAsync((void **)&cnt, ((size_t)nmax + 1) * 4 + 16, st);
-  (void)hipMallocAsync((void **)&off, ((size_t)nmax + 1) * 4 + 16, st);
-  (void)hipMallocAsync((void **)&ssb, sscap * 4, st);
-  for (const HeapSeg &g : q) {
+  int rc = RK_OK;
+  {
+    void **bufs[7] = {(void **)&R, (void **)&logb, (void **)&logq, (void **)&mode, (void **)&cnt,
+                      (void **)&off, (void **)&ssb};
+    const size_t sizes[7] = {(size_t)nmax + 16, (size_t)nmax * 4 + 16, (size_t)nmax * 2 + 16, 16,
+                             ((size_t)nmax + 1) * 4 + 16, ((size_t)nmax + 1) * 4 + 16, sscap * 4};
+    for (int i = 0; i < 7 && !rc; ++i) rc = heap_status(heap_alloc(bufs[i], sizes[i], st));
+  }
+  for (size_t si = 0; si < q.size() && !rc; ++si) {
+    const HeapSeg &g = q[si];
     const size_t o = (size_t)g.b + g.f;
     uint64_t *K = key + o;
     uint32_t *T = tag + o, *out = otag + o;
@@ -1587,31 +1607,38 @@ static void heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint
       k_heap_rank_pops<false><<<1, 64, n + 16, st>>>(R, n, n, logb, logq, mode);
     else  // the top RT (odd) nodes in LDS
       k_heap_rank_pops<true><<<1, 64, RT + 16, st>>>(R, n, RT, logb, logq, mode);
-    (void)hipMemcpyAsync(host_words, mode, 4, hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
+    e = hipMemcpyAsync(host_words, mode, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if ((rc = heap_status(e))) break;
     if (host_words[0] != HM_RANK) continue;
     const uint32_t npop = n - 1;
     k_heap_pair_counts<<<grid_for(npop + 1, 256), 256, 0, st>>>(logq, npop, cnt);
     exclusive_scan_u32(cnt, off, (size_t)npop + 1, ScanScratch{ssb, sscap}, st);
-    (void)hipMemcpyAsync(host_words, off + npop, 4, hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
+    e = hipMemcpyAsync(host_words, off + npop, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if ((rc = heap_status(e))) break;
     const uint32_t P = host_words[0];
     const size_t rw = radix_scratch_words(P);
     uint32_t *pk = nullptr, *pv = nullptr, *sk = nullptr, *sv = nullptr, *tk = nullptr,
              *tv = nullptr, *rs = nullptr, *noff = nullptr;
     for (uint32_t **b : {&pk, &pv, &sk, &sv, &tk, &tv})
-      (void)hipMallocAsync((void **)b, (size_t)P * 4 + 16, st);
-    (void)hipMallocAsync((void **)&rs, rw * 4, st);
-    (void)hipMallocAsync((void **)&noff, ((size_t)n + 2) * 4, st);
-    k_heap_pairs<<<grid_for(npop, 256), 256, 0, st>>>(logb, logq, off, npop, pk, pv);
-    radix_sort_pairs(pk, pv, sk, sv, tk, tv, P, bit_length(n), rs, rw, st);
-    k_heap_node_starts<<<grid_for(n + 1, 256), 256, 0, st>>>(sk, P, n, noff);
-    k_heap_trace<<<grid_for(n, 256), 256, 0, st>>>(sv, noff, logb, logq, T, n, out);
-    for (uint32_t *b : {pk, pv, sk, sv, tk, tv, rs, noff}) (void)hipFreeAsync(b, st);
+      if (!rc) rc = heap_status(heap_alloc((void **)b, (size_t)P * 4 + 16, st));
+    if (!rc) rc = heap_status(heap_alloc((void **)&rs, rw * 4, st));
+    if (!rc) rc = heap_status(heap_alloc((void **)&noff, ((size_t)n + 2) * 4, st));
+    if (!rc) {
+      k_heap_pairs<<<grid_for(npop, 256), 256, 0, st>>>(logb, logq, off, npop, pk, pv);
+      radix_sort_pairs(pk, pv, sk, sv, tk, tv, P, bit_length(n), rs, rw, st);
+      k_heap_node_starts<<<grid_for(n + 1, 256), 256, 0, st>>>(sk, P, n, noff);
+      k_heap_trace<<<grid_for(n, 256), 256, 0, st>>>(sv, noff, logb, logq, T, n, out);
+    }
+    for (uint32_t *b : {pk, pv, sk, sv, tk, tv, rs, noff})
+      if (b) (void)hipFreeAsync(b, st);
   }
   for (void *b : {(void *)R, (void *)logb, (void *)logq, (void *)mode, (void *)cnt, (void *)off,
                   (void *)ssb})
-    (void)hipFreeAsync(b, st);
+    if (b) (void)hipFreeAsync(b, st);
+  if (!rc && hipGetLastError() != hipSuccess) rc = RK_E_HIP;
+  return rc;
 }
 
 // phase B: LDS layout of k_sort_groups_lds with a stack for any depth budget
@@ -1831,22 +1858,24 @@ static HeapSeg *heap_queue(void *scratch, uint32_t m, uint32_t ngroups) {
 // The heap segments of a sort_groups_exact call made with `heap_count`: their
 // number was copied to heap_count, which the caller read back together with
 // its own words; this sorts them (their tags into otag) afterwards.
-void sort_groups_heap_deferred(uint32_t ngroups, uint32_t m, uint64_t *key, uint32_t *tag,
-                               uint32_t *otag, void *scratch, uint32_t nheap,
-                               uint32_t *host_words, hipStream_t st) {
+int sort_groups_heap_deferred(uint32_t ngroups, uint32_t m, uint64_t *key, uint32_t *tag,
+                              uint32_t *otag, void *scratch, uint32_t nheap,
+                              uint32_t *host_words, hipStream_t st) {
   nheap = nheap < HEAPQ_CAP ? nheap : HEAPQ_CAP;
-  if (nheap) heap_segments(heap_queue(scratch, m, ngroups), nheap, key, tag, otag, host_words, st);
+  if (!nheap) return RK_OK;
+  return heap_segments(heap_queue(scratch, m, ngroups), nheap, key, tag, otag, host_words, st);
 }
 
-void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
+int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
                        uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
                        ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
                        hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join,
                        uint32_t *heap_count) {
   if (!m) {
     if (heap_count) (void)hipMemsetAsync(heap_count, 0, 4, st);
-    return;
+    return RK_OK;
   }
+  int hrc = RK_OK;  // the heap segments' status (sorted here only without heap_count)
   constexpr int NL = NTIER;  // every tier is listed
   // groups of <= 64 members (k_sort_small, registers) run on `side`,
   // concurrently with the LDS tiers
@@ -2059,7 +2088,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
     (void)hipMemcpyAsync(host_words, heapq_n, 4, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     const uint32_t nheap = host_words[0] < HEAPQ_CAP ? host_words[0] : HEAPQ_CAP;
-    if (nheap) heap_segments(heapq, nheap, key, tag, otag, host_words, st);
+    if (nheap) hrc = heap_segments(heapq, nheap, key, tag, otag, host_words, st);
   } else {
     k_heap_segments<<<64, 256, 0, st>>>(heapq_n, heapq, key, tag, otag);
   }
@@ -2097,6 +2126,7 @@ void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_
   kt_end(st, KID_SORT_SEGS, 0.0);
   tier_slot(NTIER);
   if (side) (void)hipStreamWaitEvent(st, ev_join, 0);
+  return hrc;
 }
 
 }  // namespace rk

@@ -261,17 +261,19 @@ size_t groupsort_scratch_bytes(uint32_t n);
 // narrow_keys: every key fits 32 bits (LDS tiers stage 4-byte keys).
 // side (optional): a second stream for the tiers of <= 64 members, forked
 // and joined through ev_fork / ev_join.
-void sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
-                       uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
-                       ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
-                       hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
-                       hipEvent_t ev_join = nullptr, uint32_t *heap_count = nullptr);
+// Returns RK_OK, or the status of the depth-limit heap segments' own buffers
+// (RK_E_NOMEM / RK_E_HIP; only when they are sorted here, heap_count null).
+int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t ngroups,
+                      uint32_t m, uint64_t *key, uint32_t *tag, uint32_t *otag, void *scratch,
+                      ScanScratch ss, uint32_t *host_words, bool narrow_keys, hipStream_t st,
+                      hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
+                      hipEvent_t ev_join = nullptr, uint32_t *heap_count = nullptr);
 // heap_count != nullptr: the depth-limit heap segments are not sorted, their
 // number goes to heap_count (device), and the caller, having read it back,
-// sorts them by this before using otag
-void sort_groups_heap_deferred(uint32_t ngroups, uint32_t m, uint64_t *key, uint32_t *tag,
-                               uint32_t *otag, void *scratch, uint32_t nheap,
-                               uint32_t *host_words, hipStream_t st);
+// sorts them by this before using otag (RK_OK / RK_E_NOMEM / RK_E_HIP)
+int sort_groups_heap_deferred(uint32_t ngroups, uint32_t m, uint64_t *key, uint32_t *tag,
+                              uint32_t *otag, void *scratch, uint32_t nheap,
+                              uint32_t *host_words, hipStream_t st);
 // sorted member slots (otag), group of every slot (sgid), group bounds, the
 // members' file rows -> the output columns
 void emit_result(const uint32_t *otag, const uint32_t *sgid, const uint32_t *goff,

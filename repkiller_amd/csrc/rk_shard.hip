@@ -138,10 +138,13 @@ __global__ void __launch_bounds__(256) k_part_count(Op op, uint32_t n, uint32_t 
   if (threadIdx.x < P) cnt[(size_t)threadIdx.x * nblk + blockIdx.x] = bc[threadIdx.x];
 }
 
+// cap: positions at or past it are not written (a plan built from host-known
+// counts whose device offsets disagree: *ovf is flagged instead)
 template <class Op>
 __global__ void __launch_bounds__(256) k_part_scatter(Op op, uint32_t n, uint32_t P,
                                                       uint32_t nblk, const uint32_t *off,
-                                                      const uint32_t *mcache) {
+                                                      const uint32_t *mcache, uint32_t cap,
+                                                      uint32_t *ovf) {
   // wc[r][w][d]: round r, wave w's count of destination d, then its first position
   __shared__ uint32_t wc[PART_ROUNDS][4][MAXP];
   for (uint32_t j = threadIdx.x; j < PART_ROUNDS * 4 * MAXP; j += 256) (&wc[0][0][0])[j] = 0;
@@ -180,7 +183,11 @@ __global__ void __launch_bounds__(256) k_part_scatter(Op op, uint32_t n, uint32_
     for (uint32_t any = wave_or(mask[r]); any; any &= any - 1) {
       const uint32_t d = __builtin_ctz(any);
       const uint64_t b = __ballot((mask[r] >> d) & 1u);
-      if ((mask[r] >> d) & 1u) op.emit(i, d, wc[r][w][d] + (uint32_t)__popcll(b & lt));
+      if ((mask[r] >> d) & 1u) {
+        const uint32_t pos = wc[r][w][d] + (uint32_t)__popcll(b & lt);
+        if (pos < cap) op.emit(i, d, pos);
+        else atomicOr(ovf, 1u);
+      }
     }
   }
 }
@@ -205,9 +212,9 @@ struct Expect {
   uint32_t v[MAXP + 1];
 };
 __global__ void k_expect_totals(const uint32_t *off, uint32_t nblk, uint32_t P, Expect e,
-                                uint32_t *ctrl) {
+                                uint32_t *flag, uint32_t bit) {
   const uint32_t d = threadIdx.x;
-  if (d <= P && off[(size_t)d * nblk] != e.v[d]) atomicOr(&ctrl[0], ERRB_INTERNAL);
+  if (d <= P && off[(size_t)d * nblk] != e.v[d]) atomicOr(flag, bit);
 }
 
 template <class Op>
@@ -642,13 +649,14 @@ enum Slot : int {
   SL_LAB, SL_CUR, SL_REQ, SL_SRC, SL_RQ, SL_RESP, SL_BACK, SL_HREC, SL_MEM, SL_LG, SL_SGID,
   SL_GMEM, SL_GOFF, SL_RECKEY, SL_TAG, SL_OTAG, SL_GSORT, SL_OGID, SL_OREP, SL_OORD, SL_CKEY_Y,
   SL_CENT_Y, SL_CSTATE_Y, SL_CPK_Y, SL_CNBD_Y, SL_CCEN_Y, SL_CLEN_Y, SL_TK2, SL_TV2, SL_RADIX2,
-  SL_YXH, SL_YMASK, SL_YCODE, SL_COUNT
+  SL_YXH, SL_YMASK, SL_YCODE, SL_GMSG, SL_COUNT
 };
 
 constexpr int kPoolSlots = 160;  // slots of both drivers (rk_shard_nw.h adds its own)
 
 struct PartPlan {
   uint32_t n = 0, nblk = 1;
+  uint32_t cap = 0xFFFFFFFFu;  // send positions written (plan_same: the expected total)
   uint32_t *off = nullptr;
   uint32_t *mcache = nullptr;  // set before plan(): masks cached there (mread: read)
   bool mread = false;
@@ -658,7 +666,7 @@ struct PartPlan {
 
 // The driver's all-gather message (see Shard::allgather): a 16-B header whose
 // first word is the sender's status, then up to GMAX payload bytes.
-constexpr size_t GMAX = NBINS * 4 + 64, GHDR = 16;  // a histogram + a few words
+constexpr size_t GMAX = 2 * NBINS * 4 + 2048, GHDR = 16;  // two histograms + a few words
 constexpr int STATUS_COMM_FAILED = 0x7fffffff;
 int status_message(rk_comm *comm, hipStream_t st, int32_t status, const void *mine, void *all,
                    size_t bytes, uint32_t *who, std::string *err, std::vector<char> &snd,
@@ -702,6 +710,17 @@ struct Shard {
   uint64_t last_recv[MAXP] = {};
   uint32_t n_gathers = 0, n_a2a = 0, n_syncs = 0, n_agree_skipped = 0;  // (shard stats)
   uint64_t readbacks0 = 0;  // ctx->readbacks at the call's start
+  // fast path (rk_shard_fast.h): plans from host-known counts flag a device
+  // disagreement in *expect_flag (bit expect_bit) instead of the error word,
+  // and write no send position past the expected total
+  uint32_t *expect_flag = nullptr;
+  uint32_t expect_bit = 0;
+  // a stage whose sizes match the last completed call runs without agreement
+  // points: no buffer may grow then (a growth is reported at the next gather)
+  bool alloc_locked = false, alloc_violation = false;
+  int sticky = 0;  // a local failure inside such a stage: reported at the next gather
+  uint32_t max_sweeps[2] = {0, 0};  // the careful driver's sweeps per axis (X, Y)
+  uint32_t max_jumps = 0;           // and its pointer-jumping rounds
 
   template <class T>
   T *take(int slot, size_t count) {
@@ -709,6 +728,7 @@ struct Shard {
     if (pl.ptr.size() < (size_t)kPoolSlots) pl.ptr.resize(kPoolSlots, nullptr), pl.cap.resize(kPoolSlots, 0);
     const size_t need = align_up(count * sizeof(T) + 16);
     if (need > pl.cap[slot]) {
+      if (alloc_locked) alloc_violation = true;
       if (pl.ptr[slot]) (void)hipFree(pl.ptr[slot]);
       pl.ptr[slot] = nullptr;
       pl.cap[slot] = 0;
@@ -765,6 +785,68 @@ struct Shard {
     }
     return first;
   }
+  // ---- device-assembled messages (the fast path): the payload is written on
+  // the device by the kernels that produce it (histograms, counts, flags) plus
+  // a small host part at payload offset 0, then gathered in one collective
+  // with one wait for the stream (RCCL: on the device, one copy down)
+  static constexpr size_t MB = GHDR + GMAX;
+  uint8_t *gdev = nullptr;
+  // zeroes the header and the first dev_bytes of the payload (on the stream)
+  // and returns the device payload
+  uint8_t *msg_begin(size_t dev_bytes) {
+    if (!gdev) gdev = take<uint8_t>(SL_GMSG, MB);
+    const size_t hbytes = MB * (size_t)(P + 1);
+    if (ctx->sh_msg_cap < hbytes) {
+      if (ctx->sh_msg) (void)hipHostFree(ctx->sh_msg);
+      ctx->sh_msg = nullptr;
+      ctx->sh_msg_cap = 0;
+      if (hipHostMalloc((void **)&ctx->sh_msg, hbytes, hipHostMallocDefault) != hipSuccess) {
+        ctx->sh_msg = nullptr;
+        ctx->err = "pinned message buffer";
+        throw RK_E_NOMEM;
+      }
+      ctx->sh_msg_cap = hbytes;
+    }
+    zero(gdev, GHDR + (dev_bytes < GMAX ? dev_bytes : GMAX));
+    return gdev + GHDR;
+  }
+  // every rank's message (payloads at msg_of(q)); returns the first non-zero
+  // status (0: every rank is fine).  host: copied to payload offset 0.
+  int msg_gather(int32_t status, const void *host = nullptr, size_t host_bytes = 0) {
+    if (!status) status = sticky;
+    if (!status && alloc_violation) {
+      ctx->err = "fast path: a buffer grew inside a stage without agreement points";
+      status = RK_E_INTERNAL;
+    }
+    char *snd = ctx->sh_msg;
+    std::memset(snd, 0, GHDR);
+    std::memcpy(snd, &status, 4);
+    if (host_bytes) std::memcpy(snd + GHDR, host, host_bytes);
+    hip(hipMemcpyAsync(gdev, snd, GHDR + host_bytes, hipMemcpyHostToDevice, st), "h2d");
+    ++n_gathers;
+    ++n_syncs;
+    if (comm->allgather_dev(gdev, ctx->sh_msg + MB, MB, st)) {
+      comm_broken = true;
+      ctx->err = "allgather: " + comm->err;
+      throw RK_E_HIP;
+    }
+    int first = 0;
+    uint32_t who = 0;
+    for (uint32_t q = 0; q < P; ++q) {
+      int32_t sq;
+      std::memcpy(&sq, ctx->sh_msg + MB * (1 + q), 4);
+      if (sq && !first) first = sq, who = q;
+    }
+    if (first) {
+      peer_failed = true;
+      if (!status)
+        ctx->err = "rank " + std::to_string(who) + " failed (status " + std::to_string(first) +
+                   "); every rank stops";
+    }
+    return first;
+  }
+  const uint8_t *msg_of(uint32_t q) const { return (const uint8_t *)ctx->sh_msg + MB * (1 + q) + GHDR; }
+
   // a rank that failed outside a collective releases its peers (see allgather)
   void fail_broadcast(int code) {
     if (peer_failed || comm_broken) return;
@@ -861,8 +943,10 @@ struct Shard {
       e.v[q] = acc;
       if (q < P) acc += (uint32_t)ref.cnt[q];
     }
-    k_expect_totals<<<1, 64, 0, st>>>(pp.off, pp.nblk, P, e, ctrl);
+    k_expect_totals<<<1, 64, 0, st>>>(pp.off, pp.nblk, P, e, expect_flag ? expect_flag : ctrl,
+                                      expect_flag ? expect_bit : (uint32_t)ERRB_INTERNAL);
     launched("k_expect_totals");
+    if (expect_flag) pp.cap = (uint32_t)(ref.total < 0xFFFFFFFFull ? ref.total : 0xFFFFFFFFull);
   }
   // several device words in one round trip
   std::vector<uint32_t> d2h_words(std::initializer_list<const uint32_t *> src) {
@@ -901,7 +985,8 @@ struct Shard {
   template <class Op>
   void emit(const Op &op, const PartPlan &pp) {
     kt_begin(st, KID_PART);
-    k_part_scatter<<<pp.nblk, 256, 0, st>>>(op, pp.n, P, pp.nblk, pp.off, pp.mcache);
+    k_part_scatter<<<pp.nblk, 256, 0, st>>>(op, pp.n, P, pp.nblk, pp.off, pp.mcache, pp.cap,
+                                            expect_flag ? expect_flag : ctrl + 7);
     kt_end(st, KID_PART, 0.0);
     launched("k_part_scatter");
   }
@@ -1253,7 +1338,10 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
       S.zero(S.ctrl + 3, 4);
       jump_round(jp, m, S.ctrl + 3, rounds == 0 ? junk : nullptr, S.ctrl, S.st);
       S.launched("jump_round");
-      if (!S.read1(S.ctrl + 3)) break;
+      if (!S.read1(S.ctrl + 3)) {
+        S.max_jumps = rounds + 1 > S.max_jumps ? rounds + 1 : S.max_jumps;
+        break;
+      }
     }
     exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), S.st);
   }
@@ -1364,6 +1452,7 @@ void finish_stats(Shard &S, uint32_t nl, const rk_shard_result *out,
   ss.agree_skipped = S.n_agree_skipped;
   ss.ms_total = ms_since(t0);
   ctx->stats = rk_stats{};
+  stats_numa_unknown(&ctx->stats);
   ctx->stats.n_in = nl;
   ctx->stats.n_proc = ss.n_slice;
   ctx->stats.n_groups = out->n_groups;
@@ -1371,6 +1460,7 @@ void finish_stats(Shard &S, uint32_t nl, const rk_shard_result *out,
 }
 
 #include "rk_shard_nw.h"
+#include "rk_shard_fast.h"
 
 int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm,
                           int32_t lead_in, rk_shard_result *out, int pre) {
@@ -1411,24 +1501,61 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
     }
   }
 
-  // ---- 0: global row numbering (rank blocks are consecutive in file order);
-  // the first collective carries every rank's status
-  const uint64_t n_mine = rc ? 0 : in->n;
-  std::vector<uint64_t> nall(P);
-  if (S.status_gather(rc, &n_mine, nall.data(), sizeof n_mine)) throw rc ? rc : (int)RK_E_PEER;
-  uint64_t row_base = 0, N = 0;
-  for (uint32_t q = 0; q < P; ++q) N += nall[q], row_base += q < me ? nall[q] : 0;
-  if (N >= 0xFFFFFFFFull) return RK_E_TOO_MANY;  // every rank sees the same N
-  const uint32_t nl = (uint32_t)in->n;
-  ss.n_in = nl;
-  ss.n_total = N;
   // the record pipeline's internals when every row of every rank packs into a
   // 16-B record (rk_shard_nw.h); RK_SHARD_GENERIC=1 forces this driver
   static const bool generic_only = [] {
     const char *e = std::getenv("RK_SHARD_GENERIC");
     return e && e[0] == '1';
   }();
-  if (!generic_only) {
+  // the fast path (rk_shard_fast.h) unless RK_SH_FAST=0 or the round-3 Y
+  // schedule is asked for (RK_SH_YEARLY=1, the careful driver's option)
+  static const bool fast_on = [] {
+    const char *e = std::getenv("RK_SH_FAST"), *y = std::getenv("RK_SH_YEARLY");
+    return !(e && e[0] == '0') && !(y && y[0] == '1');
+  }();
+  uint64_t row_base = 0, N = 0;
+  if (!generic_only && fast_on) {
+    int r;
+    try {
+      r = classify_sharded_fast(S, in, p, lead_in, out, rc, &N, &row_base);
+    } catch (...) {
+      std::memset(ctx->sh_fp, 0, sizeof ctx->sh_fp);
+      throw;
+    }
+    S.expect_flag = nullptr;
+    S.alloc_locked = false;
+    if (r == RK_SHARD_RETRY) {
+      // a halo disagreement, an axis left open, a chain longer than the
+      // queued jumping rounds: every rank repeats the call the careful way
+      // (with as many queued sweeps next time as it took)
+      std::memset(ctx->sh_fp, 0, sizeof ctx->sh_fp);
+      ss.fast_retry = 1;
+      S.zero(S.ctrl, 256 * 4);
+      r = classify_sharded_nw(S, in, p, P, me, N, row_base, lead_in, out, t0);
+      for (int a = 0; a < 2; ++a)
+        ctx->sh_blind[a] = S.max_sweeps[a] > 3 ? S.max_sweeps[a] : 3u;
+      ctx->sh_jumps = S.max_jumps > 1 ? (S.max_jumps < 8 ? S.max_jumps : 8u) : 1u;
+    }
+    if (r != RK_SHARD_FALLBACK) {
+      if (r) std::memset(ctx->sh_fp, 0, sizeof ctx->sh_fp);
+      finish_stats(S, (uint32_t)(rc ? 0 : in->n), out, t0);
+      return r;
+    }
+    std::memset(ctx->sh_fp, 0, sizeof ctx->sh_fp);
+    S.zero(S.ctrl, 256 * 4);
+  } else {
+    // ---- 0: global row numbering (rank blocks are consecutive in file
+    // order); the first collective carries every rank's status
+    const uint64_t n_mine = rc ? 0 : in->n;
+    std::vector<uint64_t> nall(P);
+    if (S.status_gather(rc, &n_mine, nall.data(), sizeof n_mine)) throw rc ? rc : (int)RK_E_PEER;
+    for (uint32_t q = 0; q < P; ++q) N += nall[q], row_base += q < me ? nall[q] : 0;
+  }
+  if (N >= 0xFFFFFFFFull) return RK_E_TOO_MANY;  // every rank sees the same N
+  const uint32_t nl = (uint32_t)in->n;
+  ss.n_in = nl;
+  ss.n_total = N;
+  if (!generic_only && !fast_on) {
     const int r = classify_sharded_nw(S, in, p, P, me, N, row_base, lead_in, out, t0);
     if (r != RK_SHARD_FALLBACK) {
       finish_stats(S, nl, out, t0);
@@ -1805,9 +1932,9 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
     group_offsets(sgid, mr, Gl, goffs, S.st);
     build_records(gmem, mem, mr, reckey, tag, S.st);
     // the group-sort tiers on both streams, as in the single-device path
-    sort_groups_exact(sgid, goffs, Gl, mr, reckey, tag, otag, gsort,
-                      S.scan_scratch(SL_SCAN, mr + Gl + 2), ctx->host + 128, narrow, S.st,
-                      S.st2 != S.st ? S.st2 : nullptr, ctx->fork, ctx->join);
+    S.check(sort_groups_exact(sgid, goffs, Gl, mr, reckey, tag, otag, gsort,
+                              S.scan_scratch(SL_SCAN, mr + Gl + 2), ctx->host + 128, narrow, S.st,
+                              S.st2 != S.st ? S.st2 : nullptr, ctx->fork, ctx->join));
     emit_result(otag, sgid, goffs, gmem, mr, ogid, orep, oord, S.st);
     if (g0) k_add_u32<<<grid_for(mr, 256), 256, 0, S.st>>>(ogid, mr, g0);
     S.launched("member order");

@@ -66,14 +66,16 @@ struct ShRowsArgs {
   uint64_t vsize, max_x, max_y;
   uint32_t shift;
   uint32_t *hist, *ctrl;  // hist null: one rank owns everything, no bounds to find
+  uint32_t *yhist = nullptr;  // (fast path) the Y-centre bucket histogram, bins >> yshift
+  uint32_t yshift = 0;
 };
 __device__ __forceinline__ uint64_t div10_sh(uint64_t v) {  // 32-bit when it fits
   return v < (1ull << 32) ? (uint64_t)((uint32_t)v / 10u) : v / 10;
 }
 __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
-  __shared__ uint32_t h[NBINS];
+  __shared__ uint32_t h[NBINS], hy[NBINS];
   __shared__ uint32_t red[3];
-  for (uint32_t b = threadIdx.x; b < NBINS; b += 256) h[b] = 0;
+  for (uint32_t b = threadIdx.x; b < NBINS; b += 256) h[b] = hy[b] = 0;
   if (threadIdx.x < 3) red[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t drop = a.vsize - 1;
@@ -92,6 +94,10 @@ __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
     ubc |= probe_max_bucket_sh(xs + hl, a.max_x) > a.max_x ||
            probe_max_bucket_sh(ys + hl, a.max_y) > a.max_y;
     if (a.hist) atomicAdd(&h[(uint32_t)pk >> a.shift], 1u);
+    if (a.yhist) {  // the Y record's bucket (rk_narrow.hip DstProc): centre yStart + len / 2
+      const uint64_t yb = ((ys + hl) / 100) >> a.yshift;
+      if (yb < NBINS) atomicAdd(&hy[yb], 1u);
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     const uint32_t o = __shfl_xor(maxlen, off);
@@ -108,6 +114,9 @@ __global__ void __launch_bounds__(256) k_sh_rows(ShRowsArgs a) {
   if (a.hist)
     for (uint32_t b = threadIdx.x; b < NBINS; b += 256)
       if (h[b]) atomicAdd(&a.hist[b], h[b]);
+  if (a.yhist)
+    for (uint32_t b = threadIdx.x; b < NBINS; b += 256)
+      if (hy[b]) atomicAdd(&a.yhist[b], hy[b]);
   if (threadIdx.x == 0) {
     if (red[2]) atomicAdd(&a.ctrl[25], red[2]);
     if (red[0]) atomicMax(&a.ctrl[21], red[0]);
@@ -150,7 +159,11 @@ struct GhostOp16 {
   uint4 *out;          // records, or
   uint8_t *sout;       // the entries' X states (1 = ACTIVE), same order
   const uint32_t *xg;
+  // (fast path) the suffix start on the device: the op runs over all m
+  // entries, those before *dbase select nothing (base is then 0)
+  const uint32_t *dbase = nullptr;
   __device__ uint32_t mask(uint32_t i) const {
+    if (dbase && i < *dbase) return 0u;
     const uint64_t bk = nwr_xbucket(R[base + i]);
     uint32_t m = 0;
     for (uint32_t g = me + 1; g < P; ++g)
@@ -736,6 +749,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
                     S.ctrl + 64, S.ctrl + 4};
     uint32_t sweeps = 0;
     S.check(resolve_axis(ctx, ax, sc, true, &sweeps));
+    S.max_sweeps[0] = sweeps > S.max_sweeps[0] ? sweeps : S.max_sweeps[0];
     kt_begin(st, KID_SH_XOWN);
     k_sh_x_own<<<grid_for(mx, 256), 256, 0, st>>>(xpos, cx.state, par, halo, Gc, m, poff, xg,
                                                   xused);
@@ -828,6 +842,7 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
                     S.ctrl + 64, S.ctrl + 4};
     uint32_t sweeps = 0;
     S.check(resolve_axis(ctx, ay, sc, true, &sweeps));
+    S.max_sweeps[1] = sweeps > S.max_sweeps[1] ? sweeps : S.max_sweeps[1];
   };
   auto y_results = [&](const uint32_t *ymap, uint32_t c) {
     if (!c) return;
@@ -941,9 +956,9 @@ int classify_sharded_nw(Shard &S, const rk_frags_soa *in, const rk_params &p, ui
     }
     group_offsets(sgid, mr, Gl, goffs, st);
     // the group-sort tiers on both streams, as in the single-device path
-    sort_groups_exact(sgid, goffs, Gl, mr, reckey, tag, otag, gsort,
-                      S.scan_scratch(SL_SCAN, mr + Gl + 2), ctx->host + 128, narrow, st,
-                      st2 != st ? st2 : nullptr, ctx->fork, ctx->join);
+    S.check(sort_groups_exact(sgid, goffs, Gl, mr, reckey, tag, otag, gsort,
+                              S.scan_scratch(SL_SCAN, mr + Gl + 2), ctx->host + 128, narrow, st,
+                              st2 != st ? st2 : nullptr, ctx->fork, ctx->join));
     emit_result(otag, sgid, goffs, mrow, mr, ogid, orep, oord, st);
     if (g0) k_add_u32<<<grid_for(mr, 256), 256, 0, st>>>(ogid, mr, g0);
     S.launched("member order");

@@ -37,6 +37,7 @@ def load_case(case):
 def worker(rank, world, port, cases, q, comm_kind="host", env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.update(env or {})  # read once by the library (e.g. RK_SHARD_GENERIC)
+    import numpy as np
     import torch
     import torch.distributed as dist
     import repkiller_amd as rk
@@ -60,17 +61,33 @@ def worker(rank, world, port, cases, q, comm_kind="host", env=None):
                 lr = -1.0  # this rank alone fails its argument check
             if case.get("fault_rank") == rank:  # rk_shard.hip fault_here(): fail at that stage
                 os.environ["RK_TEST_FAULT"] = case["fault"]
+            # repeat: the same call again on the same context (the second finds
+            # every stage's sizes known: the fast path's no-agreement stages);
+            # every repetition must give the same share, the last one's
+            # statistics are reported with the list of all
+            reps, first, stats = case.get("repeat", 1), None, []
             try:
-                out = rk.classify_sharded(ctx, comm, x, y, ln, s, lx, ly, lr,
-                                          case.get("pr", 0.3), case.get("lead_in", -1))
+                for _ in range(reps):
+                    out = rk.classify_sharded(ctx, comm, x, y, ln, s, lx, ly, lr,
+                                              case.get("pr", 0.3), case.get("lead_in", -1))
+                    stats.append(rk.shard_stats(ctx))
+                    r = out.result
+                    share = (out.out_offset, out.n_out_total, out.n_groups, r.out_order, r.gid,
+                             r.repval)
+                    if first is None:
+                        first = share
+                    else:
+                        assert share[:3] == first[:3], (share[:3], first[:3])
+                        for a, b in zip(share[3:], first[3:]):
+                            assert np.array_equal(a, b), "repeated call differs"
             except rk.RkError as e:
                 q.put((ci, rank, "error", e.code))
                 continue
             finally:
                 os.environ.pop("RK_TEST_FAULT", None)
-            r = out.result
-            q.put((ci, rank, "ok", (out.out_offset, out.n_out_total, out.n_groups,
-                                    r.out_order, r.gid, r.repval, rk.shard_stats(ctx))))
+            st = dict(stats[-1])
+            st["calls"] = stats
+            q.put((ci, rank, "ok", first + (st,)))
         comm.close()
         ctx.close()
     except Exception:  # noqa: BLE001 -- surfaced to the parent

@@ -381,6 +381,88 @@ def test_killer_group_heap_segment_vs_oracle(gpu_ctx):
         assert np.array_equal(r.out_order, got.out_order) and np.array_equal(r.gid, got.gid)
 
 
+_RICH_SCRIPT = r"""
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import repkiller_amd as rk
+f = rk.synth(400_000, 40_000_000, seed=47, family_frac=0.95, copies=(100, 600))
+ctx = rk.Context(0)
+r = ctx.classify(f, 40_000_000, 40_000_000)
+h = hashlib.sha256()
+for a in (r.out_order, r.gid, r.repval):
+    h.update(np.ascontiguousarray(a).tobytes())
+print(h.hexdigest(), r.n_groups)
+"""
+
+
+@pytest.mark.parametrize("env", ["RK_SPLIT_DYN=0", "RK_SPLIT_BIG=4096", "RK_SEG_WAVES=64",
+                                 "RK_LONG_GRID=16", "RK_GS_WAVES_MUL=1", "RK_SWEEP_BLIND=1"])
+def test_schedule_switches_repeat_rich(gpu_ctx, env):
+    """The grid and claiming switches of phase A (groups above 2048 members:
+    dynamic claiming, its first pass' size), phase B's grid and the long-run
+    walk's grid, on a repeat-rich set (cfg5's shape: groups of thousands of
+    members, bucket runs of hundreds of entries) -- bit-identical to the
+    default schedule."""
+    f = rk.synth(400_000, 40_000_000, seed=47, family_frac=0.95, copies=(100, 600))
+    r = gpu_ctx.classify(f, 40_000_000, 40_000_000)
+    h = hashlib.sha256()
+    for a in (r.out_order, r.gid, r.repval):
+        h.update(np.ascontiguousarray(a).tobytes())
+    k, v = env.split("=")
+    out = subprocess.run(["python", "-c", _RICH_SCRIPT, str(ROOT)], capture_output=True,
+                         text=True, timeout=120, env={**os.environ, k: v})
+    assert out.returncode == 0, out.stderr[-2000:]
+    digest, ng = out.stdout.split()
+    assert digest == h.hexdigest() and int(ng) == r.n_groups
+
+
+_KILLER_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+import repkiller_amd as rk
+from sort_cases import killer_with_keys
+segs = [killer_with_keys(30001, 3, 22), killer_with_keys(12000, 1, 26)]
+keys = np.concatenate(segs)
+off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
+ctx = rk.Context(0)
+try:
+    perm = ctx.std_sort_segments(keys, off)
+except rk.RkError as e:
+    print("error", e.code)
+    sys.exit(0)
+np.save(sys.argv[2], perm)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("env", ["RK_HEAP_RANK=0", "RK_HEAP_ALLOC_CAP=4096"])
+def test_heap_segment_switches(gpu_ctx, tmp_path, env):
+    """RK_HEAP_RANK=0 (every depth-limit heap segment through the one-block
+    pops of k_heap_segments) gives the restated std::sort's permutation; with
+    the heap path's buffers refused (RK_HEAP_ALLOC_CAP, as an exhausted HBM
+    would) the call returns RK_E_NOMEM instead of writing through a null
+    buffer."""
+    from sort_cases import killer_with_keys
+    segs = [killer_with_keys(30001, 3, 22), killer_with_keys(12000, 1, 26)]
+    out_npy = tmp_path / "perm.npy"
+    k, v = env.split("=")
+    out = subprocess.run(["python", "-c", _KILLER_SCRIPT, str(ROOT), str(out_npy)],
+                         capture_output=True, text=True, timeout=120, env={**os.environ, k: v})
+    assert out.returncode == 0, out.stderr[-2000:]
+    if k == "RK_HEAP_ALLOC_CAP":
+        assert out.stdout.split() == ["error", str(-6)], out.stdout
+        return
+    assert out.stdout.strip() == "ok", out.stdout
+    perm = np.load(out_npy)
+    a = 0
+    for sgm in segs:
+        assert np.array_equal(perm[a:a + sgm.size], ro.std_sort(sgm) + a), sgm.size
+        a += sgm.size
+
+
 def test_pipeline_choice(gpu_ctx, generic_ctx):
     """The record pipeline runs on the BASELINE-shaped sets; inputs it cannot
     represent (a length >= 2^24) take the generic one with the same result."""

@@ -123,6 +123,63 @@ def test_sharded_matches_single_device(gpu_ctx, world):
     assert reruns > 0
 
 
+FAST = [
+    dict(kind="synth", n=200_000, L=20_000_000, seed=41, repeat=2),
+    dict(kind="synth", n=100_000, L=10_000_000, seed=42, ff=0.95, copies=(100, 600), repeat=2),
+    dict(kind="synth", n=300_000, L=15_000_000_000, seed=43, ff=0.95, copies=(100, 600), repeat=2),
+    dict(kind="long_runs", runs_len=2500, seed=2501, L=10_000_000, lr=0.05, pr=0.05, repeat=2),
+    dict(kind="synth", n=7, L=1_000, seed=44, repeat=2),
+    dict(kind="synth", n=0, L=1_000, seed=45, repeat=2),
+]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_sharded_fast_path(gpu_ctx, world):
+    """The fast path (rk_shard_fast.h): exchange sizes agreed up front through
+    device-assembled messages.  Each case runs twice on the same contexts: the
+    first call agrees on its buffers at every exchange, the second finds every
+    stage's sizes known (no agreement points).  Both are bit-identical to the
+    single device; neither falls back to the careful driver on these sets; the
+    second makes at most 8 host waits and 8 all-gathers at 1, 2 and 4 ranks
+    (one more of each per extra cross-slice request round)."""
+    got = run_ranks(world, FAST, timeout=200)
+    for ci, case in enumerate(FAST):
+        order, gid, rep, ng, stats = assemble(got, ci, world)
+        want, _, _, _ = reference(gpu_ctx, case)
+        assert ng == want.n_groups, case
+        assert np.array_equal(order, want.out_order), case
+        assert np.array_equal(gid, want.gid), case
+        assert np.array_equal(rep, want.repval), case
+        for st in stats:
+            first, second = st["calls"]
+            assert first["fast_path"] == 1 and second["fast_path"] == 1, st
+            assert first["fast_retry"] == 0 and second["fast_retry"] == 0, (case, st)
+            assert second["generic_driver"] == 0
+            if world > 1:
+                assert second["fast_stages"] == 7, (case, second)
+            extra = max(0, second["root_rounds"] - 1)
+            assert second["gathers"] <= 8 + extra, (case, second)
+            assert second["host_syncs"] <= 8 + extra, (case, second)
+
+
+def test_sharded_fast_vs_careful(gpu_ctx):
+    """RK_SH_FAST=0 (the careful driver alone) and the fast path agree, and a
+    dense no-lead-in set (halo disagreements) makes the fast path hand the call
+    to the careful driver, which re-resolves."""
+    cases = [SYNTH[0], SYNTH[4]]
+    slow = run_ranks(2, cases, env={"RK_SH_FAST": "0"})
+    fast = run_ranks(2, cases)
+    for ci, case in enumerate(cases):
+        a = assemble(slow, ci, 2)
+        b = assemble(fast, ci, 2)
+        for i in range(3):
+            assert np.array_equal(a[i], b[i]), case
+        assert a[3] == b[3]
+        assert all(st["fast_path"] == 0 for st in a[4])
+        assert all(st["fast_path"] == 1 for st in b[4])
+    assert any(st["fast_retry"] for st in assemble(fast, 1, 2)[4])
+
+
 def _check_vs_single_device(gpu_ctx, got, cases, world, generic):
     for ci, case in enumerate(cases):
         order, gid, rep, ng, stats = assemble(got, ci, world)
