@@ -27,9 +27,10 @@ measured inside the timed steps -- only that kernel's launches carry events
 there, so the timers cost the step little; PMC HBM traffic from
 profiles/traffic.json), `kernels` (every kernel, from PROFILED_STEPS further
 steps with every launch timed, after the timed region),
-`cpu_baseline` (1 core of this host: the in-repo restatement on the SAME
-arrays the GPU classified, result compared; the reference itself,
-oracle/_ref/ref_driver, on a bounded sample beside it), `parity` (the timed
+`cpu_baseline` (1 core of this host: the reference itself,
+oracle/_ref/ref_driver, on a bounded sample of the workload as the value; the
+in-repo restatement on the SAME arrays the GPU classified beside it, result
+compared; this host's nproc), `parity` (the timed
 steps' result digest against the reference's, tests/golden/large_hashes.json),
 `host_to_host_fragments_per_s` (rk_classify from host buffers, PCIe included),
 `phases_ms` (per-step device time per phase).
@@ -132,31 +133,43 @@ def aggregate(world: int, n_local: int, dt_local: float) -> tuple[float, float]:
     return allsum(world, float(n_local)), allmax(world, dt_local)
 
 
+# the reference sample's size: at most this many fragments, over the genome
+# scaled to keep the config's density (cfg3: 12.5M fragments over 750 Mbp,
+# ~15-20 s of the reference's grouping + sorting on one core)
+REF_SAMPLE_MAX = 12_500_000
+
+
 def reference_sample(cfg: dict, seconds_hint: float) -> dict | None:
-    """The reference (oracle/_ref/ref_driver, built from /root/reference/src by
-    oracle/ref.mk) on a bounded sample of the same workload: the cfg3 density
-    (fragments per bp) at 1/10 of the genome, so ~5-30 s of single-core work."""
+    """The reference itself (oracle/_ref/ref_driver, compiled from
+    /root/reference/src by oracle/ref.mk) on a bounded sample of the same
+    workload: the config's generator and density at min(n, 12.5M) fragments,
+    timed over generate_fragment_groups + generate_diagonal_func + sort_groups
+    on one core of this host."""
     from oracle import rk_oracle as ro
     if not os.path.exists(ro.REF_DRIVER):
         return None
-    scale = 10 if cfg["n"] >= 10_000_000 else 1
-    n, L = cfg["n"] // scale, cfg["genome_len"] // scale
-    f = rk.synth(n, L, seed=3)
+    n = min(cfg["n"], REF_SAMPLE_MAX)
+    L = cfg["genome_len"] * n // cfg["n"]
+    f = rk.synth(n, L, seed=3, **cfg.get("synth", {}))
     with tempfile.TemporaryDirectory() as d:
         inp = os.path.join(d, "sample.csv")
         rk.write_input_csv(inp, f, L, L)
+        del f
         p = subprocess.run([ro.REF_DRIVER, inp, "-", "0.3", "0.3"], capture_output=True,
-                           text=True, timeout=max(120.0, seconds_hint * 10))
+                           text=True, timeout=max(300.0, seconds_hint * 10))
     if p.returncode != 0:
         return None
     t = json.loads(p.stderr.strip().splitlines()[-1])
     hot = t["group_s"] + t["diag_sort_s"]
+    frac = f"1/{cfg['n'] // n}" if n < cfg["n"] else "all"
     return {"value": round(n / hot, 1), "unit": "fragments/s", "cores": 1, "kind": "reference",
-            "sample": f"{n} fragments over {L} bp ("
-                      + (f"the config's density, 1/{scale} of the genome" if scale > 1
-                         else "the config's own size") + "), "
-                      f"ratios 0.3/0.3; timed region generate_fragment_groups + "
-                      f"generate_diagonal_func + sort_groups ({hot:.2f} s); host: {host_cpu()}"}
+            "sample": f"{n} fragments over {L} bp ({frac} of the config, at its density and "
+                      f"generator), ratios 0.3/0.3; the reference's own code "
+                      f"(oracle/_ref/ref_driver built from /root/reference/src), timed region "
+                      f"generate_fragment_groups + generate_diagonal_func + sort_groups "
+                      f"({hot:.2f} s; its CSV load {t['load_s']:.2f} s not counted); "
+                      f"host: {host_cpu()}",
+            "seconds": round(hot, 3)}
 
 
 def host_cpu() -> str:
@@ -170,43 +183,55 @@ def host_cpu() -> str:
     return "unknown"
 
 
+def host_cores() -> dict:
+    """This host's CPUs: nproc (every online CPU) and the ones this process may use."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": host_cpu()}
+
+
+def port_same_input(cfg: dict, same_input) -> dict:
+    """The in-repo restatement (oracle/rk_oracle.c, one thread) on the SAME arrays
+    the GPU classified, its result compared with the GPU's."""
+    from oracle import rk_oracle as ro
+    f, L, gpu_digest = same_input
+    t0 = time.perf_counter()
+    rc, gid, rep, order, _ = ro.classify(f.x_start, f.y_start, f.length, f.strand, L, L, 0.3, 0.3)
+    dt = time.perf_counter() - t0
+    out = {"value": round(f.n / dt, 1), "unit": "fragments/s", "cores": 1, "kind": "port",
+           "sample": f"the full {f.n}-fragment input the GPU classified (same arrays, same host), "
+                     f"ratios 0.3/0.3; oracle/rk_oracle.c restatement, one thread ({dt:.2f} s)",
+           "same_result_as_gpu": bool(rc == 0 and arrays_sha256(order, gid, rep) == gpu_digest)}
+    ratio = port_reference_ratio(cfg)
+    if ratio:
+        out["port_over_reference_time"] = ratio
+        out["reference_equivalent_value"] = round(f.n / dt * ratio, 1)
+    return out
+
+
 def cpu_baseline(cfg: dict, seconds_hint: float, same_input=None) -> dict | None:
     """CPU baseline on this host, 1 core.
 
-    value: the in-repo restatement (oracle/rk_oracle.c, "port") timed on the SAME
-    arrays the GPU classified (same_input = (Frags, L, gpu result digest)), its
-    result compared with the GPU's.  Beside it: the reference itself on a
-    bounded sample (`reference_sample`), the reference's full-size rate from the
-    build container (`full_size`), and the restatement / reference time ratio on
-    the same full cfg3 input (tests/golden/large_hashes.json) that converts the
-    port's rate into a reference-equivalent one."""
-    from oracle import rk_oracle as ro
-    out = None
-    if same_input is not None:
-        f, L, gpu_digest = same_input
-        t0 = time.perf_counter()
-        rc, gid, rep, order, _ = ro.classify(f.x_start, f.y_start, f.length, f.strand, L, L,
-                                             0.3, 0.3)
-        dt = time.perf_counter() - t0
-        ratio = port_reference_ratio(cfg)
-        out = {"value": round(f.n / dt, 1), "unit": "fragments/s", "cores": 1, "kind": "port",
-               "sample": f"the full {f.n}-fragment input the GPU classified (same arrays, same "
-                         f"host), ratios 0.3/0.3; oracle/rk_oracle.c restatement, one thread "
-                         f"({dt:.2f} s); host: {host_cpu()}",
-               "same_result_as_gpu": bool(rc == 0 and arrays_sha256(order, gid, rep) == gpu_digest)}
-        if ratio:
-            out["port_over_reference_time"] = ratio
-            out["reference_equivalent_value"] = round(f.n / dt * ratio, 1)
+    value: the REFERENCE itself on a bounded sample of the workload
+    (`reference_sample`).  Beside it: the in-repo restatement on the same full
+    arrays the GPU classified (`port_same_input`, result compared with the
+    GPU's), the reference's full-size rate from the build container
+    (`full_size`), and this host's core count."""
     sample = reference_sample(cfg, seconds_hint)
+    port = port_same_input(cfg, same_input) if same_input is not None else None
     full = full_size_reference(cfg)
-    if sample and full:
-        sample["sample_over_full"] = round(sample["value"] / full["value"], 2)
+    out = sample if sample is not None else port
     if out is None:
-        out = sample
-    elif sample:
-        out["reference_sample"] = sample
-    if out is not None and full:
+        return None
+    if out is sample and port is not None:
+        out["port_same_input"] = port
+    if sample is not None and full:
+        out["sample_over_full"] = round(sample["value"] / full["value"], 2)
+    if full:
         out["full_size"] = full
+    out["host"] = host_cores()
     return out
 
 
@@ -703,10 +728,13 @@ def main():
                 line["replicas"] = replicas
     if rank != 0:
         return
-    if not args.no_cpu and world == 1:
+    if not args.no_cpu:
+        # (N > 1: rank 0's host, the reference sample alone -- the arrays of
+        # the whole set are not kept for the restatement there)
         log("cpu baseline")
-        line["cpu_baseline"] = cpu_baseline(cfg, line["ms_per_step"] / 1e3 * args.steps,
-                                            same_input)
+        line["cpu_baseline"] = cpu_baseline(
+            cfg, (line["ms_per_step"] or 0.0) / 1e3 * args.steps,
+            same_input if world == 1 else None)
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)

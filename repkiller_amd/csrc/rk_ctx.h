@@ -56,7 +56,6 @@ struct rk_ctx {
   size_t sh_msg_cap = 0;
   uint64_t sh_fp[8] = {};
   uint32_t sh_blind[2] = {3, 3};
-  uint32_t sh_jumps = 1;  // pointer-jumping rounds it queues
   rk_stats stats{};
   rk_shard_stats shard_stats{};
   std::string err;

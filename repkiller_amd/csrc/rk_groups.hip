@@ -227,6 +227,66 @@ __global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, u
   if (ch) *changed = 1u;
 }
 
+// The first round again, except that an element whose chain is longer than
+// the step budget is listed (list[(*count)++] = k) instead of flagging another
+// round, and k_jump_rest follows only the listed chains: the sharded fast
+// path compresses its slice without reading a flag back between rounds.
+__global__ void k_jump_list(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, uint32_t *list,
+                            uint32_t *count) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k - lane < m;
+       k += gridDim.x * blockDim.x) {
+    bool open = false;
+    if (k < m) {
+      const uint32_t a0 = p.par[k];
+      uint32_t a = a0;
+      if (a > k) {  // parents are always earlier
+        atomicOr(err, ERRB_INTERNAL);
+        a = k;
+        p.par[k] = k;
+      }
+      isnew[k] = a == k;
+      int step = 0;
+      for (; step < 32; ++step) {
+        const uint32_t b = p.par[a];
+        if (b == a) break;
+        a = b;
+      }
+      if (a != a0) p.par[k] = a;
+      open = step == 32;
+    }
+    const uint64_t b = __ballot(open);
+    if (b) {
+      uint32_t at = 0;
+      if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(b));
+      at = (uint32_t)__shfl((int)at, 0);
+      if (open) list[at + __popcll(b & ((1ull << lane) - 1ull))] = k;
+    }
+  }
+}
+
+// the listed chains to their roots (the other listed elements compress the
+// same chains meanwhile); a chain still open after 4096 links (a crafted
+// input) raises *changed
+__global__ void k_jump_rest(Proc p, const uint32_t *list, const uint32_t *count,
+                            uint32_t *changed) {
+  const uint32_t n = *count;
+  bool ch = false;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = list[i];
+    uint32_t a = p.par[k];
+    int step = 0;
+    for (; step < 4096; ++step) {
+      const uint32_t b = p.par[a];
+      if (b == a) break;
+      a = b;
+    }
+    p.par[k] = a;
+    ch |= step == 4096;
+  }
+  if (ch) *changed = 1u;
+}
+
 __global__ void k_assign_gid(Proc p, uint32_t m, const uint32_t *newrank) {
   GRID_STRIDE(k, m) p.gid[k] = newrank[p.par[k]];
 }
@@ -312,6 +372,17 @@ void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t
   kt_begin(st, KID_JUMP);
   k_jump<<<grid_for(m, 256, (size_t)1 << 20), 256, 0, st>>>(p, m, changed, isnew, err);
   kt_end(st, KID_JUMP, (isnew ? 16.0 : 12.0) * m);  // parent, root, parent written (+ new flag)
+}
+void jump_listed(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, uint32_t *list,
+                 uint32_t *count, uint32_t *changed, hipStream_t st) {
+  if (!m) return;
+  (void)hipMemsetAsync(count, 0, 4, st);
+  kt_begin(st, KID_JUMP);
+  k_jump_list<<<grid_for(m, 256, (size_t)1 << 20), 256, 0, st>>>(p, m, isnew, err, list, count);
+  kt_end(st, KID_JUMP, 16.0 * m);
+  kt_begin(st, KID_JUMP);
+  k_jump_rest<<<1024, 256, 0, st>>>(p, list, count, changed);
+  kt_end(st, KID_JUMP, 0.0);
 }
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st) {
   if (!m) return;

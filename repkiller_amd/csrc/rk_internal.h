@@ -243,6 +243,11 @@ void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t 
 // one pointer-jumping round; the first also writes isnew[k] = (par[k] == k)
 void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
                 hipStream_t st);
+// the compression in one pass plus a pass over the chains it left open
+// (list: m words, count: one word; *changed = 1 only for a chain still open
+// after 4096 more links), no host round trip
+void jump_listed(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, uint32_t *list,
+                 uint32_t *count, uint32_t *changed, hipStream_t st);
 void assign_gid(Proc p, uint32_t m, const uint32_t *newrank, hipStream_t st);
 void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t *goff,
                    hipStream_t st);

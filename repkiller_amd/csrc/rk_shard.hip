@@ -649,7 +649,7 @@ enum Slot : int {
   SL_LAB, SL_CUR, SL_REQ, SL_SRC, SL_RQ, SL_RESP, SL_BACK, SL_HREC, SL_MEM, SL_LG, SL_SGID,
   SL_GMEM, SL_GOFF, SL_RECKEY, SL_TAG, SL_OTAG, SL_GSORT, SL_OGID, SL_OREP, SL_OORD, SL_CKEY_Y,
   SL_CENT_Y, SL_CSTATE_Y, SL_CPK_Y, SL_CNBD_Y, SL_CCEN_Y, SL_CLEN_Y, SL_TK2, SL_TV2, SL_RADIX2,
-  SL_YXH, SL_YMASK, SL_YCODE, SL_GMSG, SL_COUNT
+  SL_YXH, SL_YMASK, SL_YCODE, SL_GMSG, SL_JLIST, SL_COUNT
 };
 
 constexpr int kPoolSlots = 160;  // slots of both drivers (rk_shard_nw.h adds its own)
@@ -720,7 +720,6 @@ struct Shard {
   bool alloc_locked = false, alloc_violation = false;
   int sticky = 0;  // a local failure inside such a stage: reported at the next gather
   uint32_t max_sweeps[2] = {0, 0};  // the careful driver's sweeps per axis (X, Y)
-  uint32_t max_jumps = 0;           // and its pointer-jumping rounds
 
   template <class T>
   T *take(int slot, size_t count) {
@@ -1338,10 +1337,7 @@ const uint32_t *resolve_roots(Shard &S, uint32_t *xg, const ParRec *prr, uint32_
       S.zero(S.ctrl + 3, 4);
       jump_round(jp, m, S.ctrl + 3, rounds == 0 ? junk : nullptr, S.ctrl, S.st);
       S.launched("jump_round");
-      if (!S.read1(S.ctrl + 3)) {
-        S.max_jumps = rounds + 1 > S.max_jumps ? rounds + 1 : S.max_jumps;
-        break;
-      }
+      if (!S.read1(S.ctrl + 3)) break;
     }
     exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), S.st);
   }
@@ -1534,7 +1530,6 @@ int classify_sharded_impl(Shard &S, const rk_frags_soa *in, const rk_params *prm
       r = classify_sharded_nw(S, in, p, P, me, N, row_base, lead_in, out, t0);
       for (int a = 0; a < 2; ++a)
         ctx->sh_blind[a] = S.max_sweeps[a] > 3 ? S.max_sweeps[a] : 3u;
-      ctx->sh_jumps = S.max_jumps > 1 ? (S.max_jumps < 8 ? S.max_jumps : 8u) : 1u;
     }
     if (r != RK_SHARD_FALLBACK) {
       if (r) std::memset(ctx->sh_fp, 0, sizeof ctx->sh_fp);

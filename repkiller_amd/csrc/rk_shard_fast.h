@@ -242,9 +242,8 @@ __global__ void __launch_bounds__(256) k_sh_y_results_fast(
 __global__ void k_expect1(const uint32_t *v, uint32_t want, uint32_t *flag, uint32_t bit) {
   if (threadIdx.x == 0 && *v != want) atomicOr(flag, bit);
 }
-__global__ void k_expect_dev(const uint32_t *v, const uint32_t *want, uint32_t *flag,
-                             uint32_t bit) {
-  if (threadIdx.x == 0 && *v != *want) atomicOr(flag, bit);
+__global__ void k_copy_word(const uint32_t *src, uint32_t *dst) {
+  if (threadIdx.x == 0) *dst = *src;
 }
 
 // k_final_gid without the error bit: after a request round that may not be
@@ -348,6 +347,7 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
   S.expect_flag = F;
   S.expect_bit = RETRY_EXPECT;
   ss.fast_path = 1;
+  const bool solo = P == 1;
   auto tphase = std::chrono::steady_clock::now();
 
   // ---- GA: rows, checks, the slice and Y-range histograms ---------------------
@@ -661,8 +661,10 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
   S.hip(hipEventRecord(ctx->fork, st), "fork");
   S.hip(hipStreamWaitEvent(st2, ctx->fork, 0), "fork wait");
   if (ny) {
-    k_sh_ycode<<<grid_for(ny, 256), 256, 0, st2>>>(yr, ny, nby, ylo, yhi, ycode);
-    S.launched("k_sh_ycode");
+    if (!solo) {  // (one rank: no halo classes, no verification, no parents to send)
+      k_sh_ycode<<<grid_for(ny, 256), 256, 0, st2>>>(yr, ny, nby, ylo, yhi, ycode);
+      S.launched("k_sh_ycode");
+    }
     if (!fast) nw_rec_hist(yr, 12, ny, 0, yd, yhist, st2);
   }
   S.hip(hipEventRecord(ctx->join, st2), "join");
@@ -738,7 +740,9 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
     cx.state = S.take<uint8_t>(SN_XSTATE, mx + 1);
     uint32_t *xpos = S.take<uint32_t>(SN_XPOS, mx + 1);
     uint4 *erec = S.take<uint4>(SN_EREC, (size_t)mx * 3 / 4 + 2);
-    uint32_t *par = S.take<uint32_t>(SN_PAR, mx + 1);
+    // one rank: entry ids are processing indices, and both axes write their
+    // decisions straight into the parent words (as on one device)
+    uint32_t *par = solo ? xg : S.take<uint32_t>(SN_PAR, mx + 1);
     nw_x_chunks(Ra, mx, nbx, max_x, maxlen, xoff, cx, xpos, erec, S.ctrl, cc.W, st, hx, G);
     S.launched("X chunks");
     Axis ax{cx.key, cx.ent, nullptr, nullptr, cx.state, nullptr, par, cx.pk, cx.nbd,
@@ -748,11 +752,16 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
                     S.take<uint8_t>(SL_WPEND, mx / 64 + 1), S.take<uint8_t>(SL_RPEND, mx),
                     S.ctrl + 64, S.ctrl + 4};
     S.check(resolve_axis_queued(ctx, ax, sc, ctx->sh_blind[0], F + 3));
-    kt_begin(st, KID_SH_XOWN);
-    k_sh_x_own_fast<<<grid_for(mx, 256), 256, 0, st>>>(xpos, cx.state, par, hx, G, m, poff, xg,
-                                                       xused, slices, me, gc_lk);
-    kt_end(st, KID_SH_XOWN, 0.0);
-    S.launched("k_sh_x_own_fast");
+    if (solo) {  // the X hits as the Y sort's bitmask (k_nw_x_bits, as on one device)
+      nw_x_bits(xpos, cx.state, m, ybits, st);
+      S.launched("k_nw_x_bits");
+    } else {
+      kt_begin(st, KID_SH_XOWN);
+      k_sh_x_own_fast<<<grid_for(mx, 256, 4096), 256, 0, st>>>(xpos, cx.state, par, hx, G, m,
+                                                               poff, xg, xused, slices, me, gc_lk);
+      kt_end(st, KID_SH_XOWN, 0.0);
+      S.launched("k_sh_x_own_fast");
+    }
   }
   // the owners' final states of the lead-in (the same selection as the records)
   if (P > 1) {
@@ -778,7 +787,9 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
 
   // ---- 7: X-hit bytes after the Y records, the Y sort, its sweeps ----------------
   tphase = std::chrono::steady_clock::now();
-  {
+  if (solo) {
+    S.hip(hipStreamWaitEvent(st, ctx->join, 0), "join wait");
+  } else {
     YOp12 xop = yop;
     xop.xg = xg;
     PartPlan xpp;
@@ -805,7 +816,7 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
     nw_y_sort_after_x(yB, yA, ny, yd, yhist, ystat, cy, nby, max_y, ybits, st,
                       reinterpret_cast<const uint4 *>(yr));
     S.launched("Y sort");
-    Axis ay{cy.key, cy.ent, nullptr, nullptr, cy.state, nullptr, par_l, cy.pk, cy.nbd,
+    Axis ay{cy.key, cy.ent, nullptr, nullptr, cy.state, nullptr, solo ? xg : par_l, cy.pk, cy.nbd,
             S.take<uint32_t>(SL_RLEN, ny), S.take<uint32_t>(SL_RBEG, ny), ny, max_y, p.len_ratio,
             p.pos_ratio};
     ay.par_dev = true;
@@ -813,8 +824,12 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
                     S.take<uint8_t>(SL_WPEND, ny / 64 + 1), S.take<uint8_t>(SL_RPEND, ny),
                     S.ctrl + 64, S.ctrl + 4};
     S.check(resolve_axis_queued(ctx, ay, sc, ctx->sh_blind[1], F + 4));
+  }
+  if (ny && !solo) {
     kt_begin(st, KID_SH_YRES);
-    k_sh_y_results_fast<<<grid_for(ny, 256), 256, 0, st>>>(yr, ycode, ny, par_l, ystate, ywin,
+    // (a grid of at most 2048 blocks: each block adds its counts with global
+    // atomics on a few shared words, and 65536 blocks serialised them there)
+    k_sh_y_results_fast<<<grid_for(ny, 256, 2048), 256, 0, st>>>(yr, ycode, ny, par_l, ystate, ywin,
                                                            poff, m, xg, slices, me, gc_pc, gc_rc,
                                                            gc_lk, F);
     kt_end(st, KID_SH_YRES, 0.0);
@@ -881,9 +896,10 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
   uint32_t *cur = S.take<uint32_t>(SL_CUR, m + 1);
   // local parents (X winners; the X misses' Y winners of this rank's slice
   // are in place, the other ranks' arrive with the parent exchange), chains
-  // compressed inside the slice by queued jumping rounds (as many as the
-  // careful driver last needed, at least one; the flag of the last says
-  // whether a chain is still open: checked with the next gather)
+  // compressed inside the slice by a jumping pass and a pass over the chains
+  // it left open (no readback between them; a chain still open after both is
+  // a crafted input: its flag, checked with the next gather, repeats the call
+  // the careful way)
   auto local_roots = [&](const ParRec *prr, uint32_t npar) {
     if (!m) return;
     if (npar) {
@@ -897,18 +913,17 @@ int classify_sharded_fast(Shard &S, const rk_frags_soa *in, const rk_params &p, 
     S.launched("parents");
     Proc jp{};
     jp.par = lpar;
-    for (uint32_t j = 0; j < ctx->sh_jumps; ++j) {
-      S.zero(S.ctrl + 3, 4);
-      jump_round(jp, m, S.ctrl + 3, j == 0 ? junk : nullptr, S.ctrl, st);
-    }
-    S.launched("jump_round");
+    S.zero(S.ctrl + 3, 4);
+    jump_listed(jp, m, junk, S.ctrl, S.take<uint32_t>(SL_JLIST, m + 1), S.ctrl + 10, S.ctrl + 3,
+                st);
+    S.launched("jump_listed");
     exclusive_scan_u32(isroot, lrank, (size_t)m + 1, S.scan_scratch(SL_SCAN, m + 1), st);
   };
   if (P == 1) {
     local_roots(nullptr, 0);
-    if (m) {  // the slice's roots against the Y owner's count of them
-      k_expect_dev<<<1, 64, 0, st>>>(lrank + m, gc_rc, F, RETRY_EXPECT);
-      S.launched("k_expect_dev");
+    if (m) {  // the slice's roots: its new groups
+      k_copy_word<<<1, 64, 0, st>>>(lrank + m, gc_rc);
+      S.launched("k_copy_word");
     }
   }
   k_msg_head<<<1, 64, 0, st>>>(S.ctrl, gc);
