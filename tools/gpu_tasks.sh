@@ -24,6 +24,7 @@
 #   rehearse  the N > 1 bench line on one GPU: 2 and 4 ranks (ARGS) on device 0
 #             over gloo host callbacks, cfg3's one 50M set strong-scaled with
 #             its digest gathered; then the world-1 sharded leg
+#   io        tools/io_bench.py at cfg3 (the file path against the reference)
 #   fast      the sharded fast path: its tests, the sharded suite, rehearsals, world 1
 #   rehearse_rccl  the same over RCCL (which refuses two ranks on one GPU:
 #             value null with the error)
@@ -182,6 +183,12 @@ fast)  # the sharded fast path: its tests, the whole sharded suite, the 2- and 4
     RK_BENCH_SAME_GPU=1 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $W --master-addr 127.0.0.1 --master-port $((29610 + W)) bench.py --gpus $W --comm host --steps 2 --warmup 1 --sharded-timeout 500 > $O/host$W.json 2> $O/host$W.err || exit 3
   done
   bench sharded_w1 --mode sharded --no-cpu --steps 20 --warmup 5 || exit 4
+  ;;
+io)  # the whole file path at cfg3 (CSV in -> classify -> CSV out) against the reference on the same file
+  T=/tmp
+  if [ "$(df -Pk /dev/shm | awk 'NR==2 {print $4}')" -gt 30000000 ]; then T=/dev/shm; fi
+  df -h /tmp /dev/shm > $O/df.txt 2>&1
+  timeout -k 10 1100 python3 -u tools/io_bench.py --tmp $T > $O/io_bench.json 2> $O/io_bench.err || exit 1
   ;;
 rehearse_rccl)  # RCCL refuses two ranks on one GPU: value null with the error
   RK_BENCH_SAME_GPU=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --config cfg2 --steps 3 --warmup 1 --sharded-timeout 60 > $O/rccl2.json 2> $O/rccl2.err

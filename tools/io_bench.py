@@ -9,7 +9,9 @@ and egress (rk_db_write_csv: parallel formatting) around the device path on
 one synthetic file, next to the reference itself (oracle/_ref/ref_driver,
 1 core) on the same file, and checks that both outputs are byte-identical.
 
-  python tools/io_bench.py [--n 10000000] [--genome 600000000]
+  python tools/io_bench.py [--n 50000000] [--genome 3000000000] [--tmp DIR]
+
+(default: cfg3, the headline config: 50M fragments over 3 Gbp)
 
 Prints one JSON line.  Test/benchmark infrastructure: the reference binary is
 only timed and compared against, never used to produce results.
@@ -33,15 +35,39 @@ import torch  # noqa: E402,F401  (one shared HIP runtime)
 import repkiller_amd as rk  # noqa: E402
 
 
+def heartbeat(stop, t0):
+    """A progress line every 30 s on stderr (the reference's run is minutes of silence)."""
+    while not stop.wait(30):
+        print(f"[io_bench] {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+
 def main():
+    import threading
+    stop = threading.Event()
+    threading.Thread(target=heartbeat, args=(stop, time.perf_counter()), daemon=True).start()
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=10_000_000)
-    ap.add_argument("--genome", type=int, default=600_000_000)  # cfg3 density
+    ap.add_argument("--n", type=int, default=50_000_000)
+    ap.add_argument("--genome", type=int, default=3_000_000_000)  # cfg3
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     args = ap.parse_args()
     n, L = args.n, args.genome
-    out = {"fragments": n, "genome_bp": L}
-    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    cpu = "unknown"
+    with open("/proc/cpuinfo") as fh:
+        for line in fh:
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    out = {"fragments": n, "genome_bp": L, "seed": 3,
+           "host": {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": cpu},
+           "note": "ours: rk_db_load_csv (mmap + parallel parse) -> rk_classify (host buffers, "
+                   "PCIe included) -> rk_db_write_csv (parallel formatting); reference: "
+                   "oracle/_ref/ref_driver (the reference's own code, one core) on the same file"}
+    with tempfile.TemporaryDirectory(dir=args.tmp) as d:
         inp = os.path.join(d, "in.csv")
         f = rk.synth(n, L, seed=3)
         rk.write_input_csv(inp, f, L, L)
@@ -62,12 +88,17 @@ def main():
         ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
         if not args.no_ref and os.path.exists(ref):
             theirs = os.path.join(d, "ref.csv")
+            t0 = time.perf_counter()
             p = subprocess.run([ref, inp, theirs, "0.3", "0.3"], capture_output=True, text=True)
+            out["reference_wall_s"] = round(time.perf_counter() - t0, 3)
             t = json.loads(p.stderr.strip().splitlines()[-1])
             out["reference"] = {k: round(t[k], 3) for k in ("load_s", "group_s", "diag_sort_s",
                                                              "save_s")}
             out["reference"]["total_s"] = round(sum(out["reference"].values()), 3)
             out["byte_identical"] = filecmp.cmp(ours, theirs, shallow=False)
+            out["output_bytes"] = os.path.getsize(ours)
+            out["speedup_total"] = round(out["reference"]["total_s"] / out["total_s"], 1)
+    stop.set()
     print(json.dumps(out), flush=True)
 
 
