@@ -448,7 +448,15 @@ def bench_sharded(args, cfg, rank, world, local, dev, ctx) -> dict:
     world independently seeded blocks of n / world rows (no digest)."""
     n_cfg, L = cfg["n"], cfg["genome_len"]
     a, b = row_block(n_cfg, rank, world)
-    one_set = not cfg.get("synth")
+    # the one-set route makes every rank generate the WHOLE set (~64 B per row
+    # with the generator's temporaries) before keeping its block: only when
+    # all ranks' copies fit half of this host's free memory
+    try:
+        import psutil
+        free = psutil.virtual_memory().available
+    except Exception:  # noqa: BLE001 -- unknown: assume it fits
+        free = float("inf")
+    one_set = not cfg.get("synth") and world * n_cfg * 64 <= 0.5 * free
     if one_set:
         f = rk.synth(n_cfg, L, seed=config_seed(args.config), with_ident=False)
         f = rk.Frags(f.x_start[a:b], f.y_start[a:b], f.length[a:b], f.strand[a:b])
