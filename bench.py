@@ -231,8 +231,31 @@ def cpu_baseline(cfg: dict, seconds_hint: float, same_input=None) -> dict | None
         out["sample_over_full"] = round(sample["value"] / full["value"], 2)
     if full:
         out["full_size"] = full
+    node = full_size_on_node(cfg)
+    if node:
+        out["full_size_on_gpu_host"] = node
     out["host"] = host_cores()
     return out
+
+
+def full_size_on_node(cfg: dict) -> dict | None:
+    """The reference on the WHOLE cfg3 file as timed by tools/io_bench.py on a
+    GPU box's host (profiles/r6_io_bench.json, committed; not this run)."""
+    if cfg is not CONFIGS["cfg3"]:
+        return None
+    try:
+        with open(os.path.join(ROOT, "profiles", "r6_io_bench.json")) as fh:
+            e = json.load(fh)
+        r = e["reference"]
+        hot = r["group_s"] + r["diag_sort_s"]
+        return {"value": round(e["fragments"] / hot, 1), "unit": "fragments/s", "cores": 1,
+                "kind": "reference",
+                "sample": f"the full set ({e['fragments']} fragments, the same generator and "
+                          f"seed), group + diag/sort {hot:.1f} s on {e['host']['cpu_model']}; "
+                          f"measured by tools/io_bench.py (profiles/r6_io_bench.json), "
+                          f"not in this run"}
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def port_reference_ratio(cfg: dict):
