@@ -295,6 +295,13 @@ typedef struct rk_db rk_db;
  * RK_E_IO if unreadable, RK_E_COUNT if more Frag lines than the header total. */
 int rk_db_load_csv(const char *path, rk_db **db);
 void rk_db_free(rk_db *db);
+/* A parsed database as a binary SoA cache file: the header
+ * text and every column rk_db_load_csv produced, so a later run skips the
+ * parse (FragmentsDatabase.cpp:17-100).  Loading a cache gives a database
+ * whose classification and egress are byte-identical to the CSV's.
+ * RK_E_IO: cannot open / read / write; RK_E_ARG: not a complete cache file. */
+int rk_db_save_soa(const rk_db *db, const char *path);
+int rk_db_load_soa(const char *path, rk_db **db);
 /* Borrow the SoA view (valid until rk_db_free) and header values. */
 int rk_db_view(const rk_db *db, rk_frags_soa *soa, uint64_t *len_x_hdr, uint64_t *len_y_hdr,
                uint64_t *total_hdr);

@@ -46,7 +46,7 @@ EXPORTS = (
     "rk_get_stats", "rk_std_sort_segments", "rk_set_profiling", "rk_get_phase_ms", "rk_reset_phases", "rk_phase_name",
     "rk_get_kernel_timing", "rk_kernel_count", "rk_kernel_name",
     "rk_db_load_csv", "rk_db_free", "rk_db_view", "rk_db_write_csv",
-    "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
+    "rk_db_save_soa", "rk_db_load_soa", "rk_saver_start", "rk_saver_add", "rk_saver_stop", "rk_synth_generate",
     "rk_synth_write_csv", "rk_comm_create_host", "rk_comm_rccl_id", "rk_comm_create_rccl",
     "rk_comm_destroy", "rk_comm_last_error", "rk_classify_sharded", "rk_get_shard_stats",
     "rk_shard_copy_result", "rk_comm_create_local", "rk_classify_sharded_host",
@@ -182,6 +182,8 @@ def load_library() -> ctypes.CDLL:
         "rk_phase_name": (ctypes.c_char_p, [ctypes.c_int]),
         "rk_db_load_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(vp)]),
         "rk_db_free": (None, [vp]),
+        "rk_db_save_soa": (ctypes.c_int, [vp, ctypes.c_char_p]),
+        "rk_db_load_soa": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(vp)]),
         "rk_db_view": (ctypes.c_int, [vp, ctypes.POINTER(FragsSoA), _u64p, _u64p, _u64p]),
         "rk_db_write_csv": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(Result)]),
         "rk_saver_start": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
@@ -284,14 +286,18 @@ class ClassifyResult:
 class FragmentsDatabase:
     """Parsed fragment CSV (FragmentsDatabase.cpp:17-101 acceptance rules)."""
 
-    def __init__(self, path: str):
+    def __init__(self, path: str, soa: bool = False):
+        """path: the fragment CSV, or with soa=True a binary SoA cache written by
+        save_soa (the parsed columns: no parse at all)."""
         lib = load_library()
         h = ctypes.c_void_p()
-        rc = lib.rk_db_load_csv(path.encode(), ctypes.byref(h))
+        rc = (lib.rk_db_load_soa if soa else lib.rk_db_load_csv)(path.encode(), ctypes.byref(h))
         if rc == -2:
             raise RkError(rc, f"Could not open input file {path}.")
         if rc == -3:
             raise RkError(rc, "Unexpected number of fragments")
+        if rc == -1 and soa:
+            raise RkError(rc, f"{path} is not a complete SoA cache file")
         _check(rc)
         self._h = h
         soa = FragsSoA()
@@ -309,6 +315,18 @@ class FragmentsDatabase:
 
         self.frags = Frags(view(soa.x_start, np.uint64, n), view(soa.y_start, np.uint64, n),
                            view(soa.length, np.uint64, n), view(soa.strand, np.uint8, n))
+
+    @classmethod
+    def load_soa(cls, path: str) -> "FragmentsDatabase":
+        """A database from a binary SoA cache (rk_db_load_soa)."""
+        return cls(path, soa=True)
+
+    def save_soa(self, path: str) -> None:
+        """The parsed columns as a binary SoA cache (rk_db_save_soa)."""
+        rc = load_library().rk_db_save_soa(self._h, path.encode())
+        if rc == -2:
+            raise RkError(rc, f"Could not write {path}")
+        _check(rc)
 
     def getTotalFrags(self) -> int:  # FragmentsDatabase.h:32
         return self.frags.n

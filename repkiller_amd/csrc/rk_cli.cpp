@@ -17,7 +17,9 @@
 // P GPUs, devices N..N+P-1, one thread each: rk_classify_sharded over RCCL),
 // --same-device (all P ranks on device N -- a rehearsal of the sharded path
 // on one GPU), --comm rccl|local (collectives: RCCL, or in-process device
-// copies; default rccl, local with --same-device).
+// copies; default rccl, local with --same-device), --save-soa PATH (after the
+// parse, keep the database as a binary SoA cache), --soa (the input is such a
+// cache: no parse at all).
 #include <chrono>
 #include <thread>
 #include <cstdio>
@@ -32,7 +34,7 @@
 static void print_help() {
   std::printf("Repkiller (MI355X) v0.9.b-compatible\n");
   std::printf("Usage: ./rk_repkiller [--device N] [--gpus P [--same-device] [--comm rccl|local]] "
-              "[--timing] <input_file_path> <output_file_path> "
+              "[--timing] [--save-soa cache.soa | --soa] <input_file_path> <output_file_path> "
               "<length_ratio> <position_ratio> [<length_ratio> <position_ratio>]...\n");
   std::fflush(stdout);
 }
@@ -110,8 +112,8 @@ static int classify_sharded_threads(const rk_frags_soa &soa, int device, int gpu
 
 int main(int argc, char **argv) {
   int device = 0, gpus = 1;
-  bool timing = false, same_device = false;
-  const char *comm_kind = nullptr;
+  bool timing = false, same_device = false, soa_in = false;
+  const char *comm_kind = nullptr, *save_soa = nullptr;
   std::vector<const char *> pos;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
@@ -119,6 +121,8 @@ int main(int argc, char **argv) {
     else if (!std::strcmp(argv[i], "--comm") && i + 1 < argc) comm_kind = argv[++i];
     else if (!std::strcmp(argv[i], "--same-device")) same_device = true;
     else if (!std::strcmp(argv[i], "--timing")) timing = true;
+    else if (!std::strcmp(argv[i], "--soa")) soa_in = true;
+    else if (!std::strcmp(argv[i], "--save-soa") && i + 1 < argc) save_soa = argv[++i];
     else pos.push_back(argv[i]);
   }
   if (gpus < 1 || gpus > 32 ||
@@ -164,7 +168,11 @@ int main(int argc, char **argv) {
   std::fflush(stdout);
   double t0 = now_s();
   rk_db *db = nullptr;
-  int rc = rk_db_load_csv(pos[0], &db);
+  int rc = soa_in ? rk_db_load_soa(pos[0], &db) : rk_db_load_csv(pos[0], &db);
+  if (rc == RK_E_ARG && soa_in) {
+    std::fprintf(stderr, "%s is not a complete SoA cache file.\n", pos[0]);
+    return 1;
+  }
   if (rc == RK_E_IO) {
     std::fprintf(stderr, "Could not open input file %s.\n", pos[0]);
     return 1;
@@ -175,6 +183,11 @@ int main(int argc, char **argv) {
   }
   if (rc) {
     std::fprintf(stderr, "loading %s failed (%d)\n", pos[0], rc);
+    return 1;
+  }
+  if (save_soa && (rc = rk_db_save_soa(db, save_soa))) {
+    std::fprintf(stderr, "writing the SoA cache %s failed (%d)\n", save_soa, rc);
+    rk_db_free(db);
     return 1;
   }
   double t1 = now_s();

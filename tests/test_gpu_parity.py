@@ -271,6 +271,20 @@ def test_cli_matches_reference(tmp_path):
         assert out.read_bytes() == f.read()  # last pair wins (E10)
     p = subprocess.run([rk.CLI_PATH, str(inp), str(out), "0.3"], capture_output=True, text=True)
     assert p.returncode == 1  # odd ratio count: usage error (E9)
+    # the binary SoA cache: written after the parse, then
+    # read instead of the CSV -- the same bytes out
+    cache, out2 = tmp_path / "db.soa", tmp_path / "out2.csv"
+    p = subprocess.run([rk.CLI_PATH, "--save-soa", str(cache), str(inp), str(out), "0.3", "0.3"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    p = subprocess.run([rk.CLI_PATH, "--soa", str(cache), str(out2), "0.3", "0.3"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    with gzip.open(os.path.join(GOLDEN, "corpus10k.out.csv.gz"), "rb") as f:
+        assert out2.read_bytes() == f.read()
+    p = subprocess.run([rk.CLI_PATH, "--soa", str(inp), str(out2), "0.3", "0.3"],
+                       capture_output=True, text=True)
+    assert p.returncode == 1  # a CSV is not a cache
 
 
 def test_std_sort_segments_vs_restatement(gpu_ctx):

@@ -95,3 +95,61 @@ def test_synth_deterministic():
     c = rk.synth(5000, 1_000_000, seed=4)
     assert np.array_equal(a.x_start, b.x_start) and np.array_equal(a.strand, b.strand)
     assert not np.array_equal(a.x_start, c.x_start)
+
+
+@pytest.mark.parametrize("name,case", [(n, c) for n, c in edge_cases()
+                                       if c["expect"] != "error:RK_E_COUNT"],
+                         ids=[n for n, c in edge_cases() if c["expect"] != "error:RK_E_COUNT"])
+def test_soa_cache_edge(tmp_path, name, case):
+    """The binary SoA cache holds every column the parse
+    produced: a database loaded from it writes the reference's output byte for
+    byte (the egress prints xEnd, yEnd, score, similarity and ident from the
+    cache's columns) and has the same SoA view and header values."""
+    db = rk.FragmentsDatabase(os.path.join(EDGE, name + ".in.csv"))
+    cache = tmp_path / "db.soa"
+    db.save_soa(str(cache))
+    db2 = rk.FragmentsDatabase.load_soa(str(cache))
+    assert (db2.len_x_hdr, db2.len_y_hdr, db2.total_hdr) == (db.len_x_hdr, db.len_y_hdr, db.total_hdr)
+    for a, b in zip((db.frags.x_start, db.frags.y_start, db.frags.length, db.frags.strand),
+                    (db2.frags.x_start, db2.frags.y_start, db2.frags.length, db2.frags.strand)):
+        assert np.array_equal(a, b)
+    rc, res = oracle_result(db2, case["len_ratio"], case["pos_ratio"])
+    if case["expect"] != "ref":
+        assert rc != 0
+        return
+    out = tmp_path / "out.csv"
+    db2.save_all_frag_pairs(str(out), res)
+    with open(os.path.join(EDGE, name + ".out.csv"), "rb") as f:
+        assert out.read_bytes() == f.read()
+
+
+def test_soa_cache_corpus_and_damage(tmp_path, corpus):
+    """corpus10k through the cache: the reference's output byte for byte; a
+    truncated, extended or foreign file is refused (RK_E_ARG), a missing one is
+    RK_E_IO."""
+    db = rk.FragmentsDatabase(corpus[0])
+    cache = tmp_path / "db.soa"
+    db.save_soa(str(cache))
+    db2 = rk.FragmentsDatabase.load_soa(str(cache))
+    rc, res = oracle_result(db2, 0.3, 0.3)
+    assert rc == 0
+    out = tmp_path / "out.csv"
+    db2.save_all_frag_pairs(str(out), res)
+    assert out.read_bytes() == corpus[1]
+    raw = cache.read_bytes()
+    for bad in (raw[:-1], raw + b"\0", b"XXXXXXXX" + raw[8:], raw[:40]):
+        p = tmp_path / "bad.soa"
+        p.write_bytes(bad)
+        with pytest.raises(rk.RkError) as e:
+            rk.FragmentsDatabase.load_soa(str(p))
+        assert e.value.code in (-1, -2), e.value.code
+    flipped = bytearray(raw)
+    flipped[60] ^= 0x01  # inside the header text: the checksum catches it
+    p = tmp_path / "flip.soa"
+    p.write_bytes(bytes(flipped))
+    with pytest.raises(rk.RkError) as e:
+        rk.FragmentsDatabase.load_soa(str(p))
+    assert e.value.code == -1
+    with pytest.raises(rk.RkError) as e:
+        rk.FragmentsDatabase.load_soa(str(tmp_path / "nope.soa"))
+    assert e.value.code == -2

@@ -85,6 +85,26 @@ def main():
         out.update(load_s=round(t1 - t0, 3), classify_s=round(t2 - t1, 3),
                    save_s=round(t3 - t2, 3), total_s=round(t3 - t0, 3),
                    host_threads=os.cpu_count())
+        # the binary SoA cache: written once, then a load
+        # with no parse; the classification from it must write the same bytes
+        cache = os.path.join(d, "db.soa")
+        t4 = time.perf_counter()
+        db.save_soa(cache)
+        t5 = time.perf_counter()
+        db2 = rk.FragmentsDatabase.load_soa(cache)
+        t6 = time.perf_counter()
+        res2 = ctx.classify(db2.frags, db2.len_x_hdr, db2.len_y_hdr, 0.3, 0.3)
+        t7 = time.perf_counter()
+        ours2 = os.path.join(d, "ours_soa.csv")
+        db2.save_all_frag_pairs(ours2, res2)
+        t8 = time.perf_counter()
+        out["soa_cache"] = {"bytes": os.path.getsize(cache), "save_s": round(t5 - t4, 3),
+                            "load_s": round(t6 - t5, 3), "classify_s": round(t7 - t6, 3),
+                            "save_csv_s": round(t8 - t7, 3), "total_s": round(t8 - t5, 3),
+                            "same_csv_as_csv_route": filecmp.cmp(ours, ours2, shallow=False)}
+        os.remove(ours2)
+        os.remove(cache)
+        del db2, res2
         ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
         if not args.no_ref and os.path.exists(ref):
             theirs = os.path.join(d, "ref.csv")
