@@ -86,4 +86,41 @@ inline char *put_float(char *o, float f) {
   return o;
 }
 
+// The common spelling of the similarity column ("93.45": optional leading
+// blanks and sign, digits, an optional '.' and digits, nothing after) with at
+// most 7 significant digits: the decimal mantissa m < 2^24 and 10^k (k <= 10)
+// are exact floats, so m / 10^k in float arithmetic is the correctly rounded
+// value strtof returns (Clinger's fast path).  Anything else returns false
+// and the caller uses strtof (tests/cpp/stof_check.cpp compares the two).
+inline bool fast_stof(const char *p, const char *e, float *out) {
+  while (p < e && (*p == ' ' || (*p >= '\t' && *p <= '\r'))) ++p;
+  bool neg = false;
+  if (p < e && (*p == '+' || *p == '-')) neg = *p++ == '-';
+  uint32_t m = 0;
+  int digits = 0, frac = 0;
+  bool any = false, dot = false;
+  for (; p < e; ++p) {
+    const char c = *p;
+    if (c >= '0' && c <= '9') {
+      any = true;
+      if (m == 0 && c == '0') {  // leading zeros add no significant digit
+        if (dot) ++frac;
+        continue;
+      }
+      if (++digits > 7) return false;
+      m = m * 10 + (uint32_t)(c - '0');
+      if (dot) ++frac;
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      return false;
+    }
+  }
+  if (!any || frac > 10) return false;
+  static const float p10[] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+  const float v = (float)m / p10[frac];
+  *out = neg ? -v : v;
+  return true;
+}
+
 }  // namespace rk

@@ -85,6 +85,7 @@ uint64_t parse_atoll(const char *p, const char *e) {
 // std::stof: strtof on the field's c_str(); throws (=> line rejected) when no
 // characters convert or errno == ERANGE.
 bool parse_stof(const char *p, const char *e, float *out) {
+  if (rk::fast_stof(p, e, out)) return true;
   char small[96];
   std::string big;
   size_t n = (size_t)(e - p);
@@ -266,14 +267,23 @@ extern "C" int rk_db_load_csv(const char *path, rk_db **out) {
     db->x_start.resize(n), db->y_start.resize(n), db->x_end.resize(n), db->y_end.resize(n);
     db->length.resize(n), db->score.resize(n), db->ident.resize(n);
     db->similarity.resize(n), db->strand.resize(n);
-    size_t i = 0;
-    for (auto &v : parts)
-      for (auto &r : v) {
+    // every part into the columns at its offset, one thread per part
+    std::vector<size_t> at(nt + 1, 0);
+    for (unsigned t = 0; t < nt; ++t) at[t + 1] = at[t] + parts[t].size();
+    auto place = [&](unsigned t) {
+      size_t i = at[t];
+      for (const Row &r : parts[t]) {
         db->x_start[i] = r.xs, db->y_start[i] = r.ys, db->x_end[i] = r.xe, db->y_end[i] = r.ye;
         db->length[i] = r.len, db->score[i] = r.score, db->ident[i] = r.ident;
         db->similarity[i] = r.sim, db->strand[i] = r.strand;
         ++i;
       }
+      std::vector<Row>().swap(parts[t]);
+    };
+    std::vector<std::thread> th2;
+    for (unsigned t = 1; t < nt; ++t) th2.emplace_back(place, t);
+    place(0);
+    for (auto &t : th2) t.join();
   }
   *out = db;
   return RK_OK;
@@ -518,7 +528,26 @@ int write_csv(const rk_db *db, const char *path, const uint32_t *gid, const uint
       }
       char *const b0 = bufs[c].get();
       char *o = b0;
+      // the rows come in output order, i.e. scattered over the nine columns:
+      // each row's column words are prefetched PF rows ahead, so a thread
+      // keeps that many rows' cache misses in flight instead of one
+      constexpr uint64_t PF = 12;
+      auto prefetch_row = [&](uint64_t k) {
+        const uint32_t i = order[k];
+        if (i >= n_rows) return;
+        __builtin_prefetch(&db->x_start[i]);
+        __builtin_prefetch(&db->y_start[i]);
+        __builtin_prefetch(&db->x_end[i]);
+        __builtin_prefetch(&db->y_end[i]);
+        __builtin_prefetch(&db->strand[i]);
+        __builtin_prefetch(&db->length[i]);
+        __builtin_prefetch(&db->score[i]);
+        __builtin_prefetch(&db->ident[i]);
+        __builtin_prefetch(&db->similarity[i]);
+      };
+      for (uint64_t k = k0; k < k1 && k < k0 + PF; ++k) prefetch_row(k);
       for (uint64_t k = k0; k < k1; ++k) {
+        if (k + PF < k1) prefetch_row(k + PF);
         const uint32_t i = order[k];
         if (i >= n_rows) {
           bad = true;
