@@ -99,7 +99,9 @@ typedef struct {
   uint32_t wire;            /* rk_classify*: 1 when the rows crossed PCIe as 12-B wire
                                records (order + flag back, gids rebuilt on the host), 0
                                when as the SoA */
-  uint32_t reserved;
+  uint32_t sweep_repeats;   /* record pipeline: ratio pairs whose queued sweeps left an axis
+                               open, repeated with a readback per sweep (0 on the BASELINE
+                               configs) */
   /* rk_classify*: NUMA nodes of the host side of the last upload (-1: unknown /
      not bound): the caller's input pages, the node the packing threads were
      bound to (RK_IO_NUMA=0: never bound), the pinned staging slots, the GPU */

@@ -89,7 +89,7 @@ class Stats(ctypes.Structure):
                 ("device_ms", ctypes.c_double), ("pipeline", ctypes.c_uint32),
                 ("record_fallback", ctypes.c_uint32), ("h2d_ms", ctypes.c_double),
                 ("d2h_ms", ctypes.c_double), ("wire", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32), ("numa_input", ctypes.c_int32),
+                ("sweep_repeats", ctypes.c_uint32), ("numa_input", ctypes.c_int32),
                 ("numa_threads", ctypes.c_int32), ("numa_staging", ctypes.c_int32),
                 ("numa_gpu", ctypes.c_int32)]
 

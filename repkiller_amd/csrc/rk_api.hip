@@ -616,56 +616,83 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
   mark(ctx, RK_PH_OCC_CSR);
   rk::SweepScratch sc{w.runs, w.wpend, reinterpret_cast<uint8_t *>(w.rpend), w.ctrl + 64,
                       w.ctrl + 2};
+  // Both axes' sweeps are queued without a host round trip (RK_SWEEP_QUEUED=0:
+  // the readback after each axis' third sweep); whether either axis was left
+  // open comes back with the roots' first readback (ctrl[10], ctrl[11]), and
+  // a pair left open repeats its axes the careful way (no input of the
+  // BASELINE configs needs more than three sweeps an axis)
+  static const bool queued_on = [] {
+    const char *e = getenv("RK_SWEEP_QUEUED");
+    return !(e && e[0] == '0');
+  }();
+  static const uint32_t blind = [] {
+    const char *e = getenv("RK_SWEEP_BLIND");
+    const int v = e ? atoi(e) : 3;
+    return (uint32_t)(v < 1 ? 1 : v > 8 ? 8 : v);
+  }();
   for (uint32_t q = 0; q < npairs; ++q) {
     const rk_params &pq = prms[q];
     rk_result *out = &outs[q];
     const bool prof = q == 0;
-    if (q > 0) HIPCHK(ctx, hipMemsetAsync(w.cx.state, rk::ST_UNKNOWN, m, st));
+    uint32_t rounds = 0, G = 0;
+    bool narrow_keys = true;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+    const bool queued = queued_on && attempt == 0;
+    if (q > 0 || attempt > 0) HIPCHK(ctx, hipMemsetAsync(w.cx.state, rk::ST_UNKNOWN, m, st));
+    // (the open flags: zero from the call's start for the first pair)
+    if (queued && q > 0) HIPCHK(ctx, hipMemsetAsync(w.ctrl + 10, 0, 2 * sizeof(uint32_t), st));
     if (prof) mark(ctx, RK_PH_SWEEP_X);
     // X decisions: hits' parents (X winner); the X states become a bitmask after
     rk::Axis ax{w.cx.key, w.cx.ent, nullptr, nullptr, w.cx.state, nullptr, w.par,
                 w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
                 pq.pos_ratio};
-    uint32_t sweeps = 0;
-    if ((rc = rk::resolve_axis(ctx, ax, sc, true, &sweeps))) return rc;
+    uint32_t sweeps = blind;
+    if ((rc = queued ? rk::resolve_axis_queued(ctx, ax, sc, blind, w.ctrl + 10)
+                     : rk::resolve_axis(ctx, ax, sc, true, &sweeps)))
+      return rc;
     ctx->stats.x_sweeps = sweeps;
     if (prof) mark(ctx, RK_PH_SWEEP_Y);
     rk::nw_x_bits(w.xpos, w.cx.state, m, w.xbits, st);
-    if (q == 0 && y_overlap) {  // the Y sort's last pass writes the CSR and the Y states
+    if (q == 0 && attempt == 0 && y_overlap) {  // the Y sort's last pass writes the CSR and the Y states
       HIPCHK(ctx, hipStreamWaitEvent(st, ctx->join, 0));
       rk::nw_y_sort_tail(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y,
                          w.xbits, st);
-    } else if (q == 0 && ysplit) {
+    } else if (q == 0 && attempt == 0 && ysplit) {
       // (the order records are done with after the X chunk kernel; the order
       // sort's segment counts after its segment kernel)
       rk::nw_y_sort_split_after_x(w.yrec, w.Rb, w.Ra, m, yp, w.yhist, w.ystatus, w.cy, pl.nby,
                                   pl.max_y, w.xbits, w.chist, w.coff, ss, st);
-    } else if (q == 0) {
+    } else if (q == 0 && attempt == 0) {
       rk::nw_y_sort_after_x(w.yrec, w.Rb, m, yd, w.yhist, w.ystatus, w.cy, pl.nby, pl.max_y,
                             w.xbits, st);
-    } else  // later ratio pairs: the same CSR, new X results
+    } else  // later ratio pairs, or a repeat: the same CSR, new X results
       rk::nw_fill_y(w.cy.ent, w.xbits, w.cy.state, m, st);
     rk::Axis ay{w.cy.key, w.cy.ent, nullptr, nullptr, w.cy.state, nullptr, w.par,
                 w.cy.pk, w.cy.nbd, w.rlen_at, w.rbeg_at, m, pl.max_y, pq.len_ratio,
                 pq.pos_ratio};
     ay.par_dev = true;
-    if ((rc = rk::resolve_axis(ctx, ay, sc, true, &sweeps))) return rc;
+    sweeps = blind;
+    if ((rc = queued ? rk::resolve_axis_queued(ctx, ay, sc, blind, w.ctrl + 11)
+                     : rk::resolve_axis(ctx, ay, sc, true, &sweeps)))
+      return rc;
     ctx->stats.y_sweeps = sweeps;
 
     // group roots and ids
     if (prof) mark(ctx, RK_PH_ROOTS);
     rk::Proc pr{};
     pr.par = w.par;
-    bool narrow_keys = true;
     // (the first round's changed-count with the scan's end word, one launch;
     // later pairs' member histograms too -- the first pair's are still zero)
     rk::zero_regions(st, {{w.isnew + m, sizeof(uint32_t)},
                           {w.ctrl + 5, sizeof(uint32_t)},
                           {q > 0 ? w.ehist : nullptr, 4096 * sizeof(uint32_t)}});
-    uint32_t rounds = 0, G = 0;
+    rounds = 0;
+    G = 0;
+    bool open_axes = false;
     for (;;) {
       if (rounds > 0) HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
-      rk::jump_round(pr, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st);
+      rk::jump_round(pr, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st,
+                     queued && rounds == 0 ? w.ctrl + 10 : nullptr);
       if (rounds == 0) {
         // the new-group flags are final after the first round: their scan
         // (the group count G, in ctrl[32]) shares the round's readback
@@ -673,7 +700,12 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
         HIPCHK(ctx, hipMemcpyAsync(w.ctrl + 32, w.newrank + m, sizeof(uint32_t),
                                    hipMemcpyDeviceToDevice, st));
       }
-      if ((rc = readback(ctx, w.ctrl + 5, 28))) return rc;  // + the wide-key flag, G
+      // + the wide-key flag, the queued axes' open flags, G
+      if ((rc = readback(ctx, w.ctrl + 5, 28))) return rc;
+      if (rounds == 0 && queued && (ctx->host[5] || ctx->host[6])) {
+        open_axes = true;  // an axis was left open: this pair again, the careful way
+        break;
+      }
       if (rounds == 0) G = ctx->host[27];
       ++rounds;
       narrow_keys = ctx->host[1] == 0;
@@ -682,6 +714,9 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
         ctx->err = "pointer jumping did not converge";
         return RK_E_INTERNAL;
       }
+    }
+    if (!open_axes) break;
+    ++ctx->stats.sweep_repeats;
     }
     ctx->stats.jump_rounds = rounds;
     out->n_groups = G;

@@ -202,7 +202,9 @@ __global__ void __launch_bounds__(256) k_group_offsets(const uint32_t *sgid, uin
 // concurrently, which only ever replaces a parent by one of its ancestors.
 // Winner chains are short, so one round usually finishes; a chain longer than
 // the step budget reports `changed` and the host runs another round.
-__global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err) {
+__global__ void k_jump(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
+                       const uint32_t *open) {
+  if (open && (open[0] | open[1])) return;  // parents not final: the caller repeats the axes
   bool ch = false;
   GRID_STRIDE(k, m) {
     const uint32_t a0 = p.par[k];
@@ -367,10 +369,10 @@ void group_offsets(const uint32_t *sgid, uint32_t m, uint32_t ngroups, uint32_t 
   kt_end(st, KID_GROUP_OFFSETS, 4.0 * m + 4.0 * ngroups);
 }
 void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
-                hipStream_t st) {
+                hipStream_t st, const uint32_t *open) {
   if (!m) return;
   kt_begin(st, KID_JUMP);
-  k_jump<<<grid_for(m, 256, (size_t)1 << 20), 256, 0, st>>>(p, m, changed, isnew, err);
+  k_jump<<<grid_for(m, 256, (size_t)1 << 20), 256, 0, st>>>(p, m, changed, isnew, err, open);
   kt_end(st, KID_JUMP, (isnew ? 16.0 : 12.0) * m);  // parent, root, parent written (+ new flag)
 }
 void jump_listed(Proc p, uint32_t m, uint32_t *isnew, uint32_t *err, uint32_t *list,

@@ -240,9 +240,11 @@ void csr_fill_x(Csr c, const ulonglong2 *xrec, uint32_t m, uint64_t max_index, h
 // Y list) else UNKNOWN
 void csr_fill_y(Csr c, const ulonglong2 *yrec, const uint32_t *ylenhi, uint32_t m,
                 uint64_t max_index, hipStream_t st);
-// one pointer-jumping round; the first also writes isnew[k] = (par[k] == k)
+// one pointer-jumping round; the first also writes isnew[k] = (par[k] == k).
+// open (optional, device): when open[0] | open[1] is set the parents are not
+// final (an axis was left open) and the round does nothing
 void jump_round(Proc p, uint32_t m, uint32_t *changed, uint32_t *isnew, uint32_t *err,
-                hipStream_t st);
+                hipStream_t st, const uint32_t *open = nullptr);
 // the compression in one pass plus a pass over the chains it left open
 // (list: m words, count: one word; *changed = 1 only for a chain still open
 // after 4096 more links), no host round trip

@@ -406,7 +406,7 @@ r = ctx.classify(f, 40_000_000, 40_000_000)
 h = hashlib.sha256()
 for a in (r.out_order, r.gid, r.repval):
     h.update(np.ascontiguousarray(a).tobytes())
-print(h.hexdigest(), r.n_groups)
+print(h.hexdigest(), r.n_groups, ctx.stats()["sweep_repeats"])
 """
 
 
@@ -427,8 +427,12 @@ def test_schedule_switches_repeat_rich(gpu_ctx, env):
     out = subprocess.run(["python", "-c", _RICH_SCRIPT, str(ROOT)], capture_output=True,
                          text=True, timeout=120, env={**os.environ, k: v})
     assert out.returncode == 0, out.stderr[-2000:]
-    digest, ng = out.stdout.split()
+    digest, ng, repeats = out.stdout.split()
     assert digest == h.hexdigest() and int(ng) == r.n_groups
+    # the queued sweeps (3 an axis) finish this set; one queued sweep does not,
+    # and the pair repeats the careful way with the same result
+    assert gpu_ctx.stats()["sweep_repeats"] == 0
+    assert int(repeats) == (1 if env == "RK_SWEEP_BLIND=1" else 0)
 
 
 _KILLER_SCRIPT = r"""
@@ -569,14 +573,15 @@ r = ctx.classify(f, 18_000_000, 18_000_000)
 h = hashlib.sha256()
 for a in (r.out_order, r.gid, r.repval):
     h.update(np.ascontiguousarray(a).tobytes())
-print(h.hexdigest(), r.n_groups)
+print(h.hexdigest(), r.n_groups, ctx.stats()["sweep_repeats"])
 """
 
 
 @pytest.mark.parametrize("env", ["RK_GS_BIG=0", "RK_GS_BIG=4", "RK_GS_REG1=0", "RK_GS_SMALL1=1",
                                  "RK_SWEEP_BLIND=1", "RK_NW_MINBITS=8",
                                  "RK_NW_SPLIT=0", "RK_GS_HALF=256", "RK_GS_HALF=2048",
-                                 "RK_NW_YSPLIT=0", "RK_NW_MSPLIT=1", "RK_Y_OVERLAP=1"])
+                                 "RK_NW_YSPLIT=0", "RK_NW_MSPLIT=1", "RK_Y_OVERLAP=1",
+                                 "RK_SWEEP_QUEUED=0"])
 def test_schedule_switches_bit_identical(gpu_ctx, env):
     """The measurement switches only move work between streams or change the
     radix of a pass: the result must not change.  300k rows at cfg3 density
@@ -591,5 +596,9 @@ def test_schedule_switches_bit_identical(gpu_ctx, env):
     out = subprocess.run(["python", "-c", _SWITCH_SCRIPT, str(ROOT)], capture_output=True,
                          text=True, timeout=120, env={**os.environ, k: v})
     assert out.returncode == 0, out.stderr[-2000:]
-    digest, ng = out.stdout.split()
+    digest, ng, repeats = out.stdout.split()
     assert digest == h.hexdigest() and int(ng) == r.n_groups
+    # the queued sweeps (3 an axis) finish this set; one queued sweep does not,
+    # and the pair repeats the careful way with the same result
+    assert gpu_ctx.stats()["sweep_repeats"] == 0
+    assert int(repeats) == (1 if env == "RK_SWEEP_BLIND=1" else 0)
