@@ -477,8 +477,19 @@ bool record_pipeline_enabled() {
 }
 
 int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, uint32_t npairs,
-                    rk_result *outs, const Plan &pl, bool *fallback, const uint3 *wire) {
+                    rk_result *outs, const Plan &pl, bool *fallback, const uint3 *wire,
+                    bool fused_roots = true) {
   *fallback = false;
+  // The roots and gids in one pass after a scan of the parents' root flags
+  // (k_nw_assign_jump; RK_ROOTS_FUSED=0: pointer-jumping rounds, each read
+  // back, then the flag scan and k_nw_assign).  A chain still open after 4128
+  // steps (none in the BASELINE configs) makes the call classify again the
+  // round-by-round way.
+  static const bool fused_on = [] {
+    const char *e = getenv("RK_ROOTS_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  fused_roots = fused_roots && fused_on;
   const uint32_t n = (uint32_t)pl.n;
   NWork w{};
   int rc = ensure_nw_small(ctx, w);
@@ -681,14 +692,32 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (prof) mark(ctx, RK_PH_ROOTS);
     rk::Proc pr{};
     pr.par = w.par;
+    rounds = 0;
+    G = 0;
+    bool open_axes = false;
+    if (fused_roots) {
+      // the new-group ranks from the parents' root flags (G in ctrl[32]) and
+      // the wide-key flag, the queued axes' open flags, G back in one readback;
+      // later pairs' member histograms and listed-chain count cleared first
+      rk::zero_regions(st, {{q > 0 ? w.ehist : nullptr, 4096 * sizeof(uint32_t)},
+                            {q > 0 ? w.ctrl + 12 : nullptr, sizeof(uint32_t)}});
+      rk::exclusive_scan_roots(w.par, m, w.newrank, ss, st);
+      HIPCHK(ctx, hipMemcpyAsync(w.ctrl + 32, w.newrank + m, sizeof(uint32_t),
+                                 hipMemcpyDeviceToDevice, st));
+      if ((rc = readback(ctx, w.ctrl + 5, 28))) return rc;
+      if (queued && (ctx->host[5] || ctx->host[6])) {
+        open_axes = true;  // an axis was left open: this pair again, the careful way
+      } else {
+        G = ctx->host[27];
+        narrow_keys = ctx->host[1] == 0;
+        rounds = 1;
+      }
+    } else {
     // (the first round's changed-count with the scan's end word, one launch;
     // later pairs' member histograms too -- the first pair's are still zero)
     rk::zero_regions(st, {{w.isnew + m, sizeof(uint32_t)},
                           {w.ctrl + 5, sizeof(uint32_t)},
                           {q > 0 ? w.ehist : nullptr, 4096 * sizeof(uint32_t)}});
-    rounds = 0;
-    G = 0;
-    bool open_axes = false;
     for (;;) {
       if (rounds > 0) HIPCHK(ctx, hipMemsetAsync(w.ctrl + 5, 0, sizeof(uint32_t), st));
       rk::jump_round(pr, m, w.ctrl + 5, rounds == 0 ? w.isnew : nullptr, w.ctrl, st,
@@ -715,6 +744,7 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
         return RK_E_INTERNAL;
       }
     }
+    }
     if (!open_axes) break;
     ++ctx->stats.sweep_repeats;
     }
@@ -737,7 +767,11 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     const bool msplit = mp.coarse.passes > 0;
     // (ehist: zero -- cleared at the start, or with the roots' words for q > 0)
     // gids into isnew's words (dead after the scan)
-    rk::nw_assign(w.par, w.newrank, w.isnew, m, msplit ? mp.coarse : ed, w.ehist, st);
+    if (fused_roots)  // (otag: free until the group sort)
+      rk::nw_assign_jump(w.par, w.newrank, w.isnew, m, msplit ? mp.coarse : ed, w.ehist, w.otag,
+                         w.ctrl, st);
+    else
+      rk::nw_assign(w.par, w.newrank, w.isnew, m, msplit ? mp.coarse : ed, w.ehist, st);
 
     // members (stable by gid => processing order), in-group order, flags
     if (prof) mark(ctx, RK_PH_MEMBERS);
@@ -767,7 +801,11 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     if (prof) mark(ctx, RK_N_PHASES);
   }
   HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
-  if ((rc = readback(ctx, w.ctrl, npairs == 1 ? 34 : 1))) return rc;
+  if ((rc = readback(ctx, w.ctrl, npairs == 1 ? 34 : 14))) return rc;
+  if (fused_roots && ctx->host[13]) {  // a parent chain above 4128 steps: round by round
+    collect_phases(ctx);
+    return classify_narrow(ctx, in, prms, npairs, outs, pl, fallback, wire, false);
+  }
   if (npairs == 1 && m && ctx->host[33]) {  // heap segments: sorted now, then the result again
     const uint32_t G = outs[0].n_groups;
     if ((rc = rk::sort_groups_heap_deferred(G, m, w.reckey, w.tag, w.otag, w.gsort, ctx->host[33],

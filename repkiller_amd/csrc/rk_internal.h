@@ -48,6 +48,10 @@ struct ScanScratch {
 size_t scan_blocks(size_t n);
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
                         hipStream_t st);
+// out[k] = number of roots (par[j] == j) among j < k, for k <= m: the
+// new-group ranks straight from the parents (out[m] = the group count)
+void exclusive_scan_roots(const uint32_t *par, uint32_t m, uint32_t *out, ScanScratch ss,
+                          hipStream_t st);
 
 // Launch-level HIP-event timing of the pipeline's kernels, active only while a
 // context profiles (rk_set_profiling): rk_classify_device points g_ktimer at
@@ -426,6 +430,12 @@ void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32
                hipStream_t st);
 void nw_assign(const uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uint32_t m,
                const NwDigits &e, uint32_t *ehist, hipStream_t st);
+// the roots and gids in one pass after exclusive_scan_roots (list: m words of
+// scratch; ctrl[12] its count (zero on entry), ctrl[13] = 1 when a chain stayed open after
+// 4128 steps, ctrl[0] |= ERRB_INTERNAL on a parent after its child)
+void nw_assign_jump(uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uint32_t m,
+                    const NwDigits &e, uint32_t *ehist, uint32_t *list, uint32_t *ctrl,
+                    hipStream_t st);
 void nw_member_sort(const uint4 *erec, const uint32_t *gidp, uint4 *t0, uint4 *t1, uint32_t m,
                     const NwDigits &e, const uint32_t *ehist, uint32_t *status, uint32_t *sgid,
                     uint64_t *key, uint32_t *tag, uint32_t *mrow, bool narrow_keys,

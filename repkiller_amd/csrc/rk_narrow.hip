@@ -34,6 +34,7 @@
 //   * group members {gid, row, sort key} are sorted by gid with the records
 //     carried (12 B when every sort key fits 32 bits, else 16 B), straight
 //     into the arrays the in-group sort reads.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <utility>
@@ -1188,6 +1189,104 @@ __global__ void __launch_bounds__(256) k_nw_assign(const uint32_t *__restrict__ 
   hist_flush(L, D, ghist);
 }
 
+// The roots and the gids in one pass (the new-group ranks already scanned from
+// the parents' root flags, exclusive_scan_roots): each member chases its
+// parent chain up to `steps` steps, writes the root back as its parent (so
+// later chases are short), and its gid = newrank[root] with the member sort's
+// digit histograms; a longer chain is listed for k_nw_assign_rest.  Replaces
+// k_jump's first round + the flag scan + k_nw_assign (their flag array
+// written and read, the parents read twice).
+//
+// Every gid written is below G = newrank[m], whatever happens: each of the G
+// roots (par[r] == r, never rewritten) takes its own rank, so no group is
+// empty and the member sort and the group sort downstream stay in bounds even
+// when a chain is left open (*open: the caller then classifies again the
+// round-by-round way) or a parent is corrupt (ERRB_INTERNAL: the call fails).
+
+// chase from `a` at most `steps` steps; stops at a root (true) or at a parent
+// not before its child (error bit; `a` is then taken as the end)
+__device__ __forceinline__ bool chase_root(const uint32_t *par, uint32_t &a, int steps,
+                                           uint32_t *err) {
+  for (int step = 0; step < steps; ++step) {
+    const uint32_t b = par[a];
+    if (b == a) return true;
+    if (b > a) {  // parents are always earlier
+      atomicOr(err, ERRB_INTERNAL);
+      return true;
+    }
+    a = b;
+  }
+  return par[a] == a;
+}
+__device__ __forceinline__ uint32_t gid_of(const uint32_t *newrank, uint32_t a, uint32_t G) {
+  const uint32_t g = newrank[a];
+  return g < G ? g : G - 1u;  // (only a corrupt parent or an open chain needs the clamp)
+}
+
+__global__ void __launch_bounds__(256) k_nw_assign_jump(uint32_t *__restrict__ par,
+                                                        const uint32_t *__restrict__ newrank,
+                                                        uint32_t *__restrict__ gidp, uint32_t m,
+                                                        Digits D, uint32_t *__restrict__ ghist,
+                                                        uint32_t *__restrict__ list,
+                                                        uint32_t *__restrict__ count,
+                                                        uint32_t *__restrict__ err, int steps) {
+  __shared__ HistLds L;
+  hist_init(L);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t G = newrank[m];  // >= 1: the first fragment always opens a group
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k - lane < m;
+       k += gridDim.x * blockDim.x) {
+    bool open = false;
+    if (k < m) {
+      const uint32_t a0 = par[k];
+      uint32_t a = a0;
+      bool done;
+      if (a0 > k) {  // corrupt: taken as its own root
+        atomicOr(err, ERRB_INTERNAL);
+        a = k;
+        done = true;
+      } else {
+        done = chase_root(par, a, steps, err);
+        if (a != a0) par[k] = a;
+      }
+      open = !done;
+      if (done) {
+        const uint32_t g = gid_of(newrank, a, G);
+        gidp[k] = g;
+        hist_add(L, D, g);
+      }
+    }
+    const uint64_t b = __ballot(open);
+    if (b) {
+      uint32_t at = 0;
+      if (lane == 0) at = atomicAdd(count, (uint32_t)__popcll(b));
+      at = (uint32_t)__shfl((int)at, 0);
+      if (open) list[at + __popcll(b & ((1ull << lane) - 1ull))] = k;
+    }
+  }
+  __syncthreads();
+  hist_flush(L, D, ghist);
+}
+
+// the listed chains, followed further (up to `steps` more); a chain still open
+// sets *open and takes a clamped gid (the caller classifies again)
+__global__ void k_nw_assign_rest(uint32_t *par, const uint32_t *newrank, uint32_t *gidp,
+                                 uint32_t m, Digits D, uint32_t *ghist, const uint32_t *list,
+                                 const uint32_t *count, uint32_t *open, uint32_t *err,
+                                 int steps) {
+  const uint32_t n = *count, G = newrank[m];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = list[i];
+    uint32_t a = par[k];
+    if (!chase_root(par, a, steps, err)) *open = 1u;
+    par[k] = a;
+    const uint32_t g = gid_of(newrank, a, G);
+    gidp[k] = g;
+    for (int p = 0; p < D.passes; ++p) atomicAdd(&ghist[p * 1024 + D.digit(p, g)], 1u);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // widest digit of the record sorts (RK_NW_BITS=8..10 for measurements): 8-bit
 // digits measured fastest at cfg3 (a 16-B record pass 0.49 ms against 0.69 ms
@@ -2050,6 +2149,29 @@ void nw_fill_y(const uint32_t *ent, const uint32_t *bits, uint8_t *state, uint32
   kt_begin(st, KID_NW_FILLY);
   k_nw_fill_y<<<grid_for(m, 256), 256, 0, st>>>(ent, bits, state, m);
   kt_end(st, KID_NW_FILLY, 5.0 * m);
+}
+
+void nw_assign_jump(uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uint32_t m,
+                    const NwDigits &e, uint32_t *ehist, uint32_t *list, uint32_t *ctrl,
+                    hipStream_t st) {
+  if (!m) return;
+  // the step budgets (RK_ROOTS_STEPS / RK_ROOTS_REST_STEPS: test hooks for the
+  // listed chains and the round-by-round fallback)
+  static const int steps1 = [] {
+    const char *e = getenv("RK_ROOTS_STEPS");
+    return e ? std::max(1, atoi(e)) : 32;
+  }();
+  static const int steps2 = [] {
+    const char *e = getenv("RK_ROOTS_REST_STEPS");
+    return e ? std::max(1, atoi(e)) : 4096;
+  }();
+  kt_begin(st, KID_NW_ASSIGN);
+  k_nw_assign_jump<<<grid_for(m, 256, 2048), 256, 0, st>>>(par, newrank, gidp, m, to_digits(e),
+                                                           ehist, list, ctrl + 12, ctrl, steps1);
+  // parent, root (+ its parent), parent back, root's rank, gid
+  kt_end(st, KID_NW_ASSIGN, 20.0 * m);
+  k_nw_assign_rest<<<256, 256, 0, st>>>(par, newrank, gidp, m, to_digits(e), ehist, list,
+                                        ctrl + 12, ctrl + 13, ctrl, steps2);
 }
 
 void nw_assign(const uint32_t *par, const uint32_t *newrank, uint32_t *gidp, uint32_t m,

@@ -55,14 +55,37 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *tot) {
   return pre + inc - v;
 }
 
-__global__ void __launch_bounds__(SCAN_THREADS) k_reduce_tiles(const uint32_t *in, size_t n,
+// the scanned words: an array, or the root flags (par[k] == k, k < m) of a
+// parent array -- the new-group ranks straight from the parents, no flag array
+struct WordsIn {
+  const uint32_t *in;
+  __device__ __forceinline__ uint4 load(size_t base, size_t n) const { return load4(in, base, n); }
+};
+struct RootsIn {
+  const uint32_t *par;
+  size_t m;
+  __device__ __forceinline__ uint4 load(size_t base, size_t) const {
+    if (base + 3 < m) {
+      const uint4 p = *reinterpret_cast<const uint4 *>(par + base);
+      return make_uint4(p.x == base, p.y == base + 1, p.z == base + 2, p.w == base + 3);
+    }
+    uint4 v = {0, 0, 0, 0};
+    if (base + 0 < m) v.x = par[base + 0] == base + 0;
+    if (base + 1 < m) v.y = par[base + 1] == base + 1;
+    if (base + 2 < m) v.z = par[base + 2] == base + 2;
+    return v;
+  }
+};
+
+template <class In>
+__global__ void __launch_bounds__(SCAN_THREADS) k_reduce_tiles(const In in, size_t n,
                                                                uint32_t *sums) {
   __shared__ uint32_t red[SCAN_THREADS / 64];
   const size_t tile = (size_t)blockIdx.x * SCAN_TILE;
   uint32_t s = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    uint4 v = load4(in, tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n);
+    uint4 v = in.load(tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n);
     s += v.x + v.y + v.z + v.w;
   }
   s = wave_incl_scan(s);
@@ -76,13 +99,14 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_reduce_tiles(const uint32_t *i
 }
 
 // exclusive scan of each tile, plus prefix[blockIdx] when given; in may == out
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const uint32_t *in, uint32_t *out,
+template <class In>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const In in, uint32_t *out,
                                                              size_t n, const uint32_t *prefix) {
   const size_t tile = (size_t)blockIdx.x * SCAN_TILE;
   uint32_t carry = prefix ? prefix[blockIdx.x] : 0u;
   uint4 v[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = load4(in, tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n);
+  for (int r = 0; r < 4; ++r) v[r] = in.load(tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     uint32_t t = v[r].x + v[r].y + v[r].z + v[r].w, tot;
@@ -108,8 +132,8 @@ size_t scan_blocks(size_t n) {
   return total + 1;
 }
 
-void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
-                        hipStream_t st) {
+template <class In>
+static void scan_any(const In in, uint32_t *out, size_t n, ScanScratch ss, hipStream_t st) {
   if (n == 0) return;
   if (n <= (size_t)SCAN_TILE) {
     k_scan_tiles<<<1, SCAN_THREADS, 0, st>>>(in, out, n, nullptr);
@@ -120,8 +144,18 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch
   const size_t stride = (nb + 4) & ~(size_t)3;  // uint4 loads need 16-B alignment
   ScanScratch rest{ss.block_sums + stride, ss.cap - stride};
   k_reduce_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, n, sums);
-  exclusive_scan_u32(sums, sums, nb, rest, st);
+  scan_any(WordsIn{sums}, sums, nb, rest, st);
   k_scan_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, out, n, sums);
+}
+
+void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
+                        hipStream_t st) {
+  scan_any(WordsIn{in}, out, n, ss, st);
+}
+
+void exclusive_scan_roots(const uint32_t *par, uint32_t m, uint32_t *out, ScanScratch ss,
+                          hipStream_t st) {
+  scan_any(RootsIn{par, m}, out, (size_t)m + 1, ss, st);
 }
 
 }  // namespace rk

@@ -303,6 +303,44 @@ def test_std_sort_segments_vs_restatement(gpu_ctx):
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
 
 
+@pytest.mark.parametrize("wide", [False, True])
+def test_std_sort_lds_tiers_vs_restatement(gpu_ctx, wide):
+    """Every LDS tier (65..2048 members): 600 segments of random sizes
+    over heavy ties, few / many distinct keys, sorted, reversed and organ-pipe
+    runs, and median-of-3 killers whose depth-limit heapsort falls inside the
+    tier -- 32-bit keys, and 64-bit ones (`wide`)."""
+    from sort_cases import heap_fallbacks, mcilroy_killer
+    rng = np.random.default_rng(31 + wide)
+    base = np.uint64(1 << 40) if wide else np.uint64(0)
+    segs = []
+    for i in range(600):
+        n = int(rng.integers(65, 2049))
+        kind = i % 6
+        if kind == 0:
+            k = rng.integers(0, 3, n)
+        elif kind == 1:
+            k = rng.integers(0, 40, n)
+        elif kind == 2:
+            k = rng.integers(0, 1 << 30, n)
+        elif kind == 3:
+            k = np.arange(n) if rng.integers(2) else np.arange(n)[::-1]
+        elif kind == 4:
+            h = n // 2
+            k = np.r_[np.arange(h), np.arange(n - h)[::-1]]
+        else:
+            k = np.sort(rng.integers(0, 8, n))[::-1]
+        segs.append(np.ascontiguousarray(k, dtype=np.uint64) + base)
+    killers = [mcilroy_killer(n) + base for n in (70, 130, 300, 511, 900, 2048)]
+    assert all(heap_fallbacks(k) > 0 for k in killers)
+    segs += killers
+    keys = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
+    perm = gpu_ctx.std_sort_segments(keys, off)
+    for a, b, sg in zip(off[:-1], off[1:], segs):
+        want = ro.std_sort(sg) + a
+        assert np.array_equal(perm[a:b], want), (int(a), sg.size)
+
+
 def test_std_sort_large_segments_vs_restatement(gpu_ctx):
     """Segments far above the LDS cap (block-partitioned top levels, then one
     wavefront per final segment): ties, sorted, reversed, organ pipe, all
@@ -581,7 +619,8 @@ print(h.hexdigest(), r.n_groups, ctx.stats()["sweep_repeats"])
                                  "RK_SWEEP_BLIND=1", "RK_NW_MINBITS=8",
                                  "RK_NW_SPLIT=0", "RK_GS_HALF=256", "RK_GS_HALF=2048",
                                  "RK_NW_YSPLIT=0", "RK_NW_MSPLIT=1", "RK_Y_OVERLAP=1",
-                                 "RK_SWEEP_QUEUED=0"])
+                                 "RK_SWEEP_QUEUED=0", "RK_ROOTS_FUSED=0", "RK_ROOTS_STEPS=1",
+                                 "RK_ROOTS_STEPS=1 RK_ROOTS_REST_STEPS=1"])
 def test_schedule_switches_bit_identical(gpu_ctx, env):
     """The measurement switches only move work between streams or change the
     radix of a pass: the result must not change.  300k rows at cfg3 density
@@ -592,9 +631,9 @@ def test_schedule_switches_bit_identical(gpu_ctx, env):
     h = hashlib.sha256()
     for a in (r.out_order, r.gid, r.repval):
         h.update(np.ascontiguousarray(a).tobytes())
-    k, v = env.split("=")
+    extra = dict(kv.split("=") for kv in env.split())
     out = subprocess.run(["python", "-c", _SWITCH_SCRIPT, str(ROOT)], capture_output=True,
-                         text=True, timeout=120, env={**os.environ, k: v})
+                         text=True, timeout=120, env={**os.environ, **extra})
     assert out.returncode == 0, out.stderr[-2000:]
     digest, ng, repeats = out.stdout.split()
     assert digest == h.hexdigest() and int(ng) == r.n_groups
