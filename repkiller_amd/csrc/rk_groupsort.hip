@@ -925,7 +925,7 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
   uint16_t *T = reinterpret_cast<uint16_t *>(K + cap);  // tags: positions in the group
   Frame *stack = reinterpret_cast<Frame *>(T + cap);
   Frame *smallq = stack + lds_stack(cap);
-  Frame *heapq = smallq + nfr;
+  Frame *heapq = reg_max ? smallq + nfr : smallq;  // (no register batches: no queue for them)
   uint16_t *PL = reinterpret_cast<uint16_t *>(heapq + nfr);
   uint16_t *PR = PL + cap;
   uint8_t *B = reinterpret_cast<uint8_t *>(PR + cap);
@@ -1824,10 +1824,13 @@ __global__ void __launch_bounds__(256) k_tier_lists(const uint32_t *goff, uint32
   }
 }
 
-size_t lds_bytes(uint32_t cap, size_t key_bytes) {  // keys, 16-bit tags, PL, PR, B, frames
+// keys, 16-bit tags, PL, PR, B, frames (the register-batch queue only when
+// reg_max > 0: without it the 257..512 tier's slab is 6.3 KB, 25 resident
+// wavefronts per CU instead of 23)
+size_t lds_bytes(uint32_t cap, size_t key_bytes, uint32_t reg_max) {
   const uint32_t nfr = cap / (THRESH + 1) + 2;
-  return (size_t)cap * (key_bytes + 2 + 2 + 2 + 1) + (lds_stack(cap) + 2 * nfr) * sizeof(Frame) +
-         16;
+  return (size_t)cap * (key_bytes + 2 + 2 + 2 + 1) +
+         (lds_stack(cap) + (reg_max ? 2 : 1) * nfr) * sizeof(Frame) + 16;
 }
 
 }  // namespace
@@ -1967,7 +1970,7 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     }();
     const uint32_t waves = (cap <= 256 ? 16384 : cap <= 512 ? 8192 : 2048) * gs_mul;
     const int wp = cap <= 512 ? wpb : 1;
-    const size_t slab = (lds_bytes(cap, narrow_keys ? 4 : 8) + 15) & ~(size_t)15;
+    const size_t slab = (lds_bytes(cap, narrow_keys ? 4 : 8, reg_max) + 15) & ~(size_t)15;
     kt_begin(sj, KID_SORT_LDS);
     if (cap <= half_cap && 2 * slab <= 65536) {
       if (narrow_keys)

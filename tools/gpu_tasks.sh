@@ -14,7 +14,7 @@
 #   cfg5      tools/cfg5_check.py (1B fragments: timing, determinism,
 #             properties) and the cfg5 bench line
 #   ablib     record-pipeline parity, then benches of the working tree's
-#             library interleaved with tools/mb/base (a build of an earlier
+#             library interleaved with ablib_base/ (a build of an earlier
 #             HEAD) through RK_LIB
 #   abenv     the same with environment variants: ARGS = "VAR=a" "VAR=b" ...
 #   abenv5    parity + cfg5q digests, then cfg5 with environment variants
@@ -105,7 +105,7 @@ abcfg5)  # parity, then cfg5 / cfg3 against the HEAD build under tools/mb/base, 
   RK_LIB=tools/mb/base/librepkiller_amd.so bench base_cfg5 --config cfg5 --no-cpu --steps 3 --warmup 1 || exit 3
   for rep in 1 2; do
     RK_LIB=repkiller_amd/librepkiller_amd.so bench new_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 4
-    RK_LIB=tools/mb/base/librepkiller_amd.so bench base_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 5
+    RK_LIB=ablib_base/librepkiller_amd.so bench base_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 5
   done
   RK_LIB=tools/mb/prof/librepkiller_amd.so bench long_cfg5 --config cfg5 --no-cpu --steps 1 --warmup 0 || exit 6
   ;;
@@ -134,7 +134,7 @@ ablib)
   timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || exit 1
   for rep in 1 2 3; do
     RK_LIB=repkiller_amd/librepkiller_amd.so bench new_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 2
-    RK_LIB=tools/mb/base/librepkiller_amd.so bench base_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 3
+    RK_LIB=ablib_base/librepkiller_amd.so bench base_$rep --gpus 1 --steps 20 --warmup 5 --no-cpu || exit 3
   done
   ;;
 abenv)
