@@ -161,13 +161,16 @@ __global__ void k_pend_flag(const uint32_t *counters, uint32_t *pend) {
 // sharded driver's fast path reads it with its next all-gather and repeats the
 // call the careful way if any axis was left open
 int resolve_axis_queued(rk_ctx *ctx, const Axis &ax, SweepScratch sc, uint32_t sweeps,
-                        uint32_t *pend) {
+                        uint32_t *pend, uint32_t *junk) {
   if (!ax.m) return RK_OK;
   RunList rl{sc.runs, sc.wpend, 0, 0, true};
   build_runs(ax, rl, sc.dev_count, ctx->host + 128, ctx->stream);  // (32-bit: no readback)
+  // junk: the sweeps before the last count into words nobody reads, and the
+  // last one into sc.counters, already zero (no clear launched per sweep)
   for (uint32_t s = 0; s < sweeps; ++s)
-    occupancy_sweep(ax, rl, sc.rpend, sc.counters, s == 0, ctx->stream);
-  k_pend_flag<<<1, 64, 0, ctx->stream>>>(sc.counters, pend);
+    occupancy_sweep(ax, rl, sc.rpend, junk && s + 1 < sweeps ? junk : sc.counters, s == 0,
+                    ctx->stream, !junk);
+  if (pend) k_pend_flag<<<1, 64, 0, ctx->stream>>>(sc.counters, pend);
   HIPCHK(ctx, hipGetLastError());
   return RK_OK;
 }
@@ -420,7 +423,11 @@ size_t carve_nw(Carve &c, uint64_t n1, uint32_t nbx, NWork &w) {
 // control words and digit histograms (ctrl, ahist / yhist / ehist), size
 // independent of n: the upfront pass that decides whether every row packs
 // writes only these, so an input that falls back never sizes the workspace
-constexpr size_t NW_SMALL_WORDS = 64 + rk::PEND_WORDS + 3 * 4096;
+// ctrl: 64 words, the X and the Y axis' pending counters (zeroed with the
+// words), a third counter block the earlier queued sweeps count into (never
+// read), then the order / Y / member histograms
+constexpr size_t NW_CTRL_WORDS = 64 + 3 * rk::PEND_WORDS;
+constexpr size_t NW_SMALL_WORDS = NW_CTRL_WORDS + 3 * 4096;
 
 int ensure_nw_small(rk_ctx *ctx, NWork &w) {
   if (!ctx->nw_small) {
@@ -432,7 +439,7 @@ int ensure_nw_small(rk_ctx *ctx, NWork &w) {
     }
   }
   w.ctrl = static_cast<uint32_t *>(ctx->nw_small);
-  w.ahist = w.ctrl + 64 + rk::PEND_WORDS;
+  w.ahist = w.ctrl + NW_CTRL_WORDS;
   w.yhist = w.ahist + 4096;
   w.ehist = w.ahist + 8192;
   return RK_OK;
@@ -526,15 +533,6 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
                                  : rk::NwOrderPlan{};
   const bool ysplit = yp.coarse.passes > 0;
 
-  HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
-  // the control words and the order / Y / member digit histograms (ehist stays
-  // zero until the first pair's k_nw_assign), one launch
-  rk::zero_regions(st, {{w.ctrl, (64 + rk::PEND_WORDS) * sizeof(uint32_t)},
-                        {w.ahist, 3 * 4096 * sizeof(uint32_t)}});
-  mark(ctx, RK_PH_PREP);
-  rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, split ? op.coarse : ad,
-                    ysplit ? yp.coarse : yd, w.ahist, w.yhist, w.ctrl, st, wire);
-  HIPCHK(ctx, hipGetLastError());
   // The control words (errors, kept rows, pack flag, longest length) come back
   // while the split sort's coarse passes run -- they need only n -- when the
   // workspace is already large enough (a repeated call; the first call
@@ -549,17 +547,31 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     NWork tmpw = w;
     early = carve_nw(probe, pl.n, pl.nbx, tmpw) <= ctx->ws_nw_cap;
   }
+  rk::ZeroRegion cr[4] = {};
   if (early) {
     if ((rc = ensure_nw(ctx, pl.n, pl.nbx, w))) return rc;  // (no allocation)
+    // what the coarse passes need cleared (the X-chunk counts for the widest
+    // chunking, 64 buckets a chunk, among it) joins the call's first clear
+    rk::nw_order_coarse_regions(
+        (uint32_t)pl.n, op, w.astatus, w.chist,
+        rk::ZeroRegion{w.xcnt, ((size_t)3 * (pl.nbx / 64 + 2) + 1) * sizeof(uint32_t)}, cr);
+  }
+  HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
+  // the control words and the order / Y / member digit histograms (ehist stays
+  // zero until the first pair's k_nw_assign), one launch
+  rk::zero_regions(st, {{w.ctrl, (64 + 2 * rk::PEND_WORDS) * sizeof(uint32_t)},
+                        {w.ahist, 3 * 4096 * sizeof(uint32_t)}, cr[0], cr[1], cr[2], cr[3]});
+  mark(ctx, RK_PH_PREP);
+  rk::nw_order_hist(*in, pl.vsize, pl.max_x, pl.max_y, pl.nby, split ? op.coarse : ad,
+                    ysplit ? yp.coarse : yd, w.ahist, w.yhist, w.ctrl, st, wire);
+  HIPCHK(ctx, hipGetLastError());
+  if (early) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->host, w.ctrl, 9 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                st));
     HIPCHK(ctx, hipEventRecord(ctx->aux, st));
     mark(ctx, RK_PH_ORDER);
-    // the X-chunk counts cleared for the widest chunking (64 buckets a chunk)
-    rk::nw_order_sort_split_coarse(
-        *in, op, w.ahist, w.astatus, w.Ra, w.Rb, w.chist,
-        rk::ZeroRegion{w.xcnt, ((size_t)3 * (pl.nbx / 64 + 2) + 1) * sizeof(uint32_t)},
-        pl.vsize, st, wire);
+    rk::nw_order_sort_split_coarse(*in, op, w.ahist, w.astatus, w.Ra, w.Rb, w.chist,
+                                   rk::ZeroRegion{}, pl.vsize, st, wire, true);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventSynchronize(ctx->aux));
   } else if ((rc = readback(ctx, w.ctrl, 9))) {
@@ -625,13 +637,21 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
                   st);
   HIPCHK(ctx, hipGetLastError());
   mark(ctx, RK_PH_OCC_CSR);
+  // pending counters: the X axis' at ctrl[64..), the Y axis' after them (both
+  // zero from the call's start), a third block for the queued sweeps before
+  // each axis' last (never read)
   rk::SweepScratch sc{w.runs, w.wpend, reinterpret_cast<uint8_t *>(w.rpend), w.ctrl + 64,
                       w.ctrl + 2};
+  rk::SweepScratch scy = sc;
+  scy.counters = w.ctrl + 64 + rk::PEND_WORDS;
+  uint32_t *const junk = w.ctrl + 64 + 2 * rk::PEND_WORDS;
   // Both axes' sweeps are queued without a host round trip (RK_SWEEP_QUEUED=0:
   // the readback after each axis' third sweep); whether either axis was left
-  // open comes back with the roots' first readback (ctrl[10], ctrl[11]), and
-  // a pair left open repeats its axes the careful way (no input of the
-  // BASELINE configs needs more than three sweeps an axis)
+  // open comes back with the roots' first readback (the two axes' pending
+  // counters; with RK_ROOTS_FUSED=0 a flag per axis in ctrl[10], ctrl[11],
+  // which the first jumping round checks), and a pair left open repeats its
+  // axes the careful way (no input of the BASELINE configs needs more than
+  // three sweeps an axis)
   static const bool queued_on = [] {
     const char *e = getenv("RK_SWEEP_QUEUED");
     return !(e && e[0] == '0');
@@ -650,15 +670,18 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     for (int attempt = 0; attempt < 2; ++attempt) {
     const bool queued = queued_on && attempt == 0;
     if (q > 0 || attempt > 0) HIPCHK(ctx, hipMemsetAsync(w.cx.state, rk::ST_UNKNOWN, m, st));
-    // (the open flags: zero from the call's start for the first pair)
-    if (queued && q > 0) HIPCHK(ctx, hipMemsetAsync(w.ctrl + 10, 0, 2 * sizeof(uint32_t), st));
+    // (the open flags and the counters: zero from the call's start for the first pair)
+    if (queued && q > 0)
+      rk::zero_regions(st, {{w.ctrl + 10, 2 * sizeof(uint32_t)},
+                            {w.ctrl + 64, 2 * rk::PEND_WORDS * sizeof(uint32_t)}});
     if (prof) mark(ctx, RK_PH_SWEEP_X);
     // X decisions: hits' parents (X winner); the X states become a bitmask after
     rk::Axis ax{w.cx.key, w.cx.ent, nullptr, nullptr, w.cx.state, nullptr, w.par,
                 w.cx.pk, w.cx.nbd, w.rlen_at, w.rbeg_at, m, pl.max_x, pq.len_ratio,
                 pq.pos_ratio};
     uint32_t sweeps = blind;
-    if ((rc = queued ? rk::resolve_axis_queued(ctx, ax, sc, blind, w.ctrl + 10)
+    if ((rc = queued ? rk::resolve_axis_queued(ctx, ax, sc, blind,
+                                               fused_roots ? nullptr : w.ctrl + 10, junk)
                      : rk::resolve_axis(ctx, ax, sc, true, &sweeps)))
       return rc;
     ctx->stats.x_sweeps = sweeps;
@@ -683,7 +706,8 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
                 pq.pos_ratio};
     ay.par_dev = true;
     sweeps = blind;
-    if ((rc = queued ? rk::resolve_axis_queued(ctx, ay, sc, blind, w.ctrl + 11)
+    if ((rc = queued ? rk::resolve_axis_queued(ctx, ay, scy, blind,
+                                               fused_roots ? nullptr : w.ctrl + 11, junk)
                      : rk::resolve_axis(ctx, ay, sc, true, &sweeps)))
       return rc;
     ctx->stats.y_sweeps = sweeps;
@@ -696,16 +720,17 @@ int classify_narrow(rk_ctx *ctx, const rk_frags_soa *in, const rk_params *prms, 
     G = 0;
     bool open_axes = false;
     if (fused_roots) {
-      // the new-group ranks from the parents' root flags (G in ctrl[32]) and
-      // the wide-key flag, the queued axes' open flags, G back in one readback;
-      // later pairs' member histograms and listed-chain count cleared first
+      // the new-group ranks from the parents' root flags (G straight into
+      // ctrl[32]); the wide-key flag, G and the queued axes' pending counters
+      // back in one readback; later pairs' member histograms and listed-chain
+      // count cleared first
       rk::zero_regions(st, {{q > 0 ? w.ehist : nullptr, 4096 * sizeof(uint32_t)},
                             {q > 0 ? w.ctrl + 12 : nullptr, sizeof(uint32_t)}});
-      rk::exclusive_scan_roots(w.par, m, w.newrank, ss, st);
-      HIPCHK(ctx, hipMemcpyAsync(w.ctrl + 32, w.newrank + m, sizeof(uint32_t),
-                                 hipMemcpyDeviceToDevice, st));
-      if ((rc = readback(ctx, w.ctrl + 5, 28))) return rc;
-      if (queued && (ctx->host[5] || ctx->host[6])) {
+      rk::exclusive_scan_roots(w.par, m, w.newrank, ss, st, w.ctrl + 32);
+      if ((rc = readback(ctx, w.ctrl + 5, 64 - 5 + 2 * rk::PEND_WORDS))) return rc;
+      uint32_t pending = 0;
+      for (uint32_t k = 0; k < 2 * rk::PEND_WORDS; ++k) pending |= ctx->host[64 - 5 + k];
+      if (queued && pending) {
         open_axes = true;  // an axis was left open: this pair again, the careful way
       } else {
         G = ctx->host[27];

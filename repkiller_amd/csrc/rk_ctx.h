@@ -152,9 +152,11 @@ struct SweepScratch {
 };
 // run sweeps on one axis until no bucket has undecided entries
 int resolve_axis(rk_ctx *ctx, const Axis &ax, SweepScratch sc, bool fast32, uint32_t *sweeps);
-// `sweeps` sweeps of a 32-bit axis with no host round trip; *pend = 1 (device)
-// when entries are still undecided after them
+// `sweeps` sweeps of a 32-bit axis with no host round trip; *pend = 1 (device,
+// when pend is given) when entries are still undecided after them.  junk:
+// PEND_WORDS words the sweeps before the last count into, sc.counters then
+// already zero (no clear per sweep); null: every sweep clears sc.counters
 int resolve_axis_queued(rk_ctx *ctx, const Axis &ax, SweepScratch sc, uint32_t sweeps,
-                        uint32_t *pend);
+                        uint32_t *pend, uint32_t *junk = nullptr);
 
 }  // namespace rk

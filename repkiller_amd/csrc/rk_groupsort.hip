@@ -1646,28 +1646,17 @@ __host__ __device__ constexpr size_t seg_lds_bytes(uint32_t cap, size_t key_byte
   return (size_t)cap * (key_bytes + 4 + 2 + 2 + 1) +
          (SPLIT_STACK + 2 * (cap / (THRESH + 1) + 2)) * sizeof(Frame) + 16;
 }
-__global__ void __launch_bounds__(256) k_clear_if_tier(TierLists tl, int tier, uint8_t *b,
-                                                       uint32_t m) {
-  uint32_t lo, hi;
-  tl.range(tier, lo, hi);
-  if (lo == hi) return;
-  for (uint32_t x = (blockIdx.x * blockDim.x + threadIdx.x) * 16; x < m;
-       x += gridDim.x * blockDim.x * 16) {
-    if (x + 16 <= m) {
-      *reinterpret_cast<uint4 *>(b + x) = make_uint4(0, 0, 0, 0);
-    } else {
-      for (uint32_t y = x; y < m; ++y) b[y] = 0;
-    }
-  }
-}
-
 template <class KT, int WPB>
 __global__ void __launch_bounds__(64 * WPB) k_sort_segments(TierLists tl, int tier, uint32_t m,
                                                             const uint8_t *bnd,
                                                             const uint32_t *head,
                                                             const uint64_t *key,
                                                             const uint32_t *tag, uint32_t *otag,
-                                                            uint32_t reg_max, uint32_t slab) {
+                                                            uint32_t reg_max, uint32_t slab,
+                                                            const uint32_t *heapq_n,
+                                                            uint32_t *heap_count) {
+  // phase A's heap-segment count to the caller's word (read back with its own)
+  if (heap_count && blockIdx.x == 0 && threadIdx.x == 0) *heap_count = *heapq_n;
   {
     uint32_t lo, hi;
     tl.range(tier, lo, hi);
@@ -1767,9 +1756,16 @@ __device__ __forceinline__ int tier_of(uint32_t n) {
 // -- after an exclusive scan of the tier-major block counts -- write every
 // group at its tier's block offset + its rank in the block.
 constexpr uint32_t TCH = 4096;
+// (block 0 also zeroes the scan's end word bc[NTIER * nblk] and the three
+// heap / claim counters of phase A: no clear launched for them)
 __global__ void __launch_bounds__(256) k_tier_count(const uint32_t *goff, uint32_t ngroups,
-                                                    uint32_t nblk, uint32_t *bc, uint32_t *bm) {
+                                                    uint32_t nblk, uint32_t *bc, uint32_t *bm,
+                                                    uint32_t *heapq_n) {
   __shared__ uint32_t cnt[NTIER], mem[NTIER];
+  if (blockIdx.x == 0 && threadIdx.x < 4) {
+    if (threadIdx.x == 3) bc[(size_t)NTIER * nblk] = 0;
+    else heapq_n[threadIdx.x] = 0;
+  }
   if (threadIdx.x < NTIER) cnt[threadIdx.x] = mem[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t g0 = blockIdx.x * TCH, g1 = min(g0 + TCH, ngroups);
@@ -1791,10 +1787,22 @@ __global__ void __launch_bounds__(256) k_tier_count(const uint32_t *goff, uint32
   if (bm && threadIdx.x < NTIER) bm[(size_t)threadIdx.x * nblk + blockIdx.x] = mem[threadIdx.x];
 }
 
+// (and, when the largest tier lists any group, bnd cleared for phase A: its
+// segment starts, which phase B scans for over all m positions)
 __global__ void __launch_bounds__(256) k_tier_lists(const uint32_t *goff, uint32_t ngroups,
                                                     uint32_t nblk, const uint32_t *off,
-                                                    uint32_t *list) {
+                                                    uint32_t *list, uint8_t *bnd, uint32_t m) {
   __shared__ uint32_t wc[4][NTIER];
+  if (off[(size_t)(NTIER - 1) * nblk] != off[(size_t)NTIER * nblk]) {
+    for (uint32_t x = (blockIdx.x * blockDim.x + threadIdx.x) * 16; x < m;
+         x += gridDim.x * blockDim.x * 16) {
+      if (x + 16 <= m) {
+        *reinterpret_cast<uint4 *>(bnd + x) = make_uint4(0, 0, 0, 0);
+      } else {
+        for (uint32_t y = x; y < m; ++y) bnd[y] = 0;
+      }
+    }
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t run[NTIER];
 #pragma unroll
@@ -1901,10 +1909,9 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     g_ktimer->tier_nblk = nblk;
     for (int u = 0; u < KernelTimer::TIERS; ++u) g_ktimer->tier_slot[u] = -1;
   }
-  k_tier_count<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, bc, timing ? bm : nullptr);
-  (void)hipMemsetAsync(bc + (size_t)NL * nblk, 0, 4, st);
+  k_tier_count<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, bc, timing ? bm : nullptr, heapq_n);
   exclusive_scan_u32(bc, boff, (size_t)NL * nblk + 1, ss, st);
-  k_tier_lists<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, boff, list);
+  k_tier_lists<<<nblk, 256, 0, st>>>(goff, ngroups, nblk, boff, list, bnd, m);
   const TierLists tl{list, boff, nblk};
   // algorithmic bytes of every tier (timing only): each member's key read, its
   // tag (its position) written once at its final slot -- 12 B x the tier's members,
@@ -2059,8 +2066,8 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
 #endif
   // phase A marks the final segments' starts in bnd (cleared first); both
   // kernels return at once when no group is that large
-  k_clear_if_tier<<<1024, 256, 0, st>>>(tl, NTIER - 1, bnd, m);
-  (void)hipMemsetAsync(heapq_n, 0, 12, st);  // the heap count and the two claim counters
+  // (bnd cleared by k_tier_lists, the heap count and the two claim counters by
+  // k_tier_count)
   // RK_SPLIT_DYN=0: the static round-robin; RK_SPLIT_BIG: the first pass' size
   static const bool split_dyn = [] {
     const char *e = getenv("RK_SPLIT_DYN");
@@ -2085,8 +2092,9 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     return !(e && e[0] == '0');
   }();
   kt_begin(st, KID_SORT_HEAP);
-  if (heap_rank && heap_count) {  // the caller reads the count back with its own words
-    (void)hipMemcpyAsync(heap_count, heapq_n, 4, hipMemcpyDeviceToDevice, st);
+  if (heap_rank && heap_count) {
+    // the caller reads the count back with its own words (k_sort_segments
+    // copies it there)
   } else if (heap_rank) {
     (void)hipMemcpyAsync(host_words, heapq_n, 4, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
@@ -2102,10 +2110,12 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     if (wpb == 4) {
       if (narrow_keys)
         k_sort_segments<uint32_t, 4><<<2048, 256, 4 * slab, st>>>(
-            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
+            heap_rank ? heap_count : nullptr);
       else
         k_sort_segments<uint64_t, 4><<<2048, 256, 4 * slab, st>>>(
-            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
+            heap_rank ? heap_count : nullptr);
     } else {
       // Each wavefront scans a fixed 1/grid of the positions: a grid many
       // times the resident wavefronts (~19 per CU) lets the hardware balance
@@ -2120,10 +2130,12 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
           seg_env > 0 ? seg_env : (int)std::min(131072u, std::max(8192u, m / 8192));
       if (narrow_keys)
         k_sort_segments<uint32_t, 1><<<seg_waves, 64, slab, st>>>(
-            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
+            heap_rank ? heap_count : nullptr);
       else
         k_sort_segments<uint64_t, 1><<<seg_waves, 64, slab, st>>>(
-            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab);
+            tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
+            heap_rank ? heap_count : nullptr);
     }
   }
   kt_end(st, KID_SORT_SEGS, 0.0);

@@ -48,10 +48,13 @@ struct ScanScratch {
 size_t scan_blocks(size_t n);
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
                         hipStream_t st);
+// the same, in[0] cleared once read (out != in)
+void exclusive_scan_u32_clear0(uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
+                               hipStream_t st);
 // out[k] = number of roots (par[j] == j) among j < k, for k <= m: the
 // new-group ranks straight from the parents (out[m] = the group count)
 void exclusive_scan_roots(const uint32_t *par, uint32_t m, uint32_t *out, ScanScratch ss,
-                          hipStream_t st);
+                          hipStream_t st, uint32_t *total = nullptr);
 
 // Launch-level HIP-event timing of the pipeline's kernels, active only while a
 // context profiles (rk_set_profiling): rk_classify_device points g_ktimer at
@@ -177,7 +180,7 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
 // sum is the number of waves/runs still pending after the sweep.
 constexpr uint32_t PEND_WORDS = 64;
 void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
-                     bool first, hipStream_t st);
+                     bool first, hipStream_t st, bool clear = true);
 
 // ---------------------------------------------------------- rk_groups.hip --
 struct Frags {  // file-order inputs
@@ -338,16 +341,21 @@ struct ZeroRegion {
   size_t bytes;
 };
 void zero_regions(hipStream_t st, std::initializer_list<ZeroRegion> regs);
+// what nw_order_sort_split_coarse clears first (four regions)
+void nw_order_coarse_regions(uint32_t n, const NwOrderPlan &op, uint32_t *status, uint32_t *chist,
+                             ZeroRegion extra, ZeroRegion out[4]);
 NwOrderPlan nw_order_split(uint32_t n, uint64_t nkeys, int bits);  // nkeys: key values in use
 NwOrderPlan nw_order_split_range(uint32_t n, uint64_t klo, uint64_t khi);  // keys in [klo, khi)
 // the same in two halves: the clears (+ `extra`) and the coarse passes, then
 // the scan and the segment kernel (cc->cnts cleared by the first half's
 // `extra`) -- the host can read the order histogram's control words back in
 // between, while the coarse passes run
+// (zeroed: the caller already cleared nw_order_coarse_regions)
 void nw_order_sort_split_coarse(const rk_frags_soa &in, const NwOrderPlan &op,
                                 const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
                                 uint32_t *chist, ZeroRegion extra, uint64_t vsize,
-                                hipStream_t st, const uint3 *wire = nullptr);
+                                hipStream_t st, const uint3 *wire = nullptr,
+                                bool zeroed = false);
 void nw_order_sort_split_fine(uint32_t n, uint32_t m, uint32_t nby, const NwOrderPlan &op,
                               uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
                               uint32_t *coff, ScanScratch ss, const NwChunkCounts *cc,

@@ -830,7 +830,8 @@ __global__ void __launch_bounds__(OF_T) k_seg_big(const SegArgs<R> a, const E e)
 
 template <class R, class E>
 static void launch_seg(const SegArgs<R> &a, const E &e, hipStream_t st) {
-  (void)hipMemsetAsync(a.big, 0, 4, st);
+  // (a.big[0], the list count, is the segment counts' first word: the scan
+  // that placed the segments cleared it, exclusive_scan_u32_clear0)
   k_seg_fine<<<a.nseg < 65536u ? a.nseg : 65536u, OF_T, 0, st>>>(a, e);
   k_seg_big<<<256, OF_T, 0, st>>>(a, e);  // (returns at once when none is listed)
 }
@@ -1738,17 +1739,31 @@ NwOrderPlan nw_order_split_range(uint32_t n, uint64_t klo, uint64_t khi) {
 // the first half: the clears (tile counters, coarse-key counts, the first
 // pass' status words, `extra`) and the coarse passes, the last one counting
 // the coarse keys into chist
-template <class Src1>
-static void nw_order_coarse(const Src1 &first, double in_bytes, uint32_t n, const NwOrderPlan &op,
-                            const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
-                            uint32_t *chist, ZeroRegion extra, hipStream_t st) {
+// what the coarse order passes need cleared before they start: the passes'
+// tile counters, the coarse-key counts, the first pass' status words, `extra`
+void nw_order_coarse_regions(uint32_t n, const NwOrderPlan &op, uint32_t *status, uint32_t *chist,
+                             ZeroRegion extra, ZeroRegion out[4]) {
   const Digits D = to_digits(op.coarse);
   const size_t sw = nw_status_words(n);
   const PassStatus ps = pass_status(status, n, D);
-  zero_regions(st, {{status + sw - 64, 64 * 4},
-                    {chist, ((size_t)op.nseg + 1) * 4},
-                    ps.region(0, n, D),
-                    extra});
+  out[0] = ZeroRegion{status + sw - 64, 64 * 4};
+  out[1] = ZeroRegion{chist, ((size_t)op.nseg + 1) * 4};
+  out[2] = ps.region(0, n, D);
+  out[3] = extra;
+}
+template <class Src1>
+static void nw_order_coarse(const Src1 &first, double in_bytes, uint32_t n, const NwOrderPlan &op,
+                            const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
+                            uint32_t *chist, ZeroRegion extra, hipStream_t st,
+                            bool zeroed = false) {
+  const Digits D = to_digits(op.coarse);
+  const size_t sw = nw_status_words(n);
+  const PassStatus ps = pass_status(status, n, D);
+  if (!zeroed) {
+    ZeroRegion r[4];
+    nw_order_coarse_regions(n, op, status, chist, extra, r);
+    zero_regions(st, {r[0], r[1], r[2], r[3]});
+  }
   for (int p = 0; p < D.passes; ++p) {
     uint4 *out = ((D.passes - 1 - p) % 2 == 0) ? Rb : Ra;  // the last coarse pass lands in Rb
     const uint4 *src = ((D.passes - p) % 2 == 0) ? Rb : Ra;
@@ -1772,7 +1787,7 @@ static void nw_order_fine(uint32_t n, uint32_t m, uint32_t nby, uint32_t base,
                           const NwOrderPlan &op, uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp,
                           uint32_t *chist, uint32_t *coff, ScanScratch ss,
                           const NwChunkCounts *cc, hipStream_t st) {
-  exclusive_scan_u32(chist, coff, (size_t)op.nseg + 1, ss, st);
+  exclusive_scan_u32_clear0(chist, coff, (size_t)op.nseg + 1, ss, st);
   OrderEmit oe{DstProc{Ra, reinterpret_cast<uint3 *>(yrec), nby, base}, m, nullptr, 0, 0, 0};
   if (cc) {
     oe.cnts = cc->cnts;
@@ -1792,13 +1807,13 @@ static ZeroRegion counts_region(const NwChunkCounts *cc) {
 void nw_order_sort_split_coarse(const rk_frags_soa &in, const NwOrderPlan &op,
                                 const uint32_t *ghist, uint32_t *status, uint4 *Ra, uint4 *Rb,
                                 uint32_t *chist, ZeroRegion extra, uint64_t vsize,
-                                hipStream_t st, const uint3 *wire) {
+                                hipStream_t st, const uint3 *wire, bool zeroed) {
   if (wire)
     nw_order_coarse(SrcFile<RowWire>{RowWire{wire}, vsize}, 12.0, (uint32_t)in.n, op, ghist,
-                    status, Ra, Rb, chist, extra, st);
+                    status, Ra, Rb, chist, extra, st, zeroed);
   else
     nw_order_coarse(SrcFile<RowSoA>{RowSoA{in.x_start, in.y_start, in.length, in.strand}, vsize},
-                    25.0, (uint32_t)in.n, op, ghist, status, Ra, Rb, chist, extra, st);
+                    25.0, (uint32_t)in.n, op, ghist, status, Ra, Rb, chist, extra, st, zeroed);
 }
 void nw_order_sort_split_fine(uint32_t n, uint32_t m, uint32_t nby, const NwOrderPlan &op,
                               uint4 *Ra, uint4 *Rb, uint4 *yrec, uint4 *tmp, uint32_t *chist,
@@ -1975,7 +1990,7 @@ void nw_y_sort_split_after_x(uint4 *yrec, uint4 *tmp, uint4 *tmp2, uint32_t m,
     }
     src = out;
   }
-  exclusive_scan_u32(chist, coff, (size_t)yp.nseg + 1, ss, st);
+  exclusive_scan_u32_clear0(chist, coff, (size_t)yp.nseg + 1, ss, st);
   const DstCsr dc{cy.key, cy.ent, cy.pk, cy.nbd, nby, max_y, nullptr, cy.state, true};
   kt_begin(st, KID_NW_YFINE);
   // (the counts are free after the scan: the list of segments above OF_CAP)
@@ -2064,7 +2079,7 @@ void nw_member_sort_split(const uint4 *erec, const uint32_t *gidp, uint4 *t0, ui
     else launch_pass(SrcRec12{src}, DstRec12{out}, m, D.shift[p], D.db[p], gh, stp, ctr, st, bytes, nxt);
     src = out;
   }
-  exclusive_scan_u32(chist, coff, (size_t)mp.nseg + 1, ss, st);
+  exclusive_scan_u32_clear0(chist, coff, (size_t)mp.nseg + 1, ss, st);
   kt_begin(st, KID_NW_MFINE);
   launch_seg(SegArgs<uint3>{b, a, c, coff, mp.nseg, mp.F, chist},
              MemberEmit{sgid, tag, mrow, key, goff, G, m}, st);

@@ -1948,8 +1948,8 @@ void build_runs(const Axis &ax, RunList &rl, uint32_t *dev_count, uint32_t *host
 }
 
 void occupancy_sweep(const Axis &ax, const RunList &rl, uint8_t *rpend, uint32_t *counters,
-                     bool first, hipStream_t st) {
-  (void)hipMemsetAsync(counters, 0, PEND_SLOTS * sizeof(uint32_t), st);
+                     bool first, hipStream_t st, bool clear) {
+  if (clear) (void)hipMemsetAsync(counters, 0, PEND_SLOTS * sizeof(uint32_t), st);
   // algorithmic bytes: the first sweep reads every entry's key, centre, length,
   // id and state and writes state (+ winner): 30 B (26 B with the packed 8-B
   // record and neighbour code of the 32-bit kernel); later sweeps only need

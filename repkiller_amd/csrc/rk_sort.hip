@@ -101,7 +101,8 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_reduce_tiles(const In in, size
 // exclusive scan of each tile, plus prefix[blockIdx] when given; in may == out
 template <class In>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const In in, uint32_t *out,
-                                                             size_t n, const uint32_t *prefix) {
+                                                             size_t n, const uint32_t *prefix,
+                                                             uint32_t *total, uint32_t *clear0) {
   const size_t tile = (size_t)blockIdx.x * SCAN_TILE;
   uint32_t carry = prefix ? prefix[blockIdx.x] : 0u;
   uint4 v[4];
@@ -116,9 +117,17 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const In in, uint32
     o.y = o.x + v[r].x;
     o.z = o.y + v[r].y;
     o.w = o.z + v[r].z;
-    store4(out, tile + (size_t)r * SCAN_ROW + threadIdx.x * 4, n, o);
+    const size_t base = tile + (size_t)r * SCAN_ROW + threadIdx.x * 4;
+    store4(out, base, n, o);
+    if (total && base <= n - 1 && n - 1 < base + 4) {  // out[n - 1] also into *total
+      const uint32_t j = (uint32_t)(n - 1 - base);
+      *total = j == 0 ? o.x : j == 1 ? o.y : j == 2 ? o.z : o.w;
+    }
     carry += tot;
   }
+  // the input's first word cleared once read (block 0 alone reads it): a
+  // count array reused as a list, its count word zero without a launch
+  if (clear0 && blockIdx.x == 0 && threadIdx.x == 0) *clear0 = 0u;
 }
 
 }  // namespace
@@ -133,10 +142,11 @@ size_t scan_blocks(size_t n) {
 }
 
 template <class In>
-static void scan_any(const In in, uint32_t *out, size_t n, ScanScratch ss, hipStream_t st) {
+static void scan_any(const In in, uint32_t *out, size_t n, ScanScratch ss, hipStream_t st,
+                     uint32_t *total = nullptr, uint32_t *clear0 = nullptr) {
   if (n == 0) return;
   if (n <= (size_t)SCAN_TILE) {
-    k_scan_tiles<<<1, SCAN_THREADS, 0, st>>>(in, out, n, nullptr);
+    k_scan_tiles<<<1, SCAN_THREADS, 0, st>>>(in, out, n, nullptr, total, clear0);
     return;
   }
   size_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
@@ -145,17 +155,21 @@ static void scan_any(const In in, uint32_t *out, size_t n, ScanScratch ss, hipSt
   ScanScratch rest{ss.block_sums + stride, ss.cap - stride};
   k_reduce_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, n, sums);
   scan_any(WordsIn{sums}, sums, nb, rest, st);
-  k_scan_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, out, n, sums);
+  k_scan_tiles<<<(unsigned)nb, SCAN_THREADS, 0, st>>>(in, out, n, sums, total, clear0);
 }
 
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
                         hipStream_t st) {
   scan_any(WordsIn{in}, out, n, ss, st);
 }
+void exclusive_scan_u32_clear0(uint32_t *in, uint32_t *out, size_t n, ScanScratch ss,
+                               hipStream_t st) {
+  scan_any(WordsIn{in}, out, n, ss, st, nullptr, in);
+}
 
 void exclusive_scan_roots(const uint32_t *par, uint32_t m, uint32_t *out, ScanScratch ss,
-                          hipStream_t st) {
-  scan_any(RootsIn{par, m}, out, (size_t)m + 1, ss, st);
+                          hipStream_t st, uint32_t *total) {
+  scan_any(RootsIn{par, m}, out, (size_t)m + 1, ss, st, total);
 }
 
 }  // namespace rk
