@@ -1,19 +1,19 @@
 #!/usr/bin/env python3
-"""Regenerate DESIGN.md's kernel table from profiles/r5_bench.json (HIP-event
+"""Regenerate DESIGN.md's kernel table from profiles/r6_bench.json (HIP-event
 timing inside bench.py's timed steps, cfg3), profiles/traffic.json
-(PMC HBM bytes, cfg3) and profiles/r5_bench_cfg5.json (the same timing at cfg5,
+(PMC HBM bytes, cfg3) and profiles/r6_bench_cfg5.json (the same timing at cfg5,
 one GPU) when present."""
 import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BEGIN, END = "<!-- kernel-table:begin -->", "<!-- kernel-table:end -->"
-BENCH, CFG5 = "r5_bench.json", "r5_bench_cfg5.json"
+BENCH, CFG5 = "r6_bench.json", "r6_bench_cfg5.json"
 # bench kernel name -> the PMC summary's name (tools/pmc_summary.py uses the bench's names)
-PMC_NAME = {}
+PMC_NAME = {"k_nw_assign": "k_nw_assign_jump"}
 JOBS = [
     ("k_nw_order_hist", "one read of the file-order SoA: digit histograms of the processing key and the Y key, kept / forward counts, longest length, bounds and pack checks", "25"),
-    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (2 coarse processing-order passes: the key's top 15 bits as 8 + 7 at cfg3, the second also counting each coarse key), 12-B records 7168 per tile (2 coarse Y passes after X, 8 + 7 bits, the first carrying the X-hit bits, the second counting each coarse key; 3 member passes, 9 + 9 + 8): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; first Y pass: 24.1)"),
+    ("k_onesweep", "one LSD pass: 16-B records 6144 per tile (2 coarse processing-order passes: the key's top 15 bits as 8 + 7 at cfg3, the second also counting each coarse key), 12-B records 7168 per tile (2 coarse Y passes after X, 8 + 7 bits, the first carrying the X-hit bits, the second counting each coarse key; 3 member passes by gid, 8 + 8 + 8 at cfg3's 24-bit gids): ballot ranks, LDS placement in rounds, decoupled look-back, digit-segment write-out", "32 / 24 (pass 1: 41; first Y pass: 24.1)"),
     ("k_seg_fine (order)", "one block per coarse-key segment (<= 4096 records in LDS): the 14 fine bits by ballot-ranked LSD rounds, then the final records, the Y records and the X-chunk counts (an LDS window of chunk counters)", "44"),
     ("k_seg_fine (Y)", "one block per coarse Y-key segment (<= 4096 records in LDS): the 11 fine bits by ballot-ranked LSD rounds, then the Y axis' CSR arrays (key, entry, packed record, neighbour code, state from the carried X-hit bit) written as whole lines", "30"),
     ("k_seg_big", "segments above 4096 records: the same passes through global memory, one block each", "-"),
@@ -24,8 +24,8 @@ JOBS = [
     ("k_sweep_long32", "runs of more than 64 entries: a pre-scan for the run's open entries (none: the run is done), then 64 entries at a time against LDS lists (redundant ACTIVE records dropped when a list would overflow)", "-"),
     ("k_nw_x_bits", "X hits as a bitmask by processing index (ballots over the X states at each fragment's X position), read in order by the first Y pass", "5"),
     ("k_nw_fill_y", "Y states from the bitmask for later ratio pairs (X hits sit in the Y lists)", "5"),
-    ("k_jump", "chase parent chains to the root", "16"),
-    ("k_nw_assign", "gid from the root's rank into each member record; member-sort histograms", "12"),
+    ("k_jump", "(RK_ROOTS_FUSED=0 only) chase parent chains to the root, round by round", "16"),
+    ("k_nw_assign", "`k_nw_assign_jump`: after the scan of the parents' root flags, each member chases its chain (up to 32 links; longer ones listed for `k_nw_assign_rest`), writes the root back as its parent and takes gid = the root's rank, with the member-sort histograms", "20"),
     ("k_group_offsets", "group bounds", "4"),
     ("k_sort_small", "groups of 2..16 members (insertion sort == stable rank): 16 lanes per group from the tier list, width-16 shuffles; singletons are not touched (second stream)", "12 per member"),
     ("k_sort_groups_reg", "17..64 members in registers (17..32: two groups per wavefront, second stream; 33..64: main stream, after its LDS tiers)", "12 per member"),
