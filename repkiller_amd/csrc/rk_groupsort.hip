@@ -710,6 +710,76 @@ __device__ uint32_t wave_partition(const V &v, uint32_t f, uint32_t l, GLanes<W>
   return cut;
 }
 
+template <class KT>
+__device__ __forceinline__ KT lane_key(KT k, uint32_t src) {  // (src wave-uniform)
+  if (sizeof(KT) == 8) {
+    const uint64_t v = (uint64_t)k;
+    return (KT)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)src) |
+                (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)src)
+                    << 32);
+  }
+  return (KT)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, (int)src);
+}
+
+// wave_partition on a segment of 17..64 elements, one per lane, in registers:
+// the keys and tags are read once, the median moves by lane reads, the
+// stoppers are two ballots, K is the rank of the first L-stopper with at most
+// its rank of R-stoppers above it (wave_partition's stop test), the partners
+// come from two lists compacted by lane permutes (reg_sort_core's form), and
+// every element is written once at its slot -- two memory round trips where
+// the list form (stopper lists written, read by the search, read again by the
+// swaps, keys and tags read and written per swap, the cut read) takes ten.
+template <bool GLOBAL, class V>
+__device__ uint32_t wave_partition_small(const V &v, uint32_t f, uint32_t l, uint32_t lane) {
+  using KT = typename V::key_t;
+  const uint32_t len = l - f;
+  const bool in = lane < len;
+  const uint32_t x = f + (in ? lane : 0u);
+  KT k = v.K[x];  // (lanes past the segment hold a copy of its first element, unused)
+  uint32_t t = v.T[x];
+  // __move_median_to_first(f, f + 1, f + len / 2, l - 1)
+  const uint32_t la = 1, lb = len / 2, lc = len - 1;
+  const KT ka = lane_key(k, la), kb = lane_key(k, lb), kc = lane_key(k, lc);
+  uint32_t mi;
+  if (ka < kb) mi = kb < kc ? lb : (ka < kc ? lc : la);
+  else mi = ka < kc ? la : (kb < kc ? lc : lb);
+  mi = (uint32_t)__builtin_amdgcn_readfirstlane((int)mi);
+  const KT k0 = lane_key(k, 0u), p = lane_key(k, mi);
+  const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)t, 0),
+                 tm = (uint32_t)__builtin_amdgcn_readlane((int)t, (int)mi);
+  if (lane == 0) k = p, t = tm;
+  else if (lane == mi) k = k0, t = t0;
+  // stoppers of __unguarded_partition(f + 1, l, f)
+  const bool lf = in && lane > 0 && !(k < p);
+  const bool rf = in && !(p < k);
+  const uint64_t BL = __ballot(lf), BR = __ballot(rf);
+  const uint32_t nL = (uint32_t)__popcll(BL), nR = (uint32_t)__popcll(BR);
+  const uint32_t pL = (uint32_t)below_count(BL), pR = (uint32_t)below_count(BR);
+  const uint32_t ra = nR - pR - (rf ? 1u : 0u);  // R-stoppers above: its rank from the right
+  const uint64_t SB = __ballot(lf && ra <= pL);
+  const uint32_t lim = nL < nR ? nL : nR;
+  const uint32_t K =
+      SB ? (uint32_t)__popcll(BL & ((1ull << __builtin_ctzll(SB)) - 1ull)) : lim;
+  // compacted stopper lists (lane j: the j-th L- / R-stopper), one permute each;
+  // the k-th L-stopper and the k-th R-stopper from the right trade places, k < K
+  const uint32_t LL = push((int)(lf ? pL : nL + (lane - pL)), lane);
+  const uint32_t RL = push((int)(rf ? pR : nR + (lane - pR)), lane);
+  const bool swl = lf && pL < K, swr = rf && ra < K;
+  const uint32_t g = pull((int)(swl ? nR - 1u - pL : swr ? ra : lane), LL | RL << 8);
+  const uint32_t src = swl ? g >> 8 : swr ? g & 0xffu : lane;
+  k = pull((int)src, k);
+  t = pull((int)src, t);
+  if (in) {
+    v.K[x] = k;
+    v.T[x] = (typename V::tag_t)t;
+  }
+  // the cut min(L_K, R_{K-1}) (L_0 when K == 0): the lowest lane that is either
+  const uint64_t cm = __ballot((lf && pL == K) || (K > 0 && rf && ra == K - 1u));
+  const uint32_t cut = f + (uint32_t)__builtin_ctzll(cm);
+  sync_mem<GLOBAL>();
+  return cut;
+}
+
 struct Frame {
   uint32_t f, l;
   int d;
@@ -730,7 +800,7 @@ __device__ unsigned long long g_gs_prof[8];
 template <bool GLOBAL, class V, int W = 64>
 __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stack,
                               Frame *smallq, Frame *heapq, GLanes<W> L, int d0,
-                              uint32_t reg_max, uint32_t tbase = 0) {
+                              uint32_t reg_max, uint32_t tbase = 0, bool small_part = true) {
   static_assert(W == 64 || W == 32, "a wavefront or a half");
   const uint32_t lane = L.lane;
   if (W != 64) reg_max = 0;  // register batches assume the whole wavefront
@@ -765,7 +835,10 @@ __device__ void wave_std_sort(const V &v, uint32_t n, uint32_t *out, Frame *stac
 #ifdef RK_GS_PROF
       const uint64_t _p0 = __builtin_amdgcn_s_memtime();
 #endif
-      const uint32_t cut = wave_partition<GLOBAL, V, W>(v, f, l, L);
+      // (segments of <= 64 in registers, RK_GS_SMALLPART=0: the list form)
+      const uint32_t cut = W == 64 && small_part && l - f <= 64
+                               ? wave_partition_small<GLOBAL, V>(v, f, l, lane)
+                               : wave_partition<GLOBAL, V, W>(v, f, l, L);
 #ifdef RK_GS_PROF
       part_cyc += __builtin_amdgcn_s_memtime() - _p0;
       ++nparts;
@@ -909,7 +982,7 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
                                                               const uint64_t *key,
                                                               const uint32_t *tag, uint32_t *otag,
                                                               uint32_t cap, uint32_t reg_max,
-                                                              uint32_t slab) {
+                                                              uint32_t slab, bool small_part) {
   extern __shared__ __align__(16) uint8_t smem_all[];
   constexpr uint32_t GPW = 64 / W;  // groups per wavefront
   // the wavefront index in a scalar register: every LDS base stays uniform
@@ -943,7 +1016,7 @@ __attribute__((amdgpu_waves_per_eu(W == 32 && sizeof(KT) == 4 ? 8 : 1))) k_sort_
     wave_sync();
     wave_std_sort<false, ViewT<KT, uint16_t, uint16_t>, W>(v, n, otag + b, stack, smallq, heapq,
                                                            L, 2 * (31 - __clz((int)n)), reg_max,
-                                                           b);
+                                                           b, small_part);
     wave_sync();
   }
 }
@@ -1654,7 +1727,7 @@ __global__ void __launch_bounds__(64 * WPB) k_sort_segments(TierLists tl, int ti
                                                             const uint32_t *tag, uint32_t *otag,
                                                             uint32_t reg_max, uint32_t slab,
                                                             const uint32_t *heapq_n,
-                                                            uint32_t *heap_count) {
+                                                            uint32_t *heap_count, bool small_part) {
   // phase A's heap-segment count to the caller's word (read back with its own)
   if (heap_count && blockIdx.x == 0 && threadIdx.x == 0) *heap_count = *heapq_n;
   {
@@ -1690,7 +1763,7 @@ __global__ void __launch_bounds__(64 * WPB) k_sort_segments(TierLists tl, int ti
       }
       wave_sync();
       wave_std_sort<false>(v, n, otag + x, stack, smallq, heapq, GLanes<64>{lane, 0u},
-                           (int)(h >> 16), reg_max);
+                           (int)(h >> 16), reg_max, 0u, small_part);
       wave_sync();
     }
   }
@@ -1933,6 +2006,12 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     const char *e = getenv("RK_GS_REGMAX");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
+  // partitions of segments of <= 64 elements in registers
+  // (wave_partition_small; RK_GS_SMALLPART=0: the stopper-list form)
+  static const bool small_part = [] {
+    const char *e = getenv("RK_GS_SMALLPART");
+    return !(e && e[0] == '0');
+  }();
   // the first `lds_side` LDS tiers also run on `side` (RK_GS_SIDE, measurements)
   static const int lds_side = [] {
     const char *e = getenv("RK_GS_SIDE");
@@ -1982,24 +2061,24 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     if (cap <= half_cap && 2 * slab <= 65536) {
       if (narrow_keys)
         k_sort_groups_lds<uint32_t, 1, 32><<<waves / 2, 64, 2 * slab, sj>>>(
-            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, 0u, (uint32_t)slab);
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, 0u, (uint32_t)slab, small_part);
       else
         k_sort_groups_lds<uint64_t, 1, 32><<<waves / 2, 64, 2 * slab, sj>>>(
-            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, 0u, (uint32_t)slab);
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, 0u, (uint32_t)slab, small_part);
     } else if (wp == 4) {
       if (narrow_keys)
         k_sort_groups_lds<uint32_t, 4><<<waves / 4, 256, 4 * slab, sj>>>(
-            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, reg_max, (uint32_t)slab);
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, reg_max, (uint32_t)slab, small_part);
       else
         k_sort_groups_lds<uint64_t, 4><<<waves / 4, 256, 4 * slab, sj>>>(
-            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, reg_max, (uint32_t)slab);
+            tl, TIER_LDS0 + j, goff, key, tag, otag, cap, reg_max, (uint32_t)slab, small_part);
     } else {
       if (narrow_keys)
         k_sort_groups_lds<uint32_t, 1><<<waves, 64, slab, sj>>>(tl, TIER_LDS0 + j, goff, key, tag,
-                                                                otag, cap, reg_max, (uint32_t)slab);
+                                                                otag, cap, reg_max, (uint32_t)slab, small_part);
       else
         k_sort_groups_lds<uint64_t, 1><<<waves, 64, slab, sj>>>(tl, TIER_LDS0 + j, goff, key, tag,
-                                                                otag, cap, reg_max, (uint32_t)slab);
+                                                                otag, cap, reg_max, (uint32_t)slab, small_part);
     }
     kt_end(sj, KID_SORT_LDS, 0.0);
     tier_slot(TIER_LDS0 + j);
@@ -2111,11 +2190,11 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
       if (narrow_keys)
         k_sort_segments<uint32_t, 4><<<2048, 256, 4 * slab, st>>>(
             tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
-            heap_rank ? heap_count : nullptr);
+            heap_rank ? heap_count : nullptr, small_part);
       else
         k_sort_segments<uint64_t, 4><<<2048, 256, 4 * slab, st>>>(
             tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
-            heap_rank ? heap_count : nullptr);
+            heap_rank ? heap_count : nullptr, small_part);
     } else {
       // Each wavefront scans a fixed 1/grid of the positions: a grid many
       // times the resident wavefronts (~19 per CU) lets the hardware balance
@@ -2131,11 +2210,11 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
       if (narrow_keys)
         k_sort_segments<uint32_t, 1><<<seg_waves, 64, slab, st>>>(
             tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
-            heap_rank ? heap_count : nullptr);
+            heap_rank ? heap_count : nullptr, small_part);
       else
         k_sort_segments<uint64_t, 1><<<seg_waves, 64, slab, st>>>(
             tl, NTIER - 1, m, bnd, pl, key, tag, otag, reg_max, (uint32_t)slab, heapq_n,
-            heap_rank ? heap_count : nullptr);
+            heap_rank ? heap_count : nullptr, small_part);
     }
   }
   kt_end(st, KID_SORT_SEGS, 0.0);

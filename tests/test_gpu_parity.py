@@ -620,7 +620,7 @@ print(h.hexdigest(), r.n_groups, ctx.stats()["sweep_repeats"])
                                  "RK_NW_SPLIT=0", "RK_GS_HALF=256", "RK_GS_HALF=2048",
                                  "RK_NW_YSPLIT=0", "RK_NW_MSPLIT=1", "RK_Y_OVERLAP=1",
                                  "RK_SWEEP_QUEUED=0", "RK_ROOTS_FUSED=0", "RK_ROOTS_STEPS=1",
-                                 "RK_ROOTS_STEPS=1 RK_ROOTS_REST_STEPS=1"])
+                                 "RK_ROOTS_STEPS=1 RK_ROOTS_REST_STEPS=1", "RK_GS_SMALLPART=0"])
 def test_schedule_switches_bit_identical(gpu_ctx, env):
     """The measurement switches only move work between streams or change the
     radix of a pass: the result must not change.  300k rows at cfg3 density
