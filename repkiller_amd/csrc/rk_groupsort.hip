@@ -1333,7 +1333,7 @@ __global__ void __launch_bounds__(256) k_heap_prep(uint64_t *K, uint32_t *T, uin
       while (vals[r] != k) ++r;
       R[x + 1] = (uint8_t)r;  // (shifted: a node pair is one aligned 16-bit word)
     }
-  if (tid == 0) *mode = md;
+  if (tid == 0) mode[0] = md, mode[1] = D;  // (D exact up to RANK_MAX)
 }
 
 // the spine-ring path (one key) and the general pops (more than RANK_MAX keys)
@@ -1562,6 +1562,147 @@ __global__ void __launch_bounds__(64) k_heap_rank_pops(uint8_t *R, uint32_t n, u
 #undef HP_T
 }
 
+// k_heap_pipe_pops: the pops of k_heap_rank_pops, pipelined.  A rank pop is a
+// top-down sift of the displaced value vk = R[last] from the root: the hole
+// takes its larger child's key (the right one unless right < left; a lone
+// left child below the last full level) while that key is >= vk, and vk lands
+// where it stops.  __adjust_heap's descent to a leaf followed by __push_heap
+// ends the same way: the path's keys descend and __push_heap lifts vk past
+// exactly the path keys below it, so the nodes below the landing slot end
+// unchanged.  A pop therefore writes one node per level, top down, and pop
+// k + 1 can descend behind pop k: with pop k's hole two levels below pop
+// k + 1's, every node pop k + 1 reads (its hole's two children) already holds
+// pop k's write.  One wavefront carries up to ~depth / 2 pops, a lane each; a
+// tick moves every pop one level (one LDS load of its children, its write as
+// an and / or pair), and the next pop starts when
+//  * the previous one started at least two ticks ago (two levels down), and
+//  * no pop in flight can still write the new pop's `last` node (no hole is
+//    that node or an ancestor of it), so vk is final when it is read.
+// The log is the path's direction bits down to the landing level j (D = j in
+// logq: the nodes below j are unchanged).  Ranks packed P bits per node (P =
+// 1, 2, 4 for 2, <= 4, <= 16 distinct keys), node x at bit (x + 1) P, so the
+// children pair 2x + 1, 2x + 2 is 2P aligned bits of one byte.  The whole heap
+// lives in LDS (the host checks the size); a pop costs two ticks instead of
+// its whole descent and push.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+template <int P>
+__device__ __forceinline__ void pipe_pops(lds_u8 *LB, lds_u32 *LW, uint32_t n, uint32_t HD,
+                                          uint32_t *logb, uint16_t *logq, uint32_t lane) {
+  constexpr uint32_t M = (1u << P) - 1u;
+  const auto pair = [&](uint32_t bit) -> uint32_t {  // the 2P bits at `bit`
+    if constexpr (P == 8) return *(const lds_u16 *)(LB + (bit >> 3));
+    else return (uint32_t)LB[bit >> 3] >> (bit & 7);
+  };
+  const uint32_t npop = n - 1, PMAX = (HD + 1) * P;  // (a pair's bit stays below PMAX)
+  // a lane's pop: B = hole + 1 -- a leading 1, then the path's direction bits
+  // from the root (its level is B's bit length - 1; the hole's children 2B - 1,
+  // 2B are the pair at bit 2B P; the next hole + 1 is 2B + direction) --, the
+  // displaced key vk, the heap length len (0: an idle lane, B = HD + 1: its
+  // writes go to the spare word) and the pop's index k
+  uint32_t B = HD + 1, vk = 0, len = 0, k = 0;
+  uint32_t knext = 0, ndone = 0;
+  int since = 2;  // ticks since the last start (very negative: every pop started)
+  uint64_t busy = 0;
+  while (ndone < npop) {
+    // the tick's loads first: every pop's children, the root's, the next `last`
+    uint32_t w = pair(min(2 * B * P, PMAX));
+    const uint32_t wroot = pair(2 * P);
+    const uint32_t y = n - 1 - knext, bv = (y + 1) * P;  // the next pop's `last`
+    const uint32_t v = ((uint32_t)LB[bv >> 3] >> (bv & 7)) & M;
+    if (since >= 2) {
+      // a pop in flight whose hole is y or an ancestor of it (B a binary prefix
+      // of y + 1; never an idle lane's HD + 1) may still write y: y is a leaf of
+      // its heap (else it might move a child's key up), so only its own
+      // displaced key, which matters only when it is not v
+      const uint32_t cy = __clz((int)(y + 1)), cb = __clz((int)B);
+      const bool unsafe = (cb >= cy) & (((y + 1) >> (cb - cy)) == B) &
+                          ((vk != v) | (2 * y + 1 < len));  // (no short cut: no branch)
+      if (!__builtin_amdgcn_ballot_w64(unsafe)) {  // (fewer pops in flight than lanes)
+        const uint32_t slot = (uint32_t)__builtin_ctzll(~busy);
+        busy |= 1ull << slot;
+        if (lane == slot) B = 1, vk = v, len = y, k = knext, w = wroot;
+        since = ++knext < npop ? 0 : -(1 << 30);
+      }
+    }
+    ++since;
+    const uint32_t kl = w & M, kr = (w >> P) & M;
+    const bool rt = (2 * B < len) & (kr >= kl);  // right child present and not smaller
+    const uint32_t kc = rt ? kr : kl;
+    const bool cont = (2 * B <= len) & (kc >= vk);  // (left child present)
+    const uint32_t nv = cont ? kc : vk;
+    if constexpr (P == 8) {
+      LB[B] = (uint8_t)nv;
+    } else {
+      const uint32_t bh = B * P, sh = bh & 31;
+      __hip_atomic_fetch_and(LW + (bh >> 5), ~(M << sh), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_or(LW + (bh >> 5), nv << sh, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const bool fin = (len != 0) & !cont;
+    const uint64_t fm = __builtin_amdgcn_ballot_w64(fin);
+    if (fm) {
+      if (fin) logb[k] = B;  // (k_heap_log_split: the bits and the level)
+      ndone += (uint32_t)__popcll(fm);
+      busy &= ~fm;
+    }
+    B = cont ? 2 * B + (rt ? 1u : 0u) : fin ? HD + 1 : B;
+    len = fin ? 0u : len;
+  }
+  (void)logq;
+}
+// k_heap_pipe_pops logs B (a leading 1, then the j direction bits): logb, logq
+// as k_heap_rank_pops writes them (D = j)
+__global__ void k_heap_log_split(uint32_t *logb, uint16_t *logq, uint32_t npop,
+                                 const uint32_t *mode) {
+  if (mode[0] != HM_RANK) return;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < npop; t += gridDim.x * blockDim.x) {
+    const uint32_t b = logb[t], j = 31 - __clz((int)b);
+    logb[t] = b ^ (1u << j);
+    logq[t] = (uint16_t)(j | j << 8);
+  }
+}
+
+// The LDS bytes of k_heap_pipe_pops: the heap's ranks P bits per node, node x
+// at bit (x + 1) P (positions 0 .. n, whole words), and a spare word
+__host__ __device__ constexpr uint32_t pipe_lds_bytes(uint32_t n, uint32_t P) {
+  return ((n + 1) * P + 31) / 32 * 4 + 16;
+}
+// P: 8 when the heap fits in LDS a byte per node, else 1, 2, 4 for 2, <= 4,
+// <= 16 distinct keys (the host checks that the packed heap fits)
+__global__ void __launch_bounds__(256) k_heap_pipe_pops(const uint8_t *R, uint32_t n, uint32_t P,
+                                                       uint32_t *logb, uint16_t *logq,
+                                                       const uint32_t *mode) {
+  extern __shared__ uint32_t lw[];
+  if (mode[0] != HM_RANK) return;
+  lds_u32 *LW = (lds_u32 *)lw;
+  const uint32_t per = 32 / P, nw = (pipe_lds_bytes(n, P) - 16) / 4;
+  for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < per; i += 4) {  // R holds n + 16 bytes
+      const uint32_t p0 = q * per + i;
+      const uint32_t r4 = p0 <= n ? *(const uint32_t *)(R + p0) : 0u;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t p = p0 + b;
+        if (p >= 1 && p <= n) v |= ((r4 >> (8 * b)) & 0xffu) << ((i + b) * P);
+      }
+    }
+    LW[q] = v;
+  }
+  if (threadIdx.x < 4) LW[nw + threadIdx.x] = 0;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  lds_u8 *LB = (lds_u8 *)lw;
+  const uint32_t HD = nw * per - 1;  // (HD + 1) P: the first spare word, nw
+  switch (P) {
+    case 1: pipe_pops<1>(LB, LW, n, HD, logb, logq, threadIdx.x); break;
+    case 2: pipe_pops<2>(LB, LW, n, HD, logb, logq, threadIdx.x); break;
+    case 4: pipe_pops<4>(LB, LW, n, HD, logb, logq, threadIdx.x); break;
+    default: pipe_pops<8>(LB, LW, n, HD, logb, logq, threadIdx.x); break;
+  }
+}
+
 __global__ void k_heap_pair_counts(const uint16_t *logq, uint32_t npop, uint32_t *cnt) {
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < npop + 1; t += gridDim.x * blockDim.x)
     cnt[t] = t < npop ? (uint32_t)(logq[t] >> 8) + 1u : 0u;
@@ -1652,9 +1793,16 @@ static int heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint3
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
     (void)hipFuncSetAttribute((const void *)k_heap_rank_pops<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+    (void)hipFuncSetAttribute((const void *)k_heap_pipe_pops,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
     return true;
   }();
   (void)attr;
+  // RK_HEAP_PIPE=0: the rank pops one after another (k_heap_rank_pops) only
+  static const bool heap_pipe = [] {
+    const char *s = getenv("RK_HEAP_PIPE");
+    return !(s && s[0] == '0');
+  }();
   uint8_t *R = nullptr;
   uint32_t *logb = nullptr, *mode = nullptr, *cnt = nullptr, *off = nullptr, *ssb = nullptr;
   uint16_t *logq = nullptr;
@@ -1676,14 +1824,21 @@ static int heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint3
     k_heap_prep<<<1, 256, 0, st>>>(K, T, n, R, mode);
     k_heap_equal<<<1, 64, 0, st>>>(T, n, out, mode);
     k_heap_general<<<1, 256, 0, st>>>(K, T, n, out, mode);
-    if (n + 16 <= LDS_MAX)  // the whole heap in LDS
-      k_heap_rank_pops<false><<<1, 64, n + 16, st>>>(R, n, n, logb, logq, mode);
-    else  // the top RT (odd) nodes in LDS
-      k_heap_rank_pops<true><<<1, 64, RT + 16, st>>>(R, n, RT, logb, logq, mode);
-    e = hipMemcpyAsync(host_words, mode, 4, hipMemcpyDeviceToHost, st);
+    e = hipMemcpyAsync(host_words, mode, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if ((rc = heap_status(e))) break;
     if (host_words[0] != HM_RANK) continue;
+    const uint32_t D = host_words[1];  // bits per node: a byte when the heap fits
+    const uint32_t bpn = pipe_lds_bytes(n, 8) <= LDS_MAX ? 8u : D <= 2 ? 1u : D <= 4 ? 2u : 4u;
+    if (heap_pipe && pipe_lds_bytes(n, bpn) <= LDS_MAX)  // the (packed) heap in LDS
+    {
+      k_heap_pipe_pops<<<1, 256, pipe_lds_bytes(n, bpn), st>>>(R, n, bpn, logb, logq, mode);
+      k_heap_log_split<<<grid_for(n, 256), 256, 0, st>>>(logb, logq, n - 1, mode);
+    }
+    else if (n + 16 <= LDS_MAX)  // the whole heap in LDS
+      k_heap_rank_pops<false><<<1, 64, n + 16, st>>>(R, n, n, logb, logq, mode);
+    else  // the top RT (odd) nodes in LDS
+      k_heap_rank_pops<true><<<1, 64, RT + 16, st>>>(R, n, RT, logb, logq, mode);
     const uint32_t npop = n - 1;
     k_heap_pair_counts<<<grid_for(npop + 1, 256), 256, 0, st>>>(logq, npop, cnt);
     exclusive_scan_u32(cnt, off, (size_t)npop + 1, ScanScratch{ssb, sscap}, st);
