@@ -407,6 +407,23 @@ def test_std_sort_rank_heap_vs_restatement(gpu_ctx):
         assert np.array_equal(perm[a:b], want), (int(a), s.size)
 
 
+def test_std_sort_pipe_heap_packings_vs_restatement(gpu_ctx):
+    """The pipelined rank pops (k_heap_pipe_pops) with the heap's ranks packed
+    into LDS: 1 bit a node (2 keys, 1.2M nodes), 4 bits (16 keys, 250K), and a
+    3-key heap too large for 2 bits a node (700K: the one-pop-at-a-time rank
+    kernel, its deeper ranks in global memory) -- against the restated
+    std::sort."""
+    from sort_cases import killer_with_keys
+    segs = [killer_with_keys(1_200_000, 2, 27), killer_with_keys(250_000, 16, 28, base=1 << 40),
+            killer_with_keys(700_000, 3, 29)]
+    keys = np.concatenate(segs)
+    off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
+    perm = gpu_ctx.std_sort_segments(keys, off)
+    for a, b, s in zip(off[:-1], off[1:], segs):
+        want = ro.std_sort(s) + a
+        assert np.array_equal(perm[a:b], want), (int(a), s.size)
+
+
 def test_killer_group_heap_segment_vs_oracle(gpu_ctx):
     """A group whose in-group sort keys (|yStart - diag|, commonFunctions.cpp:
     148-159) are a median-of-3 killer with 3 keys on its never-compared items:
@@ -494,10 +511,11 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("env", ["RK_HEAP_RANK=0", "RK_HEAP_ALLOC_CAP=4096"])
+@pytest.mark.parametrize("env", ["RK_HEAP_RANK=0", "RK_HEAP_PIPE=0", "RK_HEAP_ALLOC_CAP=4096"])
 def test_heap_segment_switches(gpu_ctx, tmp_path, env):
     """RK_HEAP_RANK=0 (every depth-limit heap segment through the one-block
-    pops of k_heap_segments) gives the restated std::sort's permutation; with
+    pops of k_heap_segments) and RK_HEAP_PIPE=0 (the rank pops one at a time,
+    not pipelined) give the restated std::sort's permutation; with
     the heap path's buffers refused (RK_HEAP_ALLOC_CAP, as an exhausted HBM
     would) the call returns RK_E_NOMEM instead of writing through a null
     buffer."""
