@@ -1651,6 +1651,135 @@ __device__ __forceinline__ void pipe_pops(lds_u8 *LB, lds_u32 *LW, uint32_t n, u
   }
   (void)logq;
 }
+// The same pops for a heap too large for LDS: levels 0 .. L - 1 packed in LDS,
+// the bottom level L (leaves only) in the global byte array R (node x at
+// R[x + 1] = R[B]).  A leaf is read only as a child of a level L - 1 hole and
+// written only as a pop's last write, so:
+//  * when a pop's hole reaches level L - 2 (end of a tick) it loads its four
+//    leaf descendants (one u32 at R[4B]); two ticks later, at level L - 1, two
+//    of those bytes are its children pair -- the load had a whole tick (~390
+//    cycles) against an L2 hit's ~200;
+//  * the loads go to a slot by tick parity (the tick is written twice, loads
+//    unconditional: a lane with nothing to load reads R[0]), so the wait
+//    counts are fixed and a slot is consumed before the same-parity tick
+//    reloads it;
+//  * leaf writes (at most one a tick: one pop per level) go to R and to a
+//    2-tick ring of (R index, key) in scalars, which patches the loaded bytes
+//    of the one pop at level L - 1 (its load was issued before those writes);
+//  * the next pop's `last` node, a leaf until the heap is down to L levels,
+//    comes the same way (loaded by parity, patched by the ring).
+// Every store is unconditional too (a lane with nothing to store writes R[0]
+// or logb[npop]).
+template <int P>
+__device__ __forceinline__ void pipe_pops_tail(lds_u8 *LB, lds_u32 *LW, uint8_t *R, uint32_t n,
+                                               uint32_t L, uint32_t HD, uint32_t *logb,
+                                               uint32_t lane) {
+  constexpr uint32_t M = (1u << P) - 1u;
+  const auto pair = [&](uint32_t bit) -> uint32_t {
+    if constexpr (P == 8) return *(const lds_u16 *)(LB + (bit >> 3));
+    else return (uint32_t)LB[bit >> 3] >> (bit & 7);
+  };
+  const uint32_t npop = n - 1, PMAX = (HD + 1) * P;
+  const uint32_t TOPB = 1u << L, HALF = TOPB >> 1, QTR = TOPB >> 2;  // B < TOPB: in LDS
+  const uint32_t RMAX = n + 12;  // (R holds n + 16 bytes: a u32 at <= n + 12)
+  uint32_t B = HD + 1, vk = 0, len = 0, k = 0;
+  uint32_t knext = 0, ndone = 0;
+  int since = 2;
+  uint64_t busy = 0;
+  // the leaf writes of the last two ticks (R index, key), newest first: a load
+  // issued at the end of tick t and used at t + 2 misses t + 1's write (and
+  // t's is kept too); older stores come before the load in the wave's order
+  uint32_t rb0 = 0, rv0 = 0, rb1 = 0, rv1 = 0;
+  const auto patch = [&](uint32_t at, uint32_t val) {  // (uniform operands: scalar)
+    val = rb1 == at ? rv1 : val;
+    return rb0 == at ? rv0 : val;
+  };
+  uint32_t pf0 = 0, pf1 = 0, vg0 = *(const uint32_t *)(R + (n & ~3u)), vg1 = vg0;  // (node n - 1)
+  // a zero the compiler cannot see through: the `last` word's load stays a
+  // vector load (a uniform one is moved to a scalar at once, waiting on it)
+  uint32_t vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  const auto tick = [&](uint32_t &pf, uint32_t &vg) {
+    uint32_t w = pair(min(2 * B * P, PMAX));
+    const uint32_t wroot = pair(2 * P);
+    const uint32_t y = n - 1 - knext;
+    if (since >= 2) {
+      uint32_t v;
+      if (y + 1 >= TOPB) {  // (its aligned word loaded)
+        const uint32_t sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)vg);
+        v = patch(y + 1, (sv >> ((y + 1) & 3u) * 8) & 0xffu);
+      } else {
+        const uint32_t bv = (y + 1) * P;
+        v = ((uint32_t)LB[bv >> 3] >> (bv & 7)) & M;
+      }
+      const uint32_t cy = __clz((int)(y + 1)), cb = __clz((int)B);
+      // (len != 0: an idle lane's B = HD + 1 = TOPB is the first leaf's B)
+      const bool unsafe = (len != 0) & (cb >= cy) & (((y + 1) >> (cb - cy)) == B) &
+                          ((vk != v) | (2 * y + 1 < len));
+      if (!__builtin_amdgcn_ballot_w64(unsafe)) {
+        const uint32_t slot = (uint32_t)__builtin_ctzll(~busy);
+        busy |= 1ull << slot;
+        if (lane == slot) B = 1, vk = v, len = y, k = knext, w = wroot;
+        since = ++knext < npop ? 0 : -(1 << 30);
+      }
+    }
+    ++since;
+    uint32_t kl = w & M, kr = (w >> P) & M;
+    // a hole at level L - 1 takes its children from pf -- one lane at most
+    // (pops are two levels apart): its bytes and their patch in scalars
+    const uint64_t lpm = __builtin_amdgcn_ballot_w64((B >= HALF) & (B < TOPB));
+    if (lpm) {
+      const int li = (int)__builtin_ctzll(lpm);
+      const uint32_t sb = (uint32_t)__builtin_amdgcn_readlane((int)B, li);
+      const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)pf, li);
+      const uint32_t sh = (sb & 1u) * 16u;  // B = 2 B' + direction since the load at B'
+      const uint32_t gl = patch(2 * sb, (sp >> sh) & 0xffu);
+      const uint32_t gr = patch(2 * sb + 1, (sp >> (sh + 8)) & 0xffu);
+      kl = lane == (uint32_t)li ? gl : kl;
+      kr = lane == (uint32_t)li ? gr : kr;
+    }
+    const bool rt = (2 * B < len) & (kr >= kl);
+    const uint32_t kc = rt ? kr : kl;
+    const bool cont = (2 * B <= len) & (kc >= vk);
+    const uint32_t nv = cont ? kc : vk;
+    const bool gw = (B >= TOPB) & (len != 0);  // a leaf hole: the pop's last write
+    const uint32_t Bw = gw ? HD + 1 : B;       // (its LDS write to the spare word)
+    if constexpr (P == 8) {
+      LB[Bw] = (uint8_t)nv;
+    } else {
+      const uint32_t bh = Bw * P, sh = bh & 31;
+      __hip_atomic_fetch_and(LW + (bh >> 5), ~(M << sh), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_or(LW + (bh >> 5), nv << sh, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    R[gw ? B : 0u] = (uint8_t)nv;
+    const uint64_t gm = __builtin_amdgcn_ballot_w64(gw);
+    const int gi = gm ? (int)__builtin_ctzll(gm) : 0;
+    const uint32_t gb = (uint32_t)__builtin_amdgcn_readlane((int)B, gi);
+    const uint32_t gv = (uint32_t)__builtin_amdgcn_readlane((int)nv, gi);
+    rb1 = rb0, rv1 = rv0;
+    rb0 = gm ? gb : 0u, rv0 = gv;
+    const bool fin = (len != 0) & !cont;
+    const uint64_t fm = __builtin_amdgcn_ballot_w64(fin);
+    logb[fin ? k : npop] = B;  // (k_heap_log_split: the bits and the level)
+    ndone += (uint32_t)__popcll(fm);
+    busy &= ~fm;
+    B = cont ? 2 * B + (rt ? 1u : 0u) : fin ? HD + 1 : B;
+    len = fin ? 0u : len;
+    // the loads for two ticks on: leaf descendants, the next `last` leaf
+    const uint32_t pa = ((B >= QTR) & (B < HALF) & (4 * B <= RMAX)) ? 4 * B : 0u;
+    pf = *(const uint32_t *)(R + pa);
+    const uint32_t y2 = n - 1 - knext;  // (a u32 load: no byte value carried over the loop)
+    vg = *(const uint32_t *)(R + (((y2 + 1 >= TOPB ? y2 + 1 : 0u) & ~3u) + vzero));
+  };
+  while (ndone < npop) {
+    tick(pf0, vg0);
+    if (ndone >= npop) break;
+    tick(pf1, vg1);
+  }
+}
+
 // k_heap_pipe_pops logs B (a leading 1, then the j direction bits): logb, logq
 // as k_heap_rank_pops writes them (D = j)
 __global__ void k_heap_log_split(uint32_t *logb, uint16_t *logq, uint32_t npop,
@@ -1670,13 +1799,15 @@ __host__ __device__ constexpr uint32_t pipe_lds_bytes(uint32_t n, uint32_t P) {
 }
 // P: 8 when the heap fits in LDS a byte per node, else 1, 2, 4 for 2, <= 4,
 // <= 16 distinct keys (the host checks that the packed heap fits)
-__global__ void __launch_bounds__(256) k_heap_pipe_pops(const uint8_t *R, uint32_t n, uint32_t P,
-                                                       uint32_t *logb, uint16_t *logq,
-                                                       const uint32_t *mode) {
+// tailL > 0: only the levels above tailL in LDS (pipe_pops_tail)
+__global__ void __launch_bounds__(256) k_heap_pipe_pops(uint8_t *R, uint32_t n, uint32_t P,
+                                                       uint32_t tailL, uint32_t *logb,
+                                                       uint16_t *logq, const uint32_t *mode) {
   extern __shared__ uint32_t lw[];
   if (mode[0] != HM_RANK) return;
   lds_u32 *LW = (lds_u32 *)lw;
-  const uint32_t per = 32 / P, nw = (pipe_lds_bytes(n, P) - 16) / 4;
+  const uint32_t ntop = tailL ? (1u << tailL) - 1u : n;  // nodes in LDS
+  const uint32_t per = 32 / P, nw = (pipe_lds_bytes(ntop, P) - 16) / 4;
   for (uint32_t q = threadIdx.x; q < nw; q += blockDim.x) {
     uint32_t v = 0;
     for (uint32_t i = 0; i < per; i += 4) {  // R holds n + 16 bytes
@@ -1685,7 +1816,7 @@ __global__ void __launch_bounds__(256) k_heap_pipe_pops(const uint8_t *R, uint32
 #pragma unroll
       for (uint32_t b = 0; b < 4; ++b) {
         const uint32_t p = p0 + b;
-        if (p >= 1 && p <= n) v |= ((r4 >> (8 * b)) & 0xffu) << ((i + b) * P);
+        if (p >= 1 && p <= ntop) v |= ((r4 >> (8 * b)) & 0xffu) << ((i + b) * P);
       }
     }
     LW[q] = v;
@@ -1695,6 +1826,14 @@ __global__ void __launch_bounds__(256) k_heap_pipe_pops(const uint8_t *R, uint32
   if (threadIdx.x >= 64) return;
   lds_u8 *LB = (lds_u8 *)lw;
   const uint32_t HD = nw * per - 1;  // (HD + 1) P: the first spare word, nw
+  if (tailL) {
+    switch (P) {
+      case 1: pipe_pops_tail<1>(LB, LW, R, n, tailL, HD, logb, threadIdx.x); break;
+      case 2: pipe_pops_tail<2>(LB, LW, R, n, tailL, HD, logb, threadIdx.x); break;
+      default: pipe_pops_tail<4>(LB, LW, R, n, tailL, HD, logb, threadIdx.x); break;
+    }
+    return;
+  }
   switch (P) {
     case 1: pipe_pops<1>(LB, LW, n, HD, logb, logq, threadIdx.x); break;
     case 2: pipe_pops<2>(LB, LW, n, HD, logb, logq, threadIdx.x); break;
@@ -1803,6 +1942,11 @@ static int heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint3
     const char *s = getenv("RK_HEAP_PIPE");
     return !(s && s[0] == '0');
   }();
+  // RK_HEAP_TAIL=0: no pipelined pops with the bottom level in global memory
+  static const bool heap_tail = [] {
+    const char *s = getenv("RK_HEAP_TAIL");
+    return !(s && s[0] == '0');
+  }();
   uint8_t *R = nullptr;
   uint32_t *logb = nullptr, *mode = nullptr, *cnt = nullptr, *off = nullptr, *ssb = nullptr;
   uint16_t *logq = nullptr;
@@ -1830,9 +1974,13 @@ static int heap_segments(const HeapSeg *dq, uint32_t nheap, uint64_t *key, uint3
     if (host_words[0] != HM_RANK) continue;
     const uint32_t D = host_words[1];  // bits per node: a byte when the heap fits
     const uint32_t bpn = pipe_lds_bytes(n, 8) <= LDS_MAX ? 8u : D <= 2 ? 1u : D <= 4 ? 2u : 4u;
-    if (heap_pipe && pipe_lds_bytes(n, bpn) <= LDS_MAX)  // the (packed) heap in LDS
-    {
-      k_heap_pipe_pops<<<1, 256, pipe_lds_bytes(n, bpn), st>>>(R, n, bpn, logb, logq, mode);
+    // a heap too large: its levels above the bottom one in LDS, when they fit
+    const uint32_t L = 31 - __builtin_clz(n), tailL =
+        pipe_lds_bytes(n, bpn) > LDS_MAX && heap_tail && L >= 6 &&
+                pipe_lds_bytes((1u << L) - 1u, bpn) <= LDS_MAX ? L : 0u;
+    if (heap_pipe && (tailL || pipe_lds_bytes(n, bpn) <= LDS_MAX)) {  // the (packed) heap in LDS
+      const uint32_t lds = pipe_lds_bytes(tailL ? (1u << L) - 1u : n, bpn);
+      k_heap_pipe_pops<<<1, 256, lds, st>>>(R, n, bpn, tailL, logb, logq, mode);
       k_heap_log_split<<<grid_for(n, 256), 256, 0, st>>>(logb, logq, n - 1, mode);
     }
     else if (n + 16 <= LDS_MAX)  // the whole heap in LDS

@@ -409,13 +409,14 @@ def test_std_sort_rank_heap_vs_restatement(gpu_ctx):
 
 def test_std_sort_pipe_heap_packings_vs_restatement(gpu_ctx):
     """The pipelined rank pops (k_heap_pipe_pops) with the heap's ranks packed
-    into LDS: 1 bit a node (2 keys, 1.2M nodes), 4 bits (16 keys, 250K), and a
-    3-key heap too large for 2 bits a node (700K: the one-pop-at-a-time rank
-    kernel, its deeper ranks in global memory) -- against the restated
+    into LDS: 1 bit a node (2 keys, 1.2M nodes), 4 bits (16 keys, 250K), and
+    heaps too large for LDS at their packing, whose bottom level stays in
+    global memory (pipe_pops_tail): 3 keys at 700K (2 bits, 19 levels in LDS)
+    and 16 keys at 400K (4 bits, 18 levels) -- against the restated
     std::sort."""
     from sort_cases import killer_with_keys
     segs = [killer_with_keys(1_200_000, 2, 27), killer_with_keys(250_000, 16, 28, base=1 << 40),
-            killer_with_keys(700_000, 3, 29)]
+            killer_with_keys(700_000, 3, 29), killer_with_keys(400_000, 16, 30)]
     keys = np.concatenate(segs)
     off = np.concatenate([[0], np.cumsum([s.size for s in segs])]).astype(np.uint32)
     perm = gpu_ctx.std_sort_segments(keys, off)
@@ -511,11 +512,13 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("env", ["RK_HEAP_RANK=0", "RK_HEAP_PIPE=0", "RK_HEAP_ALLOC_CAP=4096"])
+@pytest.mark.parametrize("env", ["RK_HEAP_RANK=0", "RK_HEAP_PIPE=0", "RK_HEAP_TAIL=0",
+                                 "RK_HEAP_ALLOC_CAP=4096"])
 def test_heap_segment_switches(gpu_ctx, tmp_path, env):
     """RK_HEAP_RANK=0 (every depth-limit heap segment through the one-block
-    pops of k_heap_segments) and RK_HEAP_PIPE=0 (the rank pops one at a time,
-    not pipelined) give the restated std::sort's permutation; with
+    pops of k_heap_segments), RK_HEAP_PIPE=0 (the rank pops one at a time,
+    not pipelined) and RK_HEAP_TAIL=0 give the restated std::sort's
+    permutation; with
     the heap path's buffers refused (RK_HEAP_ALLOC_CAP, as an exhausted HBM
     would) the call returns RK_E_NOMEM instead of writing through a null
     buffer."""
