@@ -2459,8 +2459,20 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     const char *e = getenv("RK_SPLIT_BIG");
     return e ? (uint32_t)atoi(e) : 65536u;
   }();
+  // RK_SPLIT_GRID: blocks of phase A; RK_SPLIT_LDSPAD: LDS bytes reserved per
+  // block beyond its own (fewer resident blocks: a larger L2 share each)
+  static const uint32_t split_grid = [] {
+    const char *e = getenv("RK_SPLIT_GRID");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? (uint32_t)v : 2048u;
+  }();
+  static const uint32_t split_pad = [] {
+    const char *e = getenv("RK_SPLIT_LDSPAD");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v <= 65536 ? (uint32_t)v : 0u;
+  }();
   kt_begin(st, KID_SORT_GLOBAL);
-  k_sort_groups_split<<<2048, 256, 0, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
+  k_sort_groups_split<<<split_grid, 256, split_pad, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
                                             heapq_n, heapq, split_dyn ? heapq_n + 1 : nullptr,
                                             split_big);
   kt_end(st, KID_SORT_GLOBAL, 0.0);

@@ -158,6 +158,15 @@ abenv5)  # parity + the cfg5q digests, then cfg5 with environment variants (ARGS
     done
   done
   ;;
+env5)  # cfg5 with environment variants (ARGS: "VAR=a" "VAR=b" ...) interleaved, two rounds, no parity
+  for rep in 1 2; do
+    i=0
+    for E in "$@"; do
+      i=$((i+1))
+      env $E timeout -k 10 600 python3 bench.py --config cfg5 --no-cpu --steps 2 --warmup 1 > $O/v${i}_$rep.json 2> $O/v${i}_$rep.err || exit 3
+    done
+  done
+  ;;
 trace)
   RK_NW_TRACE=$O/trace.bin timeout -k 10 300 python3 bench.py --no-cpu --steps 2 --warmup 1 > $O/bt.json 2> $O/bt.err || exit 1
   python3 tools/nw_trace.py $O/trace.bin > $O/trace.txt 2>&1
