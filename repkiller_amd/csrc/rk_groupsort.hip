@@ -1159,6 +1159,203 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
   return cut;
 }
 
+// The same partition as a block-wide Hoare scan (round 6, the default; RK_SPLIT_Q=0
+// keeps block_partition): the block runs libstdc++'s two cursors a chunk at a time.  The
+// left cursor scans QP_C positions upward from f + 1, the right one QP_C
+// downward from l - 1; each scan appends its stoppers -- position, key and
+// tag, in scan order -- to a ring queue in LDS, and a round pairs the two
+// queues' heads (the k-th left stopper with the k-th right one) up to the
+// first pair that crosses, swapping the others straight from the queues.  A
+// position is read once by each cursor at most and written only if swapped,
+// with no stopper lists in memory: ~12 B read and ~6 B written per member and
+// level against ~45 B for block_partition's list pass, probe search and
+// gathered swaps (cfg5's phase A was bound by that traffic).
+// Exactness: the pairs before the crossing Kc are the original lists' (a
+// position swapped as R_j lies above every left stopper still to come before
+// the crossing, and symmetrically), so the queues' first Kc entries do not
+// depend on when a scan reads a swapped position; at index Kc the queues hold
+// min(L[Kc], R[Kc-1]) or L[Kc] (left) and max(R[Kc], L[Kc-1]) or R[Kc]
+// (right), which cross either way, and the cut is min(QL[Kc], R[Kc-1]) --
+// where libstdc++'s left cursor stops on the modified array.
+#ifndef RK_QP_PER
+#define RK_QP_PER 2
+#endif
+constexpr int QP_PER = RK_QP_PER;        // positions per thread in a scanned chunk
+constexpr uint32_t QP_C = 256 * QP_PER;  // a chunk (and the pairs per round at most)
+constexpr uint32_t QP_CAP = 2 * QP_C;    // ring capacity (a power of 2)
+constexpr uint32_t QP_M = QP_CAP - 1;
+struct QPart {
+  uint64_t lk[QP_CAP], rk[QP_CAP];
+  uint32_t lp[QP_CAP], rp[QP_CAP], lt[QP_CAP], rt[QP_CAP];
+  uint32_t cnt[2][QP_PER * 4];
+  uint32_t cross;
+};
+
+__device__ uint32_t block_partition_q(uint64_t *K, uint32_t *T, uint32_t f, uint32_t l,
+                                      QPart &q) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  // __move_median_to_first(f, f + 1, mid, l - 1) folded into the first
+  // chunks' round trip: every thread reads the three candidates and slot f,
+  // picks the median m, and keeps its own copies of the two swapped slots
+  // right (slot m holds K[f]'s key and tag, slot f the pivot's) whenever it
+  // loads them; thread 0 writes the swap after the first barrier (before any
+  // pair's swap can write slot m)
+#ifndef RK_QP_FOLD
+#define RK_QP_FOLD 1
+#endif
+  if (!RK_QP_FOLD) {  // (A/B: the median's swap first, by thread 0)
+    if (tid == 0) median_to_first(GView{K, T, nullptr, nullptr, nullptr}, f, l);
+    __syncthreads();
+  }
+  const uint32_t ca = f + 1, cb = f + (l - f) / 2, cc = l - 1;
+  const uint64_t ka = K[ca], kb = K[cb], kc = K[cc], k0 = K[f];
+  const uint32_t ta = T[ca], tb = T[cb], tc = T[cc], t0 = T[f];
+  // cursors: the left scan's next position, the right scan's next end (its
+  // next position is rpos - 1); queue heads / tails count entries ever
+  // pushed / popped (slots modulo QP_CAP)
+  uint32_t lpos = f + 1, rpos = l;
+  uint32_t qlh = 0, qlt = 0, qrh = 0, qrt = 0;
+  uint32_t lastR = 0;  // R[Kc - 1]: the last right stopper swapped
+  uint64_t ak[QP_PER], bk[QP_PER];
+  uint32_t at[QP_PER], bt[QP_PER];
+  uint32_t m = 0xFFFFFFFFu, fp = 0xFFFFFFFFu;  // (no patch for the first loads)
+  uint64_t p = 0;
+  uint32_t tm = 0;
+  auto load_left = [&]() {
+#pragma unroll
+    for (int u = 0; u < QP_PER; ++u) {
+      const uint32_t x = lpos + 256 * u + tid;
+      const bool ok = x < l;
+      const uint64_t k = ok ? K[x] : 0;
+      const uint32_t t = ok ? T[x] : 0;
+      ak[u] = x == m ? k0 : k;
+      at[u] = x == m ? t0 : t;
+    }
+  };
+  auto load_right = [&]() {
+#pragma unroll
+    for (int u = 0; u < QP_PER; ++u) {
+      const uint32_t o = 256 * u + tid;
+      const bool ok = o < rpos - f;
+      const uint32_t x = ok ? rpos - 1 - o : f;
+      const uint64_t k = ok ? K[x] : 0;
+      const uint32_t t = ok ? T[x] : 0;
+      bk[u] = x == m ? k0 : (x == fp ? p : k);
+      bt[u] = x == m ? t0 : (x == fp ? tm : t);
+    }
+  };
+  load_left();
+  load_right();
+  if (!RK_QP_FOLD) m = f;
+  else if (ka < kb) m = kb < kc ? cb : (ka < kc ? cc : ca);
+  else m = ka < kc ? ca : (kb < kc ? cc : cb);
+  p = m == f ? k0 : m == ca ? ka : (m == cb ? kb : kc);
+  tm = m == f ? t0 : m == ca ? ta : (m == cb ? tb : tc);
+  fp = f;
+#pragma unroll
+  for (int u = 0; u < QP_PER; ++u) {
+    const uint32_t x = lpos + 256 * u + tid;
+    if (x == m) ak[u] = k0, at[u] = t0;
+    const uint32_t o = 256 * u + tid;
+    const uint32_t y = o < rpos - f ? rpos - 1 - o : 0xFFFFFFFFu;
+    if (y == m) bk[u] = k0, bt[u] = t0;
+    if (y == f) bk[u] = p, bt[u] = tm;
+  }
+  bool first = true;
+  uint32_t cut = 0;
+  for (;;) {
+    const bool addl = qlt - qlh < QP_C && lpos < l;
+    const bool addr = qrt - qrh < QP_C && rpos > f;
+    if (!addl && qlt == qlh) {  // left cursor past l: it stops on R[Kc - 1]
+      cut = qrh ? lastR : (qrt > qrh ? q.rp[qrh & QP_M] : f + 1);
+      break;
+    }
+    if (!addr && qrt == qrh) {  // (unreachable: f itself is a right stopper)
+      cut = q.lp[qlh & QP_M];
+      break;
+    }
+    uint64_t bl[QP_PER], br[QP_PER];
+#pragma unroll
+    for (int u = 0; u < QP_PER; ++u) {
+      const bool okl = addl && lpos + 256 * u + tid < l;
+      const bool okr = addr && 256 * u + tid < rpos - f;
+      bl[u] = __ballot(okl && !(ak[u] < p));
+      br[u] = __ballot(okr && !(p < bk[u]));
+      if (lane == 0) q.cnt[0][u * 4 + wv] = __popcll(bl[u]), q.cnt[1][u * 4 + wv] = __popcll(br[u]);
+    }
+    if (tid == 0) q.cross = 0xFFFFFFFFu;
+    __syncthreads();
+    if (first && tid == 0) {  // the median's swap (every candidate read by now)
+      K[f] = p;
+      T[f] = tm;
+      K[m] = k0;
+      T[m] = t0;
+    }
+    first = false;
+    uint32_t nl = 0, nr = 0, ol[QP_PER], orr[QP_PER];
+#pragma unroll
+    for (int j = 0; j < QP_PER * 4; ++j) {
+      const uint32_t cl = q.cnt[0][j], cr = q.cnt[1][j];
+      if (j % 4 == (int)wv) ol[j / 4] = nl, orr[j / 4] = nr;
+      nl += cl;
+      nr += cr;
+    }
+#pragma unroll
+    for (int u = 0; u < QP_PER; ++u) {
+      if ((bl[u] >> lane) & 1ull) {
+        const uint32_t s = (qlt + ol[u] + __popcll(bl[u] & lt)) & QP_M;
+        q.lk[s] = ak[u];
+        q.lt[s] = at[u];
+        q.lp[s] = lpos + 256 * u + tid;
+      }
+      if ((br[u] >> lane) & 1ull) {
+        const uint32_t s = (qrt + orr[u] + __popcll(br[u] & lt)) & QP_M;
+        q.rk[s] = bk[u];
+        q.rt[s] = bt[u];
+        q.rp[s] = rpos - 1 - (256 * u + tid);
+      }
+    }
+    if (addl) {
+      qlt += nl;
+      lpos += QP_C;
+      if (lpos < l) load_left();
+    }
+    if (addr) {
+      qrt += nr;
+      rpos = rpos - f > QP_C ? rpos - QP_C : f;
+      if (rpos > f) load_right();
+    }
+    __syncthreads();
+    uint32_t m = qlt - qlh < qrt - qrh ? qlt - qlh : qrt - qrh;
+    if (m > QP_C) m = QP_C;
+    for (uint32_t i = tid; i < m; i += 256)
+      if (q.lp[(qlh + i) & QP_M] >= q.rp[(qrh + i) & QP_M]) atomicMin(&q.cross, i);
+    __syncthreads();
+    const uint32_t cr = q.cross;
+    const uint32_t kc = cr < m ? cr : m;
+    for (uint32_t i = tid; i < kc; i += 256) {
+      const uint32_t sl = (qlh + i) & QP_M, sr = (qrh + i) & QP_M;
+      const uint32_t xl = q.lp[sl], xr = q.rp[sr];
+      K[xl] = q.rk[sr];
+      K[xr] = q.lk[sl];
+      T[xl] = q.rt[sr];
+      T[xr] = q.lt[sl];
+    }
+    if (kc) lastR = q.rp[(qrh + kc - 1) & QP_M];
+    if (cr < m) {
+      const uint32_t cl = q.lp[(qlh + kc) & QP_M];
+      cut = qrh + kc ? (cl < lastR ? cl : lastR) : cl;
+      break;
+    }
+    qlh += kc;
+    qrh += kc;
+    __syncthreads();  // the popped slots are read before the next appends
+  }
+  __syncthreads();
+  return cut;
+}
+
 // Depth-exhausted segments of at least HEAP_BLOCK_MIN members found by phase
 // A, heap-sorted afterwards by k_heap_segments (one block each, its LDS holding
 // the heap's top levels)
@@ -1179,9 +1376,10 @@ __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tie
                                                            uint32_t *pl, uint32_t *pr,
                                                            uint8_t *bnd, uint32_t *heapq_n,
                                                            HeapSeg *heapq, uint32_t *claim,
-                                                           uint32_t big) {
+                                                           uint32_t big, bool qpart) {
   __shared__ Frame stack[SPLIT_STACK];
   __shared__ uint32_t s_w[16];
+  __shared__ QPart qp;
   const uint32_t tid = threadIdx.x;
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
@@ -1238,7 +1436,8 @@ __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tie
           break;
         }
         --d;
-        const uint32_t cut = block_partition(K, T, pl + b, pr + b, f, l, s_w);
+        const uint32_t cut = qpart ? block_partition_q(K, T, f, l, qp)
+                                   : block_partition(K, T, pl + b, pr + b, f, l, s_w);
         if (tid == 0) stack[sp] = {cut, l, d};
         ++sp;
         l = cut;
@@ -2471,10 +2670,14 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
     const int v = e ? atoi(e) : 0;
     return v > 0 && v <= 65536 ? (uint32_t)v : 0u;
   }();
+  static const bool split_q = [] {
+    const char *e = getenv("RK_SPLIT_Q");
+    return !(e && e[0] == '0');
+  }();
   kt_begin(st, KID_SORT_GLOBAL);
   k_sort_groups_split<<<split_grid, 256, split_pad, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
                                             heapq_n, heapq, split_dyn ? heapq_n + 1 : nullptr,
-                                            split_big);
+                                            split_big, split_q);
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
   // the heap segments (libstdc++'s depth-limit fallback on 2048+ members: a

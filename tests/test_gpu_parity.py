@@ -467,13 +467,15 @@ print(h.hexdigest(), r.n_groups, ctx.stats()["sweep_repeats"])
 
 
 @pytest.mark.parametrize("env", ["RK_SPLIT_DYN=0", "RK_SPLIT_BIG=4096", "RK_SEG_WAVES=64",
-                                 "RK_LONG_GRID=16", "RK_GS_WAVES_MUL=1", "RK_SWEEP_BLIND=1"])
+                                 "RK_LONG_GRID=16", "RK_GS_WAVES_MUL=1", "RK_SWEEP_BLIND=1",
+                                 "RK_SPLIT_Q=0", "RK_SPLIT_GRID=256"])
 def test_schedule_switches_repeat_rich(gpu_ctx, env):
     """The grid and claiming switches of phase A (groups above 2048 members:
     dynamic claiming, its first pass' size), phase B's grid and the long-run
     walk's grid, on a repeat-rich set (cfg5's shape: groups of thousands of
     members, bucket runs of hundreds of entries) -- bit-identical to the
-    default schedule."""
+    default schedule; RK_SPLIT_Q=0 partitions phase A's segments through
+    stopper lists in memory instead of the block-wide queue scan."""
     f = rk.synth(400_000, 40_000_000, seed=47, family_frac=0.95, copies=(100, 600))
     r = gpu_ctx.classify(f, 40_000_000, 40_000_000)
     h = hashlib.sha256()

@@ -158,6 +158,25 @@ abenv5)  # parity + the cfg5q digests, then cfg5 with environment variants (ARGS
     done
   done
   ;;
+qpart)  # phase A's queue partition: std::sort parity + switches, the cfg5q digest, cfg5 with / without it
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v -k "std_sort or repeat_rich" --timeout 200 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  timeout -k 10 600 python3 -u -m pytest tests/test_large_configs.py -x -v -k "cfg5q_oracle_digest and not sharded" --timeout 500 --timeout-method thread > $O/cfg5q.log 2>&1 || exit 2
+  for rep in 1 2; do
+    for E in RK_SPLIT_Q=1 RK_SPLIT_Q=0; do
+      env $E timeout -k 10 300 python3 bench.py --config cfg5 --no-cpu --steps 2 --warmup 1 > $O/${E}_$rep.json 2> $O/${E}_$rep.err || exit 3
+    done
+  done
+  ;;
+qvar)  # phase A's queue partition: parity of the working tree, then cfg5 against library variants (ARGS: dirs with a librepkiller_amd.so)
+  timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v -k "std_sort or repeat_rich" --timeout 200 --timeout-method thread > $O/parity.log 2>&1 || exit 1
+  timeout -k 10 600 python3 -u -m pytest tests/test_large_configs.py -x -v -k "cfg5q_oracle_digest and not sharded" --timeout 500 --timeout-method thread > $O/cfg5q.log 2>&1 || exit 2
+  for rep in 1 2; do
+    for D in repkiller_amd "$@"; do
+      n=$(basename $D)
+      RK_LIB=$D/librepkiller_amd.so timeout -k 10 300 python3 bench.py --config cfg5 --no-cpu --steps 2 --warmup 1 > $O/${n}_$rep.json 2> $O/${n}_$rep.err || exit 3
+    done
+  done
+  ;;
 env5)  # cfg5 with environment variants (ARGS: "VAR=a" "VAR=b" ...) interleaved, two rounds, no parity
   for rep in 1 2; do
     i=0
