@@ -1178,7 +1178,7 @@ __device__ uint32_t block_partition(uint64_t *K, uint32_t *T, uint32_t *PL, uint
 // (right), which cross either way, and the cut is min(QL[Kc], R[Kc-1]) --
 // where libstdc++'s left cursor stops on the modified array.
 #ifndef RK_QP_PER
-#define RK_QP_PER 2
+#define RK_QP_PER 1
 #endif
 constexpr int QP_PER = RK_QP_PER;        // positions per thread in a scanned chunk
 constexpr uint32_t QP_C = 256 * QP_PER;  // a chunk (and the pairs per round at most)
@@ -1370,16 +1370,19 @@ constexpr uint32_t HEAPQ_CAP = 512;
 // share of ~18 groups per block left the launch waiting on its heaviest
 // blocks).  big = 0: one dynamic pass in list order; claim null: the static
 // round-robin.
+template <bool qpart>
 __global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tier,
                                                            const uint32_t *goff, uint64_t *key,
                                                            uint32_t *tag, uint32_t *otag,
                                                            uint32_t *pl, uint32_t *pr,
                                                            uint8_t *bnd, uint32_t *heapq_n,
                                                            HeapSeg *heapq, uint32_t *claim,
-                                                           uint32_t big, bool qpart) {
+                                                           uint32_t big) {
   __shared__ Frame stack[SPLIT_STACK];
   __shared__ uint32_t s_w[16];
-  __shared__ QPart qp;
+  // the queues in dynamic LDS: reserved only when the queue partition runs
+  extern __shared__ __attribute__((aligned(16))) uint8_t split_lds[];
+  QPart &qp = *reinterpret_cast<QPart *>(split_lds);
   const uint32_t tid = threadIdx.x;
   uint32_t lo, hi;
   tl.range(tier, lo, hi);
@@ -2668,16 +2671,19 @@ int sort_groups_exact(const uint32_t *gid_sorted, const uint32_t *goff, uint32_t
   static const uint32_t split_pad = [] {
     const char *e = getenv("RK_SPLIT_LDSPAD");
     const int v = e ? atoi(e) : 0;
-    return v > 0 && v <= 65536 ? (uint32_t)v : 0u;
+    return v > 0 && v <= 32768 ? (uint32_t)v : 0u;
   }();
   static const bool split_q = [] {
     const char *e = getenv("RK_SPLIT_Q");
     return !(e && e[0] == '0');
   }();
   kt_begin(st, KID_SORT_GLOBAL);
-  k_sort_groups_split<<<split_grid, 256, split_pad, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd,
-                                            heapq_n, heapq, split_dyn ? heapq_n + 1 : nullptr,
-                                            split_big, split_q);
+  {
+    const uint32_t lds = split_pad + (split_q ? (uint32_t)sizeof(QPart) : 0u);
+    auto kern = split_q ? k_sort_groups_split<true> : k_sort_groups_split<false>;
+    kern<<<split_grid, 256, lds, st>>>(tl, NTIER - 1, goff, key, tag, otag, pl, pr, bnd, heapq_n,
+                                       heapq, split_dyn ? heapq_n + 1 : nullptr, split_big);
+  }
   kt_end(st, KID_SORT_GLOBAL, 0.0);
   tier_slot(NTIER - 1);
   // the heap segments (libstdc++'s depth-limit fallback on 2048+ members: a

@@ -175,6 +175,7 @@ qvar)  # phase A's queue partition: parity of the working tree, then cfg5 agains
       n=$(basename $D)
       RK_LIB=$D/librepkiller_amd.so timeout -k 10 300 python3 bench.py --config cfg5 --no-cpu --steps 2 --warmup 1 > $O/${n}_$rep.json 2> $O/${n}_$rep.err || exit 3
     done
+    RK_SPLIT_Q=0 timeout -k 10 300 python3 bench.py --config cfg5 --no-cpu --steps 2 --warmup 1 > $O/listpart_$rep.json 2> $O/listpart_$rep.err || exit 4
   done
   ;;
 env5)  # cfg5 with environment variants (ARGS: "VAR=a" "VAR=b" ...) interleaved, two rounds, no parity
