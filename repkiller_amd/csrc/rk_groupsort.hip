@@ -1188,7 +1188,7 @@ struct QPart {
   uint64_t lk[QP_CAP], rk[QP_CAP];
   uint32_t lp[QP_CAP], rp[QP_CAP], lt[QP_CAP], rt[QP_CAP];
   uint32_t cnt[2][QP_PER * 4];
-  uint32_t cross;
+  uint32_t cross[2];  // by round parity (see the end of a round)
 };
 
 __device__ uint32_t block_partition_q(uint64_t *K, uint32_t *T, uint32_t f, uint32_t l,
@@ -1263,6 +1263,7 @@ __device__ uint32_t block_partition_q(uint64_t *K, uint32_t *T, uint32_t f, uint
     if (y == f) bk[u] = p, bt[u] = tm;
   }
   bool first = true;
+  uint32_t par = 0;
   uint32_t cut = 0;
   for (;;) {
     const bool addl = qlt - qlh < QP_C && lpos < l;
@@ -1284,7 +1285,7 @@ __device__ uint32_t block_partition_q(uint64_t *K, uint32_t *T, uint32_t f, uint
       br[u] = __ballot(okr && !(p < bk[u]));
       if (lane == 0) q.cnt[0][u * 4 + wv] = __popcll(bl[u]), q.cnt[1][u * 4 + wv] = __popcll(br[u]);
     }
-    if (tid == 0) q.cross = 0xFFFFFFFFu;
+    if (tid == 0) q.cross[par] = 0xFFFFFFFFu;
     __syncthreads();
     if (first && tid == 0) {  // the median's swap (every candidate read by now)
       K[f] = p;
@@ -1330,9 +1331,9 @@ __device__ uint32_t block_partition_q(uint64_t *K, uint32_t *T, uint32_t f, uint
     uint32_t m = qlt - qlh < qrt - qrh ? qlt - qlh : qrt - qrh;
     if (m > QP_C) m = QP_C;
     for (uint32_t i = tid; i < m; i += 256)
-      if (q.lp[(qlh + i) & QP_M] >= q.rp[(qrh + i) & QP_M]) atomicMin(&q.cross, i);
+      if (q.lp[(qlh + i) & QP_M] >= q.rp[(qrh + i) & QP_M]) atomicMin(&q.cross[par], i);
     __syncthreads();
-    const uint32_t cr = q.cross;
+    const uint32_t cr = q.cross[par];
     const uint32_t kc = cr < m ? cr : m;
     for (uint32_t i = tid; i < kc; i += 256) {
       const uint32_t sl = (qlh + i) & QP_M, sr = (qrh + i) & QP_M;
@@ -1350,7 +1351,11 @@ __device__ uint32_t block_partition_q(uint64_t *K, uint32_t *T, uint32_t f, uint
     }
     qlh += kc;
     qrh += kc;
-    __syncthreads();  // the popped slots are read before the next appends
+    // no barrier here: the next round's appends (the only writes to the
+    // queues' slots) follow its first barrier, which every wavefront reaches
+    // only after this round's swaps; the crossing word alternates by parity,
+    // so the next round's reset cannot meet a slow wavefront's read of it
+    par ^= 1u;
   }
   __syncthreads();
   return cut;
