@@ -1375,8 +1375,19 @@ constexpr uint32_t HEAPQ_CAP = 512;
 // share of ~18 groups per block left the launch waiting on its heaviest
 // blocks).  big = 0: one dynamic pass in list order; claim null: the static
 // round-robin.
+// 8 wavefronts per SIMD (the queue partition's 53 VGPRs, 8 blocks of 17 KB of
+// LDS per CU; the SGPRs above 96 spill to VGPR lanes) instead of the 7 its
+// SGPRs allowed.  RK_SPLIT_WPE=0: the compiler's choice
+#ifndef RK_SPLIT_WPE
+#define RK_SPLIT_WPE 8
+#endif
+#if RK_SPLIT_WPE
+#define RK_SPLIT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RK_SPLIT_WPE)))
+#else
+#define RK_SPLIT_WPE_ATTR
+#endif
 template <bool qpart>
-__global__ void __launch_bounds__(256) k_sort_groups_split(TierLists tl, int tier,
+__global__ void __launch_bounds__(256) RK_SPLIT_WPE_ATTR k_sort_groups_split(TierLists tl, int tier,
                                                            const uint32_t *goff, uint64_t *key,
                                                            uint32_t *tag, uint32_t *otag,
                                                            uint32_t *pl, uint32_t *pr,
