@@ -30,7 +30,7 @@ JOBS = [
     ("k_sort_small", "groups of 2..16 members (insertion sort == stable rank): 16 lanes per group from the tier list, width-16 shuffles; singletons are not touched (second stream)", "12 per member"),
     ("k_sort_groups_reg", "17..64 members in registers (17..32: two groups per wavefront, second stream; 33..64: main stream, after its LDS tiers)", "12 per member"),
     ("k_sort_groups_lds", "65..2048 members in LDS: partitions down to the leaves (a segment of <= 64 partitioned in registers: read once, stoppers by ballots, partners by lane permutes, written once), then the final insertion pass with ballot-found leaf bounds (257..2048: second stream, first)", "12 per member"),
-    ("k_sort_groups_split", "groups above 2048: block-wide partitions down to 512-member segments", "12 per member"),
+    ("k_sort_groups_split", "groups above 2048: partitions down to 512-member segments, each a block-wide Hoare scan (both cursors a chunk at a time into LDS stopper queues, pairs swapped from the queues), groups claimed largest first", "12 per member"),
     ("k_sort_segments", "those segments, one LDS wavefront each", "12 per member"),
     ("k_heap_segments", "depth-exhausted segments of >= 2048 members (median-of-3 killers only): make_heap level-parallel; sort_heap by one wavefront: all-equal keys (the killer) as a spine FIFO, else top 13 heap levels in LDS", "-"),
     ("k_emit", "gid, flag, output order", "29"),
